@@ -1,0 +1,188 @@
+#!/usr/bin/env python3
+"""Benchmark: GiB/s reduced by shmem_double_sum_to_all, device-resident, 256 MiB per PE.
+
+Contract (driver): `python bench.py --gpus N --steps K --warmup W`; for N > 1
+it runs under torch.distributed.run, one process (= one PE = one GPU) per
+rank, identity from RANK/WORLD_SIZE/LOCAL_RANK. A step is one
+shmem_double_sum_to_all call over the whole active set on 256 MiB per PE,
+source and target in the device symmetric heap (inputs resident in HBM when
+the timed region starts). K steps are bracketed by shmem_barrier_all + a
+device synchronize on both sides; the time is the max over PEs.
+
+value = N * 256 MiB / t_step / 2^30 (whole job); per-PE S/t_step is also
+printed. roofline: the dominant kernel's algorithmic bytes per launch / its
+average duration from HIP events recorded by the library on its own stream.
+cpu_baseline: the reference algorithm restated in C (oracle/liboracle.so),
+1 PE on 1 host core, timed on a bounded sample before the GPU is touched.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "osss-gasnet_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import shmem_reduce  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
+XGMI_LINK_GBS = 153.0      # per link, 7 links per GPU
+GIB = float(1 << 30)
+
+
+def synth(pe, idx):
+    """Deterministic full-mantissa doubles: value of element idx on PE pe
+    (splitmix64 of (pe, idx)); random access, so any PE can recompute any
+    other PE's samples for the correctness check."""
+    z = (np.uint64(pe) << np.uint64(40)) + idx.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+    z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+    z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+    z = z ^ (z >> np.uint64(31))
+    mant = (z >> np.uint64(11)).astype(np.float64) * 2.0**-53          # [0,1) full 53 bits
+    k = (z & np.uint64(7)).astype(np.float64)
+    return (mant - 0.5) * np.exp2(k)
+
+
+def cpu_baseline(n, budget_s):
+    """The reference algorithm (oracle restatement) at 1 PE on 1 core: median
+    seconds per call over as many calls as fit in ~budget_s."""
+    import oracle
+    t1 = oracle.cpu_baseline_double_sum(1, n, 0, 1)
+    reps = int(max(3, min(200, budget_s / max(t1, 1e-6))))
+    t = oracle.cpu_baseline_double_sum(1, n, 1, reps)
+    return t, reps
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--mib", type=int, default=256, help="MiB per PE")
+    ap.add_argument("--algorithm", default=os.environ.get("SHMEM_REDUCE_ALGORITHM", "auto"))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    S = args.mib << 20
+    n = S // 8
+
+    # CPU baseline first, before this process initialises the GPU
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        t, reps = cpu_baseline(n, args.cpu_seconds)
+        cpu = {"value": round(S / t / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+               "sample": f"{reps} calls of the reference algorithm (restated in C, oracle/reduce_oracle.c) "
+                         f"at 1 PE on {args.mib} MiB double, median per call {t * 1e3:.1f} ms"}
+
+    os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(2 * S + (64 << 20)))
+    os.environ.setdefault("SHMEM_DEVICE_SCRATCH_SIZE", str(96 << 20))
+    shm = shmem_reduce.Shmem()
+    shm.init()
+    shm.set_algorithm(args.algorithm)
+    me, npes = shm.my_pe(), shm.n_pes()
+    src = shm.malloc_device(S)
+    dst = shm.malloc_device(S)
+    shm.put(src, synth(me, np.arange(n, dtype=np.uint64)))
+
+    def step():
+        shm.to_all("sum", "double", dst, src, n, 0, 0, npes)
+
+    for _ in range(args.warmup):
+        step()
+    shm.barrier_all()
+    shm.sync()
+    shm.kernel_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    shm.sync()
+    t_local = time.perf_counter() - t0
+    shm.barrier_all()
+    nk, k_total_ms, k_avg_ms = shm.kernel_timing_stats()
+    shm.kernel_timing(False)
+
+    # max over PEs, through the library's own host-staged double max reduction
+    tbuf = np.array([t_local], dtype=np.float64)
+    tout = np.zeros(1, dtype=np.float64)
+    shm.to_all("max", "double", tout.ctypes.data, tbuf.ctypes.data, 1, 0, 0, npes)
+    t_max = float(tout[0])
+    t_step = t_max / args.steps
+
+    # correctness of the last result on a sample: the P2P schedule's result is
+    # the reference's result on PE_start (own-first = ascending order)
+    check = "skipped"
+    if not args.no_check:
+        idx = np.unique(np.random.default_rng(me).integers(0, n, 1 << 16).astype(np.uint64))
+        got_full = shm.get(dst, n, "double")
+        got = got_full[idx.astype(np.int64)]
+        import oracle
+        srcs = [synth(p, idx) for p in range(npes)]
+        want = oracle.reduce_pe("sum", "double", srcs, 0)
+        bad = int((got.view(np.uint64) != want.view(np.uint64)).sum())
+        check = "bit-exact vs reference order (PE_start), %d samples" % len(idx) if bad == 0 else \
+            "MISMATCH %d of %d samples" % (bad, len(idx))
+        del got_full
+
+    # dominant kernel and its algorithmic bytes per launch
+    if npes == 1:
+        kname = "copy_segments<8> (identity fold, PE_size=1)"
+        alg_bytes = 2 * S
+    else:
+        kname = f"combine_vec<sum,double,{npes}> (reduce-scatter leg, {npes - 1} sources over xGMI)"
+        shard = S // npes
+        alg_bytes = (npes + 1) * shard
+    achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
+    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                "kernel": kname, "alg_bytes_per_launch": alg_bytes, "kernel_avg_us": round(k_avg_ms * 1e3, 2),
+                "launches_timed": nk}
+    traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(traffic_file):
+        try:
+            tr = json.load(open(traffic_file)).get(f"n{npes}_{args.mib}mib")
+            if tr:
+                roofline["traffic"] = tr["hbm_bytes_per_launch"]
+                roofline["traffic_source"] = tr["source"]
+        except (ValueError, KeyError):
+            pass
+
+    if me == 0:
+        out = {
+            "metric": "GiB/s reduced (device-resident), shmem_double_sum_to_all @256MiB, 1/2/4/8 GPU",
+            "value": round(npes * S / t_step / GIB, 2),
+            "unit": "GiB/s",
+            "n_gpus": npes,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(t_step * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (splitmix64 full-mantissa doubles, device-resident symmetric heap)",
+            "config": {"workload": f"shmem_double_sum_to_all, {npes} PE = {npes} GPU, {args.mib} MiB "
+                                   f"device-resident array per PE", "nreduce": n, "bytes_per_pe": S,
+                       "algorithm": args.algorithm, "parallelism": f"pe{npes}"},
+            "per_pe_gib_s": round(S / t_step / GIB, 2),
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "check": check,
+        }
+        print(json.dumps(out), flush=True)
+    shm.free_device(dst)
+    shm.free_device(src)
+    shm.finalize()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,84 @@
+/*
+ * mi355_reduce.h -- C ABI of the HIP combine layer (gfx950).
+ *
+ * This is the thin layer the host C runtime drives. It replaces the scalar
+ * combine loops of the reference schedule:
+ *   - the element functions    src/reduce/reduce-op.c:79-158
+ *     (sum/prod, and/or/xor, min/max; called through `the_op`)
+ *   - the per-PE combine loops src/reduce/reduce-op.c:241-261
+ *     (`write_to[ti] = (*the_op)(write_to[ti], pWrk[j])`)
+ *   - the initial copy         src/reduce/reduce-op.c:226-229
+ * with streaming HIP kernels. Plain pointers and sizes only; `stream` is a
+ * hipStream_t passed as void* (NULL = the null stream).
+ *
+ * Every function is asynchronous on `stream` and returns 0 on success, a
+ * negative MI355_E* code for a rejected argument, or a positive hipError_t
+ * from the launch.
+ */
+#ifndef MI355_REDUCE_H
+#define MI355_REDUCE_H 1
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* reduce-op.c:79-158 operator families */
+enum mi355_op {
+    MI355_OP_SUM = 0,
+    MI355_OP_PROD = 1,
+    MI355_OP_AND = 2,
+    MI355_OP_OR = 3,
+    MI355_OP_XOR = 4,
+    MI355_OP_MIN = 5,
+    MI355_OP_MAX = 6,
+    MI355_NUM_OPS = 7
+};
+
+/* reduce-op.c:278-286 element types (LP64 host ABI layouts) */
+enum mi355_dtype {
+    MI355_SHORT = 0,      /* int16                                        */
+    MI355_INT = 1,        /* int32                                        */
+    MI355_LONG = 2,       /* int64                                        */
+    MI355_LONGLONG = 3,   /* int64                                        */
+    MI355_FLOAT = 4,      /* binary32                                     */
+    MI355_DOUBLE = 5,     /* binary64                                     */
+    MI355_LONGDOUBLE = 6, /* x87 80-bit extended in a 16-byte slot        */
+    MI355_COMPLEXF = 7,   /* {float re, im}                               */
+    MI355_COMPLEXD = 8,   /* {double re, im}                              */
+    MI355_NUM_DTYPES = 9
+};
+
+#define MI355_E_INVAL  (-1)   /* bad op/dtype/pointer/count        */
+#define MI355_E_UNSUP  (-2)   /* op not defined for dtype          */
+
+/* Bytes per element of a dtype (0 for an unknown dtype). */
+size_t mi355_dtype_size (int dtype);
+
+/* 1 if (op, dtype) is one of the 44 reference reductions. */
+int mi355_op_supported (int op, int dtype);
+
+/* dst[i] = (((srcs[0][i] op srcs[1][i]) op srcs[2][i]) ... op srcs[nsrc-1][i])
+ * for i < n: a left fold with the accumulator on the left, exactly the
+ * operand order of reduce-op.c:247-248. Sources may be peer (xGMI) pointers.
+ * dst may alias srcs[0] exactly; other overlaps are undefined. nsrc >= 1
+ * (nsrc == 1 is a copy). */
+int mi355_combine (int op, int dtype, void *dst, const void *const *srcs,
+                   int nsrc, size_t n, void *stream);
+
+/* nseg independent byte copies dsts[i] <- srcs[i] of nbytes[i] bytes in ONE
+ * launch (the all-gather leg of the shard schedule). nseg <= 64. */
+int mi355_copy_segments (void *const *dsts, const void *const *srcs,
+                         const size_t *nbytes, int nseg, void *stream);
+
+/* Shard i of nshards for n elements of elem_size bytes: the P2P schedule's
+ * partition (contiguous, shard starts 256-byte aligned, trailing shards may
+ * be empty). Host-only arithmetic, callable without a GPU. */
+void mi355_shard_bounds (size_t n, size_t elem_size, int nshards, int i, size_t *lo, size_t *hi);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MI355_REDUCE_H */

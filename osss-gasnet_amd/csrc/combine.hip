@@ -1,0 +1,467 @@
+// combine.hip -- element-wise combine kernels for the *_to_all reductions (gfx950).
+//
+// Replaces the scalar, indirect-call combine loops of the reference schedule
+// (src/reduce/reduce-op.c:241-261, element functions :79-158) with streaming
+// HIP kernels. The work is bandwidth-bound vector arithmetic: every output
+// element costs NSRC loads and one store and a handful of VALU ops, so the
+// design target is the HBM (or xGMI) roofline, not MFMA:
+//   * 16-byte loads/stores per lane (1 KiB per wave instruction),
+//   * UNROLL independent 16-byte vectors per lane x NSRC sources issued
+//     before the first use, so each lane keeps NSRC*UNROLL loads in flight,
+//   * grid-stride over a grid capped at a few blocks per CU (256 CUs),
+//   * no LDS: nothing is re-used, staging through LDS would only add traffic.
+//
+// Numerics follow the reference operators exactly (compiled with
+// -ffp-contract=off so no a*b+c is fused):
+//   sum/prod      a + b, a * b (integers wrap two's-complement, like gcc's
+//                 code for reduce-op.c:79-101; short promotes to int and
+//                 truncates)
+//   and/or/xor    bitwise (reduce-op.c:108-131)
+//   min/max       a < b ? a : b / a > b ? a : b  -- a select, NOT v_min/v_max,
+//                 so NaN and signed-zero cases pick the same operand as the
+//                 reference (reduce-op.c:138-158)
+//   complex prod  the C99 Annex G algorithm of libgcc __muldc3/__mulsc3, which
+//                 is what gcc emits for `a * b` on double/float complex
+//   long double   x87 80-bit extended arithmetic in software (x80.h)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <type_traits>
+
+#include "mi355_reduce.h"
+#include "x80.h"
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kMaxSrc = 8;
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct cplxf { float re, im; };
+struct cplxd { double re, im; };
+
+// ---------------------------------------------------------------------------
+// element operators (reduce-op.c:79-158)
+// ---------------------------------------------------------------------------
+template <typename T> struct IsInt : std::is_integral<T> {};
+
+template <int OP, typename T>
+__device__ __forceinline__ T int_op(T a, T b) {
+    // 32-bit unsigned arithmetic for short/int, 64-bit for long/long long:
+    // defined wrap-around, identical bits to gcc's add/imul on the host.
+    using W = typename std::conditional<(sizeof(T) <= 4), uint32_t, uint64_t>::type;
+    if constexpr (OP == MI355_OP_SUM) return (T)((W)a + (W)b);
+    else if constexpr (OP == MI355_OP_PROD) return (T)((W)a * (W)b);
+    else if constexpr (OP == MI355_OP_AND) return (T)(a & b);
+    else if constexpr (OP == MI355_OP_OR) return (T)(a | b);
+    else if constexpr (OP == MI355_OP_XOR) return (T)(a ^ b);
+    else if constexpr (OP == MI355_OP_MIN) return a < b ? a : b;
+    else return a > b ? a : b;
+}
+
+template <int OP, typename T>
+__device__ __forceinline__ T fp_op(T a, T b) {
+    if constexpr (OP == MI355_OP_SUM) return a + b;
+    else if constexpr (OP == MI355_OP_PROD) return a * b;
+    else if constexpr (OP == MI355_OP_MIN) return a < b ? a : b;
+    else return a > b ? a : b;
+}
+
+// libgcc __muldc3/__mulsc3 (C99 Annex G.5.1): plain products, then recovery
+// of infinities when both parts came out NaN.
+template <typename R>
+__device__ __forceinline__ void cmul(R a, R b, R c, R d, R &x, R &y) {
+    R ac = a * c, bd = b * d, ad = a * d, bc = b * c;
+    x = ac - bd;
+    y = ad + bc;
+    if (__builtin_isnan(x) && __builtin_isnan(y)) {
+        bool recalc = false;
+        const R inf = __builtin_inf();
+        if (__builtin_isinf(a) || __builtin_isinf(b)) {
+            a = __builtin_copysign(__builtin_isinf(a) ? R(1) : R(0), a);
+            b = __builtin_copysign(__builtin_isinf(b) ? R(1) : R(0), b);
+            if (__builtin_isnan(c)) c = __builtin_copysign(R(0), c);
+            if (__builtin_isnan(d)) d = __builtin_copysign(R(0), d);
+            recalc = true;
+        }
+        if (__builtin_isinf(c) || __builtin_isinf(d)) {
+            c = __builtin_copysign(__builtin_isinf(c) ? R(1) : R(0), c);
+            d = __builtin_copysign(__builtin_isinf(d) ? R(1) : R(0), d);
+            if (__builtin_isnan(a)) a = __builtin_copysign(R(0), a);
+            if (__builtin_isnan(b)) b = __builtin_copysign(R(0), b);
+            recalc = true;
+        }
+        if (!recalc && (__builtin_isinf(ac) || __builtin_isinf(bd) ||
+                        __builtin_isinf(ad) || __builtin_isinf(bc))) {
+            if (__builtin_isnan(a)) a = __builtin_copysign(R(0), a);
+            if (__builtin_isnan(b)) b = __builtin_copysign(R(0), b);
+            if (__builtin_isnan(c)) c = __builtin_copysign(R(0), c);
+            if (__builtin_isnan(d)) d = __builtin_copysign(R(0), d);
+            recalc = true;
+        }
+        if (recalc) {
+            x = inf * (a * c - b * d);
+            y = inf * (a * d + b * c);
+        }
+    }
+}
+
+template <int OP, typename C>
+__device__ __forceinline__ C cplx_op(C a, C b) {
+    C r;
+    if constexpr (OP == MI355_OP_SUM) {
+        r.re = a.re + b.re;
+        r.im = a.im + b.im;
+    } else {
+        cmul(a.re, a.im, b.re, b.im, r.re, r.im);
+    }
+    return r;
+}
+
+template <int OP, typename T>
+__device__ __forceinline__ T apply(T a, T b) {
+    if constexpr (std::is_same<T, cplxf>::value || std::is_same<T, cplxd>::value)
+        return cplx_op<OP>(a, b);
+    else if constexpr (std::is_same<T, x80>::value)
+        return x80_op<OP>(a, b);
+    else if constexpr (std::is_floating_point<T>::value)
+        return fp_op<OP>(a, b);
+    else
+        return int_op<OP>(a, b);
+}
+
+// Which (op, type) pairs exist: reduce-op.c:405-448.
+template <int OP, typename T>
+constexpr bool valid_pair() {
+    constexpr bool is_int = std::is_integral<T>::value;
+    constexpr bool is_real = std::is_floating_point<T>::value || std::is_same<T, x80>::value;
+    constexpr bool is_cplx = std::is_same<T, cplxf>::value || std::is_same<T, cplxd>::value;
+    if (OP == MI355_OP_SUM || OP == MI355_OP_PROD) return is_int || is_real || is_cplx;
+    if (OP == MI355_OP_AND || OP == MI355_OP_OR || OP == MI355_OP_XOR) return is_int;
+    return is_int || is_real;  // min/max
+}
+
+// ---------------------------------------------------------------------------
+// kernels
+// ---------------------------------------------------------------------------
+struct CombineParams {
+    void *dst;
+    const void *src[kMaxSrc];
+    uint64_t nvec;   // vector kernel: whole 16-byte vectors; scalar kernel: elements
+    uint32_t tail;   // vector kernel: elements after nvec*V (< V)
+};
+
+template <typename T>
+union Pack {
+    u32x4 v;
+    T e[16 / sizeof(T)];
+};
+
+__device__ __forceinline__ u32x4 ld16(const u32x4 *p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void st16(u32x4 *p, u32x4 v) { __builtin_nontemporal_store(v, p); }
+
+// Vector path: every pointer 16-byte aligned. Each lane owns UNROLL vectors
+// spaced one block apart (so a wave touches contiguous 1 KiB per source per
+// step) and issues all NSRC*UNROLL loads before combining.
+template <int OP, typename T, int NSRC, int UNROLL>
+__global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
+    constexpr int V = 16 / sizeof(T);
+    const u32x4 *s[NSRC];
+#pragma unroll
+    for (int k = 0; k < NSRC; ++k) s[k] = (const u32x4 *)p.src[k];
+    u32x4 *d = (u32x4 *)p.dst;
+    const uint64_t nvec = p.nvec;
+    const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
+    for (uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x; base < nvec;
+         base += step) {
+        Pack<T> x[UNROLL][NSRC];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = base + (uint64_t)u * kBlock;
+            if (i < nvec) {
+#pragma unroll
+                for (int k = 0; k < NSRC; ++k) x[u][k].v = ld16(s[k] + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = base + (uint64_t)u * kBlock;
+            if (i < nvec) {
+                Pack<T> acc = x[u][0];
+#pragma unroll
+                for (int k = 1; k < NSRC; ++k) {
+#pragma unroll
+                    for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[u][k].e[e]);
+                }
+                st16(d + i, acc.v);
+            }
+        }
+    }
+    if (V > 1 && p.tail != 0 && blockIdx.x == 0 && threadIdx.x < p.tail) {
+        const uint64_t i = nvec * V + threadIdx.x;
+        T acc = ((const T *)p.src[0])[i];
+#pragma unroll
+        for (int k = 1; k < NSRC; ++k) acc = apply<OP>(acc, ((const T *)p.src[k])[i]);
+        ((T *)p.dst)[i] = acc;
+    }
+}
+
+// Scalar path for pointers that are not 16-byte aligned (user offsets into
+// arrays). Coalesced element loads, grid-stride.
+template <int OP, typename T, int NSRC>
+__global__ __launch_bounds__(kBlock) void combine_scalar(CombineParams p) {
+    const T *s[NSRC];
+#pragma unroll
+    for (int k = 0; k < NSRC; ++k) s[k] = (const T *)p.src[k];
+    T *d = (T *)p.dst;
+    const uint64_t n = p.nvec;
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
+         i += (uint64_t)gridDim.x * kBlock) {
+        T v[NSRC];
+#pragma unroll
+        for (int k = 0; k < NSRC; ++k) v[k] = s[k][i];
+        T acc = v[0];
+#pragma unroll
+        for (int k = 1; k < NSRC; ++k) acc = apply<OP>(acc, v[k]);
+        d[i] = acc;
+    }
+}
+
+// Byte copy of up to kMaxSeg segments in one launch; blockIdx.y = segment.
+constexpr int kMaxSeg = 64;
+struct SegParams {
+    void *dst[kMaxSeg];
+    const void *src[kMaxSeg];
+    uint64_t nbytes[kMaxSeg];
+};
+
+template <int UNROLL>
+__global__ __launch_bounds__(kBlock) void copy_segments(SegParams p) {
+    const int sg = blockIdx.y;
+    const uint64_t nb = p.nbytes[sg];
+    const char *src = (const char *)p.src[sg];
+    char *dst = (char *)p.dst[sg];
+    if (nb == 0) return;
+    const bool aligned = ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0;
+    uint64_t done = 0;
+    if (aligned) {
+        const u32x4 *s = (const u32x4 *)src;
+        u32x4 *d = (u32x4 *)dst;
+        const uint64_t nvec = nb / 16;
+        const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
+        for (uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x; base < nvec;
+             base += step) {
+            u32x4 x[UNROLL];
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                const uint64_t i = base + (uint64_t)u * kBlock;
+                if (i < nvec) x[u] = ld16(s + i);
+            }
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) {
+                const uint64_t i = base + (uint64_t)u * kBlock;
+                if (i < nvec) st16(d + i, x[u]);
+            }
+        }
+        done = nvec * 16;
+    }
+    for (uint64_t i = done + (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nb;
+         i += (uint64_t)gridDim.x * kBlock)
+        dst[i] = src[i];
+}
+
+// ---------------------------------------------------------------------------
+// launch helpers
+// ---------------------------------------------------------------------------
+int g_cus[64];
+
+int device_cus() {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    if (g_cus[dev] == 0) {
+        int cus = 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            cus <= 0)
+            cus = 256;
+        g_cus[dev] = cus;
+    }
+    return g_cus[dev];
+}
+
+// Blocks for a streaming launch: enough to cover the work once, capped at
+// kBlocksPerCU resident blocks per CU (grid-stride covers the rest).
+constexpr int kBlocksPerCU = 8;
+
+unsigned grid_for(uint64_t units_per_block_pass, uint64_t units) {
+    uint64_t want = (units + units_per_block_pass - 1) / units_per_block_pass;
+    uint64_t cap = (uint64_t)device_cus() * kBlocksPerCU;
+    if (want < 1) want = 1;
+    return (unsigned)(want < cap ? want : cap);
+}
+
+// Loads in flight per lane ~ 8 x 16 B whatever NSRC is.
+template <int NSRC>
+constexpr int unroll_for() {
+    return NSRC == 1 ? 8 : NSRC == 2 ? 4 : NSRC <= 4 ? 2 : 1;
+}
+
+template <int OP, typename T, int NSRC>
+int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st) {
+    CombineParams p{};
+    p.dst = dst;
+    uintptr_t orbits = (uintptr_t)dst;
+    for (int k = 0; k < NSRC; ++k) {
+        p.src[k] = srcs[k];
+        orbits |= (uintptr_t)srcs[k];
+    }
+    constexpr int V = 16 / sizeof(T);
+    if ((orbits & 15) == 0) {
+        constexpr int U = unroll_for<NSRC>();
+        p.nvec = n / V;
+        p.tail = (uint32_t)(n % V);
+        const unsigned grid = grid_for((uint64_t)kBlock * U, p.nvec);
+        hipLaunchKernelGGL((combine_vec<OP, T, NSRC, U>), dim3(grid), dim3(kBlock), 0, st, p);
+    } else {
+        p.nvec = n;
+        p.tail = 0;
+        const unsigned grid = grid_for((uint64_t)kBlock * 4, n);
+        hipLaunchKernelGGL((combine_scalar<OP, T, NSRC>), dim3(grid), dim3(kBlock), 0, st, p);
+    }
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+template <int OP, typename T>
+int launch_n(int nsrc, void *dst, const void *const *srcs, size_t n, hipStream_t st) {
+    switch (nsrc) {
+    case 1: return launch_fixed<OP, T, 1>(dst, srcs, n, st);
+    case 2: return launch_fixed<OP, T, 2>(dst, srcs, n, st);
+    case 3: return launch_fixed<OP, T, 3>(dst, srcs, n, st);
+    case 4: return launch_fixed<OP, T, 4>(dst, srcs, n, st);
+    case 5: return launch_fixed<OP, T, 5>(dst, srcs, n, st);
+    case 6: return launch_fixed<OP, T, 6>(dst, srcs, n, st);
+    case 7: return launch_fixed<OP, T, 7>(dst, srcs, n, st);
+    case 8: return launch_fixed<OP, T, 8>(dst, srcs, n, st);
+    default: return MI355_E_INVAL;
+    }
+}
+
+// Left fold of any number of sources: first kMaxSrc into dst, then dst
+// stays the accumulator (first operand) of every following launch.
+template <int OP, typename T>
+int launch_fold(void *dst, const void *const *srcs, int nsrc, size_t n, hipStream_t st) {
+    if constexpr (!valid_pair<OP, T>()) {
+        return MI355_E_UNSUP;
+    } else {
+        int first = nsrc < kMaxSrc ? nsrc : kMaxSrc;
+        int rc = launch_n<OP, T>(first, dst, srcs, n, st);
+        int done = first;
+        while (rc == 0 && done < nsrc) {
+            const void *chunk[kMaxSrc];
+            chunk[0] = dst;
+            int take = nsrc - done < kMaxSrc - 1 ? nsrc - done : kMaxSrc - 1;
+            for (int k = 0; k < take; ++k) chunk[1 + k] = srcs[done + k];
+            rc = launch_n<OP, T>(1 + take, dst, chunk, n, st);
+            done += take;
+        }
+        return rc;
+    }
+}
+
+template <typename T>
+int dispatch_op(int op, void *dst, const void *const *srcs, int nsrc, size_t n, hipStream_t st) {
+    switch (op) {
+    case MI355_OP_SUM: return launch_fold<MI355_OP_SUM, T>(dst, srcs, nsrc, n, st);
+    case MI355_OP_PROD: return launch_fold<MI355_OP_PROD, T>(dst, srcs, nsrc, n, st);
+    case MI355_OP_AND: return launch_fold<MI355_OP_AND, T>(dst, srcs, nsrc, n, st);
+    case MI355_OP_OR: return launch_fold<MI355_OP_OR, T>(dst, srcs, nsrc, n, st);
+    case MI355_OP_XOR: return launch_fold<MI355_OP_XOR, T>(dst, srcs, nsrc, n, st);
+    case MI355_OP_MIN: return launch_fold<MI355_OP_MIN, T>(dst, srcs, nsrc, n, st);
+    case MI355_OP_MAX: return launch_fold<MI355_OP_MAX, T>(dst, srcs, nsrc, n, st);
+    default: return MI355_E_INVAL;
+    }
+}
+
+}  // namespace
+
+extern "C" size_t mi355_dtype_size(int dtype) {
+    switch (dtype) {
+    case MI355_SHORT: return 2;
+    case MI355_INT: return 4;
+    case MI355_LONG:
+    case MI355_LONGLONG: return 8;
+    case MI355_FLOAT: return 4;
+    case MI355_DOUBLE: return 8;
+    case MI355_LONGDOUBLE: return 16;
+    case MI355_COMPLEXF: return 8;
+    case MI355_COMPLEXD: return 16;
+    default: return 0;
+    }
+}
+
+extern "C" int mi355_op_supported(int op, int dtype) {
+    if (op < 0 || op >= MI355_NUM_OPS || dtype < 0 || dtype >= MI355_NUM_DTYPES) return 0;
+    const bool is_int = dtype <= MI355_LONGLONG;
+    const bool is_cplx = dtype == MI355_COMPLEXF || dtype == MI355_COMPLEXD;
+    if (op == MI355_OP_SUM || op == MI355_OP_PROD) return 1;
+    if (op == MI355_OP_AND || op == MI355_OP_OR || op == MI355_OP_XOR) return is_int ? 1 : 0;
+    return is_cplx ? 0 : 1;
+}
+
+extern "C" int mi355_combine(int op, int dtype, void *dst, const void *const *srcs, int nsrc,
+                             size_t n, void *stream) {
+    if (!mi355_op_supported(op, dtype)) return MI355_E_UNSUP;
+    if (nsrc < 1 || dst == nullptr || srcs == nullptr) return MI355_E_INVAL;
+    for (int k = 0; k < nsrc; ++k)
+        if (srcs[k] == nullptr) return MI355_E_INVAL;
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    if (nsrc == 1) {
+        // a one-source fold is a copy: byte copy, independent of op/type
+        if (dst == srcs[0]) return 0;
+        void *d[1] = {dst};
+        size_t nb[1] = {n * mi355_dtype_size(dtype)};
+        return mi355_copy_segments(d, srcs, nb, 1, stream);
+    }
+    switch (dtype) {
+    case MI355_SHORT: return dispatch_op<int16_t>(op, dst, srcs, nsrc, n, st);
+    case MI355_INT: return dispatch_op<int32_t>(op, dst, srcs, nsrc, n, st);
+    case MI355_LONG:
+    case MI355_LONGLONG: return dispatch_op<int64_t>(op, dst, srcs, nsrc, n, st);
+    case MI355_FLOAT: return dispatch_op<float>(op, dst, srcs, nsrc, n, st);
+    case MI355_DOUBLE: return dispatch_op<double>(op, dst, srcs, nsrc, n, st);
+    case MI355_LONGDOUBLE: return dispatch_op<x80>(op, dst, srcs, nsrc, n, st);
+    case MI355_COMPLEXF: return dispatch_op<cplxf>(op, dst, srcs, nsrc, n, st);
+    case MI355_COMPLEXD: return dispatch_op<cplxd>(op, dst, srcs, nsrc, n, st);
+    default: return MI355_E_INVAL;
+    }
+}
+
+extern "C" int mi355_copy_segments(void *const *dsts, const void *const *srcs,
+                                   const size_t *nbytes, int nseg, void *stream) {
+    if (nseg < 0 || nseg > kMaxSeg) return MI355_E_INVAL;
+    if (nseg == 0) return 0;
+    if (dsts == nullptr || srcs == nullptr || nbytes == nullptr) return MI355_E_INVAL;
+    SegParams p{};
+    uint64_t maxv = 0;
+    int used = 0;
+    for (int k = 0; k < nseg; ++k) {
+        if (nbytes[k] == 0 || dsts[k] == srcs[k]) continue;
+        if (dsts[k] == nullptr || srcs[k] == nullptr) return MI355_E_INVAL;
+        p.dst[used] = dsts[k];
+        p.src[used] = srcs[k];
+        p.nbytes[used] = nbytes[k];
+        uint64_t v = (nbytes[k] + 15) / 16;
+        if (v > maxv) maxv = v;
+        ++used;
+    }
+    if (used == 0) return 0;
+    constexpr int U = 8;
+    unsigned gx = grid_for((uint64_t)kBlock * U, maxv);
+    // keep total blocks ~ cap when many segments share the chip
+    unsigned cap = (unsigned)device_cus() * kBlocksPerCU;
+    if ((uint64_t)gx * used > cap) gx = cap / used > 0 ? cap / used : 1;
+    hipLaunchKernelGGL((copy_segments<U>), dim3(gx, used), dim3(kBlock), 0, (hipStream_t)stream, p);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}

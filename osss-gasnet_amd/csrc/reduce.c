@@ -1,0 +1,375 @@
+/*
+ * reduce.c -- the 44 shmem_<TYPE>_<OP>_to_all collectives on MI355X.
+ *
+ * Reference: src/reduce/reduce-op.c. There, every PE copies its source into
+ * the target (:226-229), barriers (:230), then pulls every other PE's source
+ * in 64-element chunks with shmem_getmem and folds them in with one indirect
+ * call per element (:232-264), barriers again (:266) and copies back from a
+ * temporary if target and source overlapped (:267-275).
+ *
+ * Here the combine runs on the PE's GPU (combine.hip, C ABI mi355_reduce.h)
+ * and the cross-PE movement is xGMI peer access to the device symmetric heap:
+ *
+ *   P2P (default)  split the nreduce elements into PE_size contiguous shards
+ *                  (256-byte aligned); PE i folds shard i of every member's
+ *                  source, in active-set order, into its own target shard;
+ *                  barrier; PE i gathers the other shards from the members'
+ *                  targets. Every PE gets the same bits, which equal the
+ *                  reference's result on PE_start (whose fold order is the
+ *                  ascending active-set order).
+ *   EXACT          every PE folds the full arrays in ITS reference order
+ *                  (own source first, then the others ascending): bit-identical
+ *                  to the reference on every PE, at PE_size x the xGMI reads.
+ *   RCCL           ncclAllReduce for the op/type pairs RCCL has, when the
+ *                  active set is the whole job; P2P otherwise.
+ *
+ * Buffers outside the device symmetric heap (host memory from shmem_malloc,
+ * static arrays, other device memory) are staged through the heap's scratch
+ * area in chunks: copy in, reduce device-resident, copy out.
+ */
+#define _GNU_SOURCE
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mi355_reduce.h"
+#include "pshmem.h"
+#include "shmem.h"
+#include "shmemx.h"
+#include "shmemi.h"
+
+struct aset {
+    int start, stride, size, me; /* me = index of this PE in the set */
+};
+
+static int aset_pe (const struct aset *s, int i) { return s->start + i * s->stride; }
+
+static void combine_or_die (int op, int dtype, void *dst, const void *const *srcs, int nsrc, size_t n)
+{
+    shmemi_timed_begin ();
+    int rc = mi355_combine (op, dtype, dst, srcs, nsrc, n, shmemi.stream);
+    shmemi_timed_end ();
+    if (rc != 0)
+        shmemi_fatal ("combine kernel launch failed (op %d, dtype %d, %d sources, %zu elements): %d",
+                      op, dtype, nsrc, n, rc);
+}
+
+static void copy_or_die (void *const *dsts, const void *const *srcs, const size_t *nbytes, int nseg)
+{
+    for (int base = 0; base < nseg; base += 64) {
+        int k = nseg - base < 64 ? nseg - base : 64;
+        int rc = mi355_copy_segments (dsts + base, srcs + base, nbytes + base, k, shmemi.stream);
+        if (rc != 0)
+            shmemi_fatal ("copy kernel launch failed: %d", rc);
+    }
+}
+
+static void sync_stream (void) { SHMEMI_HIP (hipStreamSynchronize (shmemi.stream)); }
+
+static int ranges_overlap (size_t a, size_t b, size_t nbytes)
+{
+    return a < b + nbytes && b < a + nbytes;
+}
+
+/* Shard bounds of member i for n elements of es bytes over `size` members. */
+void mi355_shard_bounds (size_t n, size_t es, int size, int i, size_t *lo, size_t *hi)
+{
+    size_t align = es >= 256 ? 1 : 256 / es;
+    size_t chunk = (n + (size_t) size - 1) / (size_t) size;
+    chunk = (chunk + align - 1) / align * align;
+    size_t l = (size_t) i * chunk;
+    *lo = l < n ? l : n;
+    *hi = l + chunk < n ? l + chunk : n;
+}
+
+/* ---------------------------------------------------------------------- */
+/* device-resident schedules on symmetric heap offsets                     */
+/* ---------------------------------------------------------------------- */
+
+/* P2P shard schedule, dst and src disjoint or identical. */
+static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
+                       const struct aset *s)
+{
+    const void *srcs[SHMEMI_MAX_PES > 64 ? 64 : SHMEMI_MAX_PES];
+    const void **sp = srcs;
+    const void **heap_srcs = NULL;
+    if (s->size > 64) {
+        heap_srcs = (const void **) malloc (sizeof (void *) * (size_t) s->size);
+        if (heap_srcs == NULL)
+            shmemi_fatal ("out of host memory");
+        sp = heap_srcs;
+    }
+    size_t lo, hi;
+    mi355_shard_bounds (n, es, s->size, s->me, &lo, &hi);
+
+    shmemi_barrier_set (s->start, s->stride, s->size); /* every source is ready */
+    if (hi > lo) {
+        for (int i = 0; i < s->size; ++i)
+            sp[i] = shmemi_peer_ptr (aset_pe (s, i), src_off + lo * es);
+        combine_or_die (op, dtype, shmemi_peer_ptr (shmemi.mype, dst_off + lo * es), sp, s->size, hi - lo);
+        sync_stream ();
+    }
+    shmemi_barrier_set (s->start, s->stride, s->size); /* every shard is reduced */
+
+    /* gather the other members' shards from their targets */
+    void *dsts[64];
+    const void *gsrc[64];
+    size_t nb[64];
+    int k = 0;
+    for (int i = 0; i < s->size; ++i) {
+        if (i == s->me)
+            continue;
+        size_t l, h;
+        mi355_shard_bounds (n, es, s->size, i, &l, &h);
+        if (h <= l)
+            continue;
+        dsts[k] = shmemi_peer_ptr (shmemi.mype, dst_off + l * es);
+        gsrc[k] = shmemi_peer_ptr (aset_pe (s, i), dst_off + l * es);
+        nb[k] = (h - l) * es;
+        if (++k == 64) {
+            copy_or_die (dsts, gsrc, nb, k);
+            k = 0;
+        }
+    }
+    if (k > 0)
+        copy_or_die (dsts, gsrc, nb, k);
+    sync_stream ();
+    shmemi_barrier_set (s->start, s->stride, s->size); /* peers are done reading us */
+    free (heap_srcs);
+}
+
+/* EXACT: fold everything in this PE's reference order into dst; dst must
+ * not overlap any source (callers route overlaps through scratch). */
+static void exact_into (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
+                        const struct aset *s)
+{
+    const void **sp = (const void **) malloc (sizeof (void *) * (size_t) s->size);
+    if (sp == NULL)
+        shmemi_fatal ("out of host memory");
+    sp[0] = shmemi_peer_ptr (shmemi.mype, src_off);
+    int k = 1;
+    for (int i = 0; i < s->size; ++i)
+        if (i != s->me)
+            sp[k++] = shmemi_peer_ptr (aset_pe (s, i), src_off);
+    combine_or_die (op, dtype, shmemi_peer_ptr (shmemi.mype, dst_off), sp, s->size, n);
+    sync_stream ();
+    free (sp);
+    (void) es;
+}
+
+/* timed: the copy is the call's dominant kernel (the PE_size == 1 identity) */
+static void copy_local (size_t dst_off, size_t src_off, size_t nbytes, int timed)
+{
+    void *d = shmemi_peer_ptr (shmemi.mype, dst_off);
+    const void *sv = shmemi_peer_ptr (shmemi.mype, src_off);
+    size_t nb = nbytes;
+    if (timed)
+        shmemi_timed_begin ();
+    copy_or_die (&d, &sv, &nb, 1);
+    if (timed)
+        shmemi_timed_end ();
+}
+
+/* Reduce n elements at symmetric offsets. Handles aliasing like the
+ * reference's temporary target (reduce-op.c:174-215), but chunked through
+ * scratch in memmove order so any overlap is safe. */
+static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
+                              const struct aset *s)
+{
+    const size_t nbytes = n * es;
+    const int exact = shmemi.algorithm == SHMEMX_REDUCE_EXACT;
+    const int same = dst_off == src_off;
+    const int overlap = ranges_overlap (dst_off, src_off, nbytes);
+
+    if (s->size == 1) {
+        /* a one-PE fold is the identity: target = source (reduce-op.c:226-229) */
+        if (same)
+            return;
+        if (!overlap) {
+            copy_local (dst_off, src_off, nbytes, 1);
+            sync_stream ();
+            return;
+        }
+    } else if (!exact && (same || !overlap)) {
+        p2p_range (op, dtype, es, dst_off, src_off, n, s);
+        return;
+    } else if (exact && !overlap) {
+        shmemi_barrier_set (s->start, s->stride, s->size);
+        exact_into (op, dtype, es, dst_off, src_off, n, s);
+        shmemi_barrier_set (s->start, s->stride, s->size);
+        return;
+    }
+
+    /* overlapping target/source: through scratch buffer C, chunk by chunk,
+     * walking down when target lies above source (memmove order) */
+    const size_t tmp_off = shmemi.scratch_off + 2 * shmemi.scratch_chunk;
+    const size_t per = shmemi.scratch_chunk / es;
+    const size_t nchunks = (n + per - 1) / per;
+    const int down = dst_off > src_off;
+    for (size_t c = 0; c < nchunks; ++c) {
+        const size_t idx = down ? nchunks - 1 - c : c;
+        const size_t b = idx * per;
+        const size_t cn = n - b < per ? n - b : per;
+        if (s->size == 1) {
+            copy_local (tmp_off, src_off + b * es, cn * es, 0);
+        } else if (!exact) {
+            p2p_range (op, dtype, es, tmp_off, src_off + b * es, cn, s);
+        } else {
+            shmemi_barrier_set (s->start, s->stride, s->size);
+            exact_into (op, dtype, es, tmp_off, src_off + b * es, cn, s);
+            shmemi_barrier_set (s->start, s->stride, s->size);
+        }
+        copy_local (dst_off + b * es, tmp_off, cn * es, 0);
+        sync_stream ();
+        /* nobody reads our target chunk; the next chunk's first barrier orders
+         * our write before any peer reads the source bytes it may cover */
+    }
+    if (s->size > 1)
+        shmemi_barrier_set (s->start, s->stride, s->size);
+}
+
+/* ---------------------------------------------------------------------- */
+/* RCCL                                                                    */
+/* ---------------------------------------------------------------------- */
+int shmemi_rccl_allreduce (int op, int dtype, const void *src, void *dst, size_t n);
+int shmemi_rccl_supported (int op, int dtype);
+
+/* ---------------------------------------------------------------------- */
+/* entry                                                                   */
+/* ---------------------------------------------------------------------- */
+enum { PK_HOST = 0, PK_DEV_SYM = 1, PK_DEV_OTHER = 2 };
+
+static int ptr_kind (const void *p, size_t nbytes)
+{
+    if (shmemi_in_device_heap (p, nbytes))
+        return PK_DEV_SYM;
+    hipPointerAttribute_t a;
+    memset (&a, 0, sizeof a);
+    hipError_t e = hipPointerGetAttributes (&a, p);
+    (void) hipGetLastError ();
+    if (e == hipSuccess && (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged))
+        return PK_DEV_OTHER;
+    return PK_HOST;
+}
+
+static void reduce_impl (int op, int dtype, const char *fn, void *target, const void *source,
+                         int nreduce, int PE_start, int logPE_stride, int PE_size, long *pSync)
+{
+    shmemi_init_check (fn);
+    if (shmemi.heap == NULL)
+        shmemi_fatal ("%s: no GPU: this library reduces on the GPU only (SHMEM_BOOTSTRAP_ONLY set?)", fn);
+    if (logPE_stride < 0 || logPE_stride > 30 || PE_size < 1 || PE_start < 0 ||
+        PE_start + (long) (PE_size - 1) * (1L << logPE_stride) >= shmemi.npes)
+        shmemi_fatal ("%s: active set (PE_start %d, logPE_stride %d, PE_size %d) outside the %d PEs",
+                      fn, PE_start, logPE_stride, PE_size, shmemi.npes);
+    struct aset s = {PE_start, 1 << logPE_stride, PE_size, -1};
+    for (int i = 0; i < PE_size; ++i)
+        if (aset_pe (&s, i) == shmemi.mype)
+            s.me = i;
+    if (s.me < 0)
+        shmemi_fatal ("%s: PE %d is not in the active set (PE_start %d, logPE_stride %d, PE_size %d)",
+                      fn, shmemi.mype, PE_start, logPE_stride, PE_size);
+    if (nreduce < 0)
+        shmemi_fatal ("%s: nreduce %d < 0", fn, nreduce);
+    if (shmemi.debug && pSync != NULL && (pSync[0] != SHMEM_SYNC_VALUE || pSync[1] != SHMEM_SYNC_VALUE))
+        shmemi_fatal ("%s: pSync not initialised to SHMEM_SYNC_VALUE", fn);
+
+    const size_t es = mi355_dtype_size (dtype);
+    const size_t n = (size_t) nreduce;
+    if (n == 0) {
+        /* both barriers of reduce-op.c:230,266 still run */
+        shmemi_barrier_set (s.start, s.stride, s.size);
+        shmemi_barrier_set (s.start, s.stride, s.size);
+        return;
+    }
+    if (target == NULL || source == NULL)
+        shmemi_fatal ("%s: NULL target or source", fn);
+    const size_t nbytes = n * es;
+    const int kt = ptr_kind (target, nbytes), ks = ptr_kind (source, nbytes);
+    if (kt != PK_HOST || ks != PK_HOST)
+        SHMEMI_HIP (hipDeviceSynchronize ()); /* the caller's kernels that wrote source are done */
+
+    const int overlap = target != source && ranges_overlap ((size_t) target, (size_t) source, nbytes);
+    const int use_rccl = shmemi.algorithm == SHMEMX_REDUCE_RCCL && s.size == shmemi.npes && s.size > 1 &&
+                         shmemi_rccl_supported (op, dtype);
+    if (use_rccl && kt != PK_HOST && ks != PK_HOST && !overlap) {
+        if (shmemi_rccl_allreduce (op, dtype, source, target, n) != 0)
+            shmemi_fatal ("%s: ncclAllReduce failed", fn);
+        return;
+    }
+    if (kt == PK_DEV_SYM && ks == PK_DEV_SYM) {
+        reduce_symmetric (op, dtype, es, shmemi_heap_offset (target), shmemi_heap_offset (source), n, &s);
+        return;
+    }
+
+    /* staged: source -> scratch A, reduce into scratch B, B -> target */
+    const size_t a_off = shmemi.scratch_off, b_off = shmemi.scratch_off + shmemi.scratch_chunk;
+    const size_t per = shmemi.scratch_chunk / es;
+    for (size_t b = 0; b < n; b += per) {
+        const size_t cn = n - b < per ? n - b : per;
+        const hipMemcpyKind in_kind = ks == PK_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+        const hipMemcpyKind out_kind = kt == PK_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+        SHMEMI_HIP (hipMemcpyAsync (shmemi.heap + a_off, (const char *) source + b * es, cn * es, in_kind,
+                                    shmemi.stream));
+        sync_stream ();
+        size_t out_off = b_off;
+        if (s.size == 1) {
+            out_off = a_off; /* identity: copy straight back out */
+        } else if (use_rccl) {
+            if (shmemi_rccl_allreduce (op, dtype, shmemi.heap + a_off, shmemi.heap + b_off, cn) != 0)
+                shmemi_fatal ("%s: ncclAllReduce failed", fn);
+        } else {
+            reduce_symmetric (op, dtype, es, b_off, a_off, cn, &s);
+        }
+        SHMEMI_HIP (hipMemcpyAsync ((char *) target + b * es, shmemi.heap + out_off, cn * es, out_kind,
+                                    shmemi.stream));
+        sync_stream ();
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* the 44 entry points (reduce-op.c:388-448), pshmem_ strong, shmem_ weak  */
+/* ---------------------------------------------------------------------- */
+#define SHMEMI_REDUCE(Name, Op, Type, DT, OPC)                                                      \
+    void pshmem_##Name##_##Op##_to_all (Type *target, Type *source, int nreduce, int PE_start,       \
+                                        int logPE_stride, int PE_size, Type *pWrk, long *pSync)      \
+    {                                                                                                \
+        (void) pWrk; /* scratch lives in the device heap; pWrk is not touched */                   \
+        reduce_impl (OPC, DT, "shmem_" #Name "_" #Op "_to_all", target, source, nreduce, PE_start,  \
+                     logPE_stride, PE_size, pSync);                                                  \
+    }                                                                                                \
+    void shmem_##Name##_##Op##_to_all (Type *target, Type *source, int nreduce, int PE_start,        \
+                                       int logPE_stride, int PE_size, Type *pWrk, long *pSync)       \
+        __attribute__ ((weak, alias ("pshmem_" #Name "_" #Op "_to_all")));
+
+#define SUMPROD(Name, Type, DT)                          \
+    SHMEMI_REDUCE (Name, sum, Type, DT, MI355_OP_SUM)    \
+    SHMEMI_REDUCE (Name, prod, Type, DT, MI355_OP_PROD)
+#define LOGIC(Name, Type, DT)                            \
+    SHMEMI_REDUCE (Name, and, Type, DT, MI355_OP_AND)    \
+    SHMEMI_REDUCE (Name, or, Type, DT, MI355_OP_OR)      \
+    SHMEMI_REDUCE (Name, xor, Type, DT, MI355_OP_XOR)
+#define MINMAX(Name, Type, DT)                           \
+    SHMEMI_REDUCE (Name, max, Type, DT, MI355_OP_MAX)    \
+    SHMEMI_REDUCE (Name, min, Type, DT, MI355_OP_MIN)
+
+SUMPROD (short, short, MI355_SHORT)
+SUMPROD (int, int, MI355_INT)
+SUMPROD (long, long, MI355_LONG)
+SUMPROD (longlong, long long, MI355_LONGLONG)
+SUMPROD (double, double, MI355_DOUBLE)
+SUMPROD (float, float, MI355_FLOAT)
+SUMPROD (longdouble, long double, MI355_LONGDOUBLE)
+SUMPROD (complexd, double _Complex, MI355_COMPLEXD)
+SUMPROD (complexf, float _Complex, MI355_COMPLEXF)
+LOGIC (short, short, MI355_SHORT)
+LOGIC (int, int, MI355_INT)
+LOGIC (long, long, MI355_LONG)
+LOGIC (longlong, long long, MI355_LONGLONG)
+MINMAX (short, short, MI355_SHORT)
+MINMAX (int, int, MI355_INT)
+MINMAX (long, long, MI355_LONG)
+MINMAX (longlong, long long, MI355_LONGLONG)
+MINMAX (double, double, MI355_DOUBLE)
+MINMAX (float, float, MI355_FLOAT)
+MINMAX (longdouble, long double, MI355_LONGDOUBLE)

@@ -1,0 +1,772 @@
+/*
+ * runtime.c -- minimal OpenSHMEM runtime for the MI355X reduction path.
+ *
+ * The reference brings PEs up through GASNet (src/updown/updown.c:126-184 ->
+ * shmemi_comms_init, src/comms/gasnet/comms-inline.h:2893-2960). GASNet does
+ * not exist here and the reduction path only needs: PE identity, one GPU per
+ * PE, a symmetric heap, an active-set barrier, and the peer mappings that let
+ * one GPU read another's heap over xGMI. This file provides exactly that:
+ *
+ *   identity   SHMEM_PE/SHMEM_NPES, else RANK/WORLD_SIZE (torchrun), else
+ *              OMPI_COMM_WORLD_*, PMI_*; device = SHMEM_DEVICE, LOCAL_RANK or
+ *              the PE number, modulo the visible GPUs
+ *   bootstrap  one POSIX shared-memory segment per job (node-local): PE 0
+ *              creates it, every PE publishes pid/GPU/IPC handle there
+ *   heaps      device symmetric heap = one hipMalloc arena per PE, exported
+ *              with hipIpcGetMemHandle and mapped by every peer; a
+ *              deterministic first-fit allocator keeps offsets symmetric
+ *              (reference: dlmalloc mspace, src/memory/memalloc.c:71-154)
+ *   barrier    pairwise monotonic arrival counters in the segment: PE p
+ *              passes once every q of the active set has signalled p as many
+ *              times as p has met q in a barrier. This is the pSync contract
+ *              of src/barrier/barrier-linear.c:57-85 without touching pSync.
+ */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <fcntl.h>
+#include <sched.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <time.h>
+#include <unistd.h>
+
+#include "pshmem.h"
+#include "shmem.h"
+#include "shmemx.h"
+#include "shmemi.h"
+
+struct shmemi_state shmemi;
+
+struct shmemi_hostblk {
+    void *p;
+    size_t size;
+    int registered;
+    struct shmemi_hostblk *next;
+};
+
+#define SEG_MAGIC 0x4d49333535534d45ull /* "MI355SME" */
+#define SEG_VERSION 1
+
+static double now_s (void)
+{
+    struct timespec ts;
+    clock_gettime (CLOCK_MONOTONIC, &ts);
+    return (double) ts.tv_sec + 1e-9 * (double) ts.tv_nsec;
+}
+
+double shmemx_wtime (void) { return now_s (); }
+
+void shmemi_fatal (const char *fmt, ...)
+{
+    char msg[256];
+    va_list ap;
+    va_start (ap, fmt);
+    vsnprintf (msg, sizeof msg, fmt, ap);
+    va_end (ap);
+    fprintf (stderr, "[shmem PE %d/%d] FATAL: %s\n", shmemi.mype, shmemi.npes, msg);
+    fflush (stderr);
+    if (shmemi.seg != NULL) {
+        int zero = 0;
+        if (atomic_compare_exchange_strong (&shmemi.seg->abort_flag, &zero, 1)) {
+            shmemi.seg->abort_pe = shmemi.mype;
+            shmemi.seg->abort_status = 1;
+            snprintf (shmemi.seg->abort_msg, sizeof shmemi.seg->abort_msg, "%s", msg);
+        }
+    }
+    _exit (1);
+}
+
+void shmemi_hip_check (hipError_t e, const char *what)
+{
+    if (e != hipSuccess)
+        shmemi_fatal ("%s failed: %s (%d)", what, hipGetErrorString (e), (int) e);
+}
+
+void shmemi_init_check (const char *fn)
+{
+    if (!shmemi.initialized)
+        shmemi_fatal ("%s called before shmem_init()", fn);
+}
+
+/* ---------------------------------------------------------------------- */
+/* environment                                                             */
+/* ---------------------------------------------------------------------- */
+static const char *env_first (const char *const *names)
+{
+    for (; *names != NULL; ++names) {
+        const char *v = getenv (*names);
+        if (v != NULL && *v != '\0')
+            return v;
+    }
+    return NULL;
+}
+
+static long env_long (const char *const *names, long dflt)
+{
+    const char *v = env_first (names);
+    if (v == NULL)
+        return dflt;
+    char *end = NULL;
+    long x = strtol (v, &end, 10);
+    if (end == v)
+        return dflt;
+    return x;
+}
+
+/* "512M", "2G", "4096" (reference unit parser: src/utils/unitparse.c:74-142) */
+static size_t env_size (const char *name, size_t dflt)
+{
+    const char *v = getenv (name);
+    if (v == NULL || *v == '\0')
+        return dflt;
+    char *end = NULL;
+    double x = strtod (v, &end);
+    if (end == v || x < 0)
+        shmemi_fatal ("cannot parse %s=\"%s\"", name, v);
+    switch (*end) {
+    case 'k': case 'K': x *= 1024.0; break;
+    case 'm': case 'M': x *= 1024.0 * 1024.0; break;
+    case 'g': case 'G': x *= 1024.0 * 1024.0 * 1024.0; break;
+    case 't': case 'T': x *= 1024.0 * 1024.0 * 1024.0 * 1024.0; break;
+    default: break;
+    }
+    return (size_t) x;
+}
+
+static size_t round_up (size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+static int parse_algorithm (const char *v)
+{
+    if (v == NULL || strcasecmp (v, "auto") == 0) return SHMEMX_REDUCE_AUTO;
+    if (strcasecmp (v, "p2p") == 0) return SHMEMX_REDUCE_P2P;
+    if (strcasecmp (v, "exact") == 0) return SHMEMX_REDUCE_EXACT;
+    if (strcasecmp (v, "rccl") == 0) return SHMEMX_REDUCE_RCCL;
+    shmemi_fatal ("unknown SHMEM_REDUCE_ALGORITHM=\"%s\" (auto|p2p|exact|rccl)", v);
+}
+
+/* ---------------------------------------------------------------------- */
+/* bootstrap segment                                                       */
+/* ---------------------------------------------------------------------- */
+static struct shmemi_pe_info *seg_info (int pe)
+{
+    return (struct shmemi_pe_info *) ((char *) shmemi.seg + shmemi.seg->info_off) + pe;
+}
+
+static _Atomic uint64_t *seg_flag (int row_pe, int from_pe)
+{
+    _Atomic uint64_t *base = (_Atomic uint64_t *) ((char *) shmemi.seg + shmemi.seg->flags_off);
+    return base + (size_t) row_pe * shmemi.seg->flags_row + (size_t) from_pe;
+}
+
+static void seg_name (char *out, size_t len)
+{
+    const char *job = getenv ("SHMEM_JOB_ID");
+    if (job != NULL && *job != '\0') {
+        snprintf (out, len, "/mi355shmem-%u-%s", (unsigned) getuid (), job);
+        return;
+    }
+    /* every PE launched by one torchrun agent / one launcher shares a parent */
+    const char *port = getenv ("MASTER_PORT");
+    snprintf (out, len, "/mi355shmem-%u-p%d-%s", (unsigned) getuid (), (int) getppid (),
+              port != NULL ? port : "0");
+}
+
+static void check_abort (void)
+{
+    if (shmemi.seg != NULL && atomic_load (&shmemi.seg->abort_flag)) {
+        fprintf (stderr, "[shmem PE %d/%d] aborting: PE %d failed: %s\n", shmemi.mype,
+                 shmemi.npes, shmemi.seg->abort_pe, shmemi.seg->abort_msg);
+        fflush (stderr);
+        _exit (shmemi.seg->abort_status ? shmemi.seg->abort_status : 1);
+    }
+}
+
+static void bootstrap_attach (void)
+{
+    const int npes = shmemi.npes;
+    const size_t hdr = round_up (sizeof (struct shmemi_seg), 4096);
+    const size_t info = round_up (sizeof (struct shmemi_pe_info) * (size_t) npes, 4096);
+    const size_t row = round_up ((size_t) npes, 8);
+    const size_t flags = round_up (row * (size_t) npes * sizeof (uint64_t), 4096);
+    const size_t total = hdr + info + flags;
+    seg_name (shmemi.seg_name, sizeof shmemi.seg_name);
+
+    const double deadline = now_s () + shmemi.barrier_timeout;
+    if (shmemi.mype == 0) {
+        shm_unlink (shmemi.seg_name); /* stale leftover of a crashed job */
+        int fd = shm_open (shmemi.seg_name, O_CREAT | O_EXCL | O_RDWR, 0600);
+        if (fd < 0)
+            shmemi_fatal ("shm_open(%s): %s", shmemi.seg_name, strerror (errno));
+        if (ftruncate (fd, (off_t) total) != 0)
+            shmemi_fatal ("ftruncate(%s, %zu): %s", shmemi.seg_name, total, strerror (errno));
+        void *p = mmap (NULL, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+        close (fd);
+        if (p == MAP_FAILED)
+            shmemi_fatal ("mmap bootstrap segment: %s", strerror (errno));
+        shmemi.seg = (struct shmemi_seg *) p;
+        shmemi.seg->version = SEG_VERSION;
+        shmemi.seg->npes = npes;
+        shmemi.seg->info_off = hdr;
+        shmemi.seg->flags_off = hdr + info;
+        shmemi.seg->flags_row = row;
+        shmemi.seg->total_size = total;
+        atomic_store (&shmemi.seg->magic, SEG_MAGIC);
+    } else {
+        for (;;) {
+            if (now_s () > deadline)
+                shmemi_fatal ("timed out waiting for PE 0 to create %s", shmemi.seg_name);
+            int fd = shm_open (shmemi.seg_name, O_RDWR, 0600);
+            if (fd < 0) {
+                usleep (1000);
+                continue;
+            }
+            struct stat st;
+            if (fstat (fd, &st) != 0 || (size_t) st.st_size < total) {
+                close (fd);
+                usleep (1000);
+                continue;
+            }
+            void *p = mmap (NULL, total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+            close (fd);
+            if (p == MAP_FAILED)
+                shmemi_fatal ("mmap bootstrap segment: %s", strerror (errno));
+            struct shmemi_seg *s = (struct shmemi_seg *) p;
+            if (atomic_load (&s->magic) != SEG_MAGIC) {
+                munmap (p, total);
+                usleep (1000);
+                continue;
+            }
+            if (s->npes != npes || s->total_size != total)
+                shmemi_fatal ("bootstrap segment %s belongs to a job of %d PEs, not %d",
+                              shmemi.seg_name, s->npes, npes);
+            shmemi.seg = s;
+            break;
+        }
+    }
+    shmemi.seg_size = total;
+    atomic_fetch_add (&shmemi.seg->attached, 1);
+    shmemi.bar_count = (uint64_t *) calloc ((size_t) npes, sizeof (uint64_t));
+    if (shmemi.bar_count == NULL)
+        shmemi_fatal ("out of host memory");
+}
+
+/* Active-set barrier {PE_start + i*stride : i < PE_size}. Each PE adds one
+ * arrival to every other member's row, then waits until it has seen, from each
+ * member q, as many arrivals as barriers it has shared with q. A member that
+ * races ahead to the next barrier only raises a count that is already due, so
+ * no reset round (the reference's second pSync word) is needed. */
+void shmemi_barrier_set (int PE_start, int stride, int PE_size)
+{
+    if (PE_size <= 1 || shmemi.npes <= 1)
+        return;
+    const int me = shmemi.mype;
+    for (int i = 0; i < PE_size; ++i) {
+        const int q = PE_start + i * stride;
+        if (q != me)
+            atomic_fetch_add_explicit (seg_flag (q, me), 1, memory_order_release);
+    }
+    const double t0 = now_s ();
+    for (int i = 0; i < PE_size; ++i) {
+        const int q = PE_start + i * stride;
+        if (q == me)
+            continue;
+        const uint64_t want = ++shmemi.bar_count[q];
+        unsigned spins = 0;
+        while (atomic_load_explicit (seg_flag (me, q), memory_order_acquire) < want) {
+            if ((++spins & 1023u) == 0) {
+                check_abort ();
+                if (now_s () - t0 > shmemi.barrier_timeout)
+                    shmemi_fatal ("barrier timed out after %.0f s waiting for PE %d",
+                                  shmemi.barrier_timeout, q);
+                if (spins > 65536u)
+                    sched_yield ();
+            } else {
+                __builtin_ia32_pause ();
+            }
+        }
+    }
+}
+
+/* ---------------------------------------------------------------------- */
+/* device symmetric heap                                                   */
+/* ---------------------------------------------------------------------- */
+int shmemi_in_device_heap (const void *p, size_t nbytes)
+{
+    if (shmemi.heap == NULL || p == NULL)
+        return 0;
+    const char *c = (const char *) p;
+    return c >= shmemi.heap && c + nbytes <= shmemi.heap + shmemi.user_size;
+}
+
+size_t shmemi_heap_offset (const void *p) { return (size_t) ((const char *) p - shmemi.heap); }
+
+void *shmemi_peer_ptr (int pe, size_t off) { return shmemi.peer_heap[pe] + off; }
+
+static void heap_init (void)
+{
+    shmemi.user_size = round_up (env_size ("SHMEM_DEVICE_HEAP_SIZE", (size_t) 2 << 30), SHMEMI_ALIGN);
+    size_t scratch = round_up (env_size ("SHMEM_DEVICE_SCRATCH_SIZE", (size_t) 768 << 20),
+                               3 * SHMEMI_ALIGN);
+    if (scratch < 3 * 65536)
+        scratch = 3 * 65536;
+    shmemi.scratch_off = shmemi.user_size;
+    shmemi.scratch_chunk = scratch / 3 / SHMEMI_ALIGN * SHMEMI_ALIGN;
+    shmemi.heap_size = shmemi.user_size + scratch;
+    void *p = NULL;
+    hipError_t e = hipMalloc (&p, shmemi.heap_size);
+    if (e != hipSuccess)
+        shmemi_fatal ("hipMalloc of the %zu-byte device symmetric heap failed: %s "
+                      "(set SHMEM_DEVICE_HEAP_SIZE / SHMEM_DEVICE_SCRATCH_SIZE)",
+                      shmemi.heap_size, hipGetErrorString (e));
+    shmemi.heap = (char *) p;
+    struct shmemi_block *b = (struct shmemi_block *) calloc (1, sizeof *b);
+    if (b == NULL)
+        shmemi_fatal ("out of host memory");
+    b->off = 0;
+    b->size = shmemi.user_size;
+    shmemi.blocks = b;
+    shmemi.peer_heap = (char **) calloc ((size_t) shmemi.npes, sizeof (char *));
+    if (shmemi.peer_heap == NULL)
+        shmemi_fatal ("out of host memory");
+    shmemi.peer_heap[shmemi.mype] = shmemi.heap;
+}
+
+/* Publish this PE's heap and map every peer's (after the info barrier). */
+static void heap_exchange (void)
+{
+    struct shmemi_pe_info *me = seg_info (shmemi.mype);
+    me->pid = (int32_t) getpid ();
+    me->device = shmemi.device;
+    if (hipDeviceGetPCIBusId (me->pci_bus_id, (int) sizeof me->pci_bus_id, shmemi.device) != hipSuccess)
+        me->pci_bus_id[0] = '\0';
+    SHMEMI_HIP (hipIpcGetMemHandle (&me->heap_handle, shmemi.heap));
+    me->heap_size = shmemi.heap_size;
+    __atomic_store_n (&me->published, 1, __ATOMIC_RELEASE);
+    shmemi_barrier_set (0, 1, shmemi.npes);
+
+    for (int pe = 0; pe < shmemi.npes; ++pe) {
+        if (pe == shmemi.mype)
+            continue;
+        struct shmemi_pe_info *pi = seg_info (pe);
+        if (!__atomic_load_n (&pi->published, __ATOMIC_ACQUIRE))
+            shmemi_fatal ("PE %d did not publish its heap", pe);
+        if (pi->heap_size != shmemi.heap_size)
+            shmemi_fatal ("PE %d has a %llu-byte device heap, this PE %zu: heap sizes must match",
+                          pe, (unsigned long long) pi->heap_size, shmemi.heap_size);
+        int peer_dev = -1;
+        if (pi->pci_bus_id[0] != '\0' && hipDeviceGetByPCIBusId (&peer_dev, pi->pci_bus_id) != hipSuccess)
+            peer_dev = -1;
+        (void) hipGetLastError ();
+        if (peer_dev >= 0 && peer_dev != shmemi.device) {
+            int can = 0;
+            if (hipDeviceCanAccessPeer (&can, shmemi.device, peer_dev) == hipSuccess && can) {
+                hipError_t e = hipDeviceEnablePeerAccess (peer_dev, 0);
+                if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled)
+                    shmemi_fatal ("hipDeviceEnablePeerAccess(%d -> %d): %s", shmemi.device,
+                                  peer_dev, hipGetErrorString (e));
+                (void) hipGetLastError ();
+            }
+        }
+        void *p = NULL;
+        hipError_t e = hipIpcOpenMemHandle (&p, pi->heap_handle, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess)
+            shmemi_fatal ("hipIpcOpenMemHandle for PE %d (GPU %s) failed: %s", pe,
+                          pi->pci_bus_id, hipGetErrorString (e));
+        shmemi.peer_heap[pe] = (char *) p;
+    }
+    shmemi_barrier_set (0, 1, shmemi.npes);
+}
+
+void *shmemx_malloc_device (size_t size)
+{
+    shmemi_init_check ("shmemx_malloc_device");
+    if (shmemi.heap == NULL)
+        shmemi_fatal ("shmemx_malloc_device: no GPU (SHMEM_BOOTSTRAP_ONLY)");
+    void *ret = NULL;
+    if (size != 0) {
+        const size_t need = round_up (size, SHMEMI_ALIGN);
+        for (struct shmemi_block *b = shmemi.blocks; b != NULL; b = b->next) {
+            if (b->used || b->size < need)
+                continue;
+            if (b->size > need) {
+                struct shmemi_block *rest = (struct shmemi_block *) calloc (1, sizeof *rest);
+                if (rest == NULL)
+                    shmemi_fatal ("out of host memory");
+                rest->off = b->off + need;
+                rest->size = b->size - need;
+                rest->next = b->next;
+                b->next = rest;
+                b->size = need;
+            }
+            b->used = 1;
+            ret = shmemi.heap + b->off;
+            break;
+        }
+    }
+    shmem_barrier_all ();
+    return ret;
+}
+
+static int device_free (void *ptr)
+{
+    if (!shmemi_in_device_heap (ptr, 0))
+        return 0;
+    const size_t off = shmemi_heap_offset (ptr);
+    struct shmemi_block *prev = NULL;
+    for (struct shmemi_block *b = shmemi.blocks; b != NULL; prev = b, b = b->next) {
+        if (b->off != off || !b->used)
+            continue;
+        b->used = 0;
+        struct shmemi_block *n = b->next;
+        if (n != NULL && !n->used) {
+            b->size += n->size;
+            b->next = n->next;
+            free (n);
+        }
+        if (prev != NULL && !prev->used) {
+            prev->size += b->size;
+            prev->next = b->next;
+            free (b);
+        }
+        return 1;
+    }
+    shmemi_fatal ("shmem_free(%p): not an allocated device-heap block", ptr);
+}
+
+void shmemx_free_device (void *ptr)
+{
+    shmemi_init_check ("shmemx_free_device");
+    shmem_barrier_all ();
+    if (ptr != NULL && !device_free (ptr))
+        shmemi_fatal ("shmemx_free_device(%p): not in the device symmetric heap", ptr);
+}
+
+int shmemx_is_device_symmetric (const void *ptr) { return shmemi_in_device_heap (ptr, 0); }
+
+/* ---------------------------------------------------------------------- */
+/* host heap (shmem_malloc's default: the reference returns host memory)    */
+/* ---------------------------------------------------------------------- */
+static int heap_kind_device (void)
+{
+    const char *v = getenv ("SHMEM_SYMMETRIC_HEAP_KIND");
+    return v != NULL && strcasecmp (v, "device") == 0;
+}
+
+void *pshmem_malloc (size_t size)
+{
+    shmemi_init_check ("shmem_malloc");
+    if (heap_kind_device ())
+        return shmemx_malloc_device (size);
+    void *p = NULL;
+    if (size != 0) {
+        if (posix_memalign (&p, 4096, round_up (size, 4096)) != 0)
+            shmemi_fatal ("shmem_malloc(%zu): out of host memory", size);
+        struct shmemi_hostblk *h = (struct shmemi_hostblk *) calloc (1, sizeof *h);
+        if (h == NULL)
+            shmemi_fatal ("out of host memory");
+        h->p = p;
+        h->size = size;
+        /* page-locked so the staging copies run at full PCIe rate */
+        if (shmemi.device >= 0) {
+            h->registered = hipHostRegister (p, round_up (size, 4096), hipHostRegisterDefault) == hipSuccess;
+            (void) hipGetLastError ();
+        }
+        h->next = shmemi.host_blocks;
+        shmemi.host_blocks = h;
+    }
+    shmem_barrier_all ();
+    return p;
+}
+
+static void host_free_one (struct shmemi_hostblk *h)
+{
+    if (h->registered)
+        (void) hipHostUnregister (h->p);
+    free (h->p);
+    free (h);
+}
+
+void pshmem_free (void *ptr)
+{
+    shmemi_init_check ("shmem_free");
+    shmem_barrier_all ();
+    if (ptr == NULL)
+        return;
+    if (device_free (ptr))
+        return;
+    for (struct shmemi_hostblk **pp = &shmemi.host_blocks; *pp != NULL; pp = &(*pp)->next) {
+        if ((*pp)->p == ptr) {
+            struct shmemi_hostblk *h = *pp;
+            *pp = h->next;
+            host_free_one (h);
+            return;
+        }
+    }
+    shmemi_fatal ("shmem_free(%p): not allocated by shmem_malloc", ptr);
+}
+
+/* ---------------------------------------------------------------------- */
+/* init / finalize                                                         */
+/* ---------------------------------------------------------------------- */
+static void finalize_atexit (void) { pshmem_finalize (); }
+
+void pshmem_init (void)
+{
+    if (shmemi.initialized)
+        return;
+    static const char *pe_env[] = {"SHMEM_PE", "RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", NULL};
+    static const char *np_env[] = {"SHMEM_NPES", "WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", NULL};
+    static const char *dev_env[] = {"SHMEM_DEVICE", "LOCAL_RANK", "SHMEM_LOCAL_PE",
+                                    "OMPI_COMM_WORLD_LOCAL_RANK", NULL};
+    static const char *to_env[] = {"SHMEM_BARRIER_TIMEOUT", NULL};
+    static const char *dbg_env[] = {"SHMEM_DEBUG", NULL};
+    shmemi.npes = (int) env_long (np_env, 1);
+    shmemi.mype = (int) env_long (pe_env, 0);
+    if (shmemi.npes < 1 || shmemi.npes > SHMEMI_MAX_PES || shmemi.mype < 0 || shmemi.mype >= shmemi.npes)
+        shmemi_fatal ("invalid PE identity %d of %d (SHMEM_PE/SHMEM_NPES or RANK/WORLD_SIZE)",
+                      shmemi.mype, shmemi.npes);
+    shmemi.barrier_timeout = (double) env_long (to_env, 600);
+    shmemi.debug = (int) env_long (dbg_env, 0);
+    shmemi.algorithm = parse_algorithm (getenv ("SHMEM_REDUCE_ALGORITHM"));
+
+    /* test hook: bring up PEs, barriers and the host heap without a GPU (CPU
+     * tests of the bootstrap); every reduction then aborts, there is no CPU path */
+    static const char *bo_env[] = {"SHMEM_BOOTSTRAP_ONLY", NULL};
+    if (env_long (bo_env, 0) != 0) {
+        shmemi.device = -1;
+        if (shmemi.npes > 1) {
+            bootstrap_attach ();
+            shmemi_barrier_set (0, 1, shmemi.npes);
+            if (shmemi.mype == 0) {
+                shm_unlink (shmemi.seg_name);
+                shmemi.seg_unlinked = 1;
+            }
+        }
+        shmemi.initialized = 1;
+        return;
+    }
+
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount (&ndev);
+    if (e != hipSuccess || ndev < 1)
+        shmemi_fatal ("no HIP device visible (%s): the reduction path runs on the GPU and has "
+                      "no CPU fallback", e != hipSuccess ? hipGetErrorString (e) : "0 devices");
+    long dev = env_long (dev_env, shmemi.mype);
+    shmemi.device = (int) (dev % ndev);
+    SHMEMI_HIP (hipSetDevice (shmemi.device));
+    SHMEMI_HIP (hipStreamCreateWithFlags (&shmemi.stream, hipStreamNonBlocking));
+    heap_init ();
+
+    if (shmemi.npes > 1) {
+        bootstrap_attach ();
+        heap_exchange ();
+        if (shmemi.mype == 0 && !shmemi.seg_unlinked) {
+            shm_unlink (shmemi.seg_name); /* every PE is attached: drop the name */
+            shmemi.seg_unlinked = 1;
+        }
+    }
+    shmemi.initialized = 1;
+    static int registered = 0;
+    if (!registered) {
+        atexit (finalize_atexit);
+        registered = 1;
+    }
+}
+
+void pstart_pes (int npes)
+{
+    (void) npes; /* the reference ignores the argument too */
+    pshmem_init ();
+}
+
+void pshmem_finalize (void)
+{
+    if (!shmemi.initialized)
+        return;
+    shmem_barrier_all ();
+    if (shmemi.device >= 0)
+        (void) hipDeviceSynchronize ();
+    if (shmemi.rccl_comm != NULL) {
+        extern void shmemi_rccl_destroy (void);
+        shmemi_rccl_destroy ();
+    }
+    if (shmemi.peer_heap != NULL) {
+        for (int pe = 0; pe < shmemi.npes; ++pe)
+            if (pe != shmemi.mype && shmemi.peer_heap[pe] != NULL)
+                (void) hipIpcCloseMemHandle (shmemi.peer_heap[pe]);
+        /* the peers may still read this heap until they have closed theirs */
+        shmem_barrier_all ();
+        free (shmemi.peer_heap);
+        shmemi.peer_heap = NULL;
+    }
+    while (shmemi.blocks != NULL) {
+        struct shmemi_block *n = shmemi.blocks->next;
+        free (shmemi.blocks);
+        shmemi.blocks = n;
+    }
+    while (shmemi.host_blocks != NULL) {
+        struct shmemi_hostblk *n = shmemi.host_blocks->next;
+        host_free_one (shmemi.host_blocks);
+        shmemi.host_blocks = n;
+    }
+    if (shmemi.heap != NULL)
+        (void) hipFree (shmemi.heap);
+    shmemi.heap = NULL;
+    if (shmemi.ev != NULL) {
+        for (int i = 0; i < 2 * shmemi.timed_cap; ++i)
+            (void) hipEventDestroy (shmemi.ev[i]);
+        free (shmemi.ev);
+        shmemi.ev = NULL;
+        shmemi.timed_cap = 0;
+    }
+    if (shmemi.stream != NULL)
+        (void) hipStreamDestroy (shmemi.stream);
+    shmemi.stream = NULL;
+    if (shmemi.seg != NULL) {
+        munmap (shmemi.seg, shmemi.seg_size);
+        shmemi.seg = NULL;
+    }
+    free (shmemi.bar_count);
+    shmemi.bar_count = NULL;
+    shmemi.initialized = 0;
+}
+
+void pshmem_global_exit (int status)
+{
+    if (shmemi.seg != NULL) {
+        int zero = 0;
+        if (atomic_compare_exchange_strong (&shmemi.seg->abort_flag, &zero, 1)) {
+            shmemi.seg->abort_pe = shmemi.mype;
+            shmemi.seg->abort_status = status;
+            snprintf (shmemi.seg->abort_msg, sizeof shmemi.seg->abort_msg,
+                      "shmem_global_exit(%d)", status);
+        }
+    }
+    fflush (NULL);
+    _exit (status);
+}
+
+int pshmem_my_pe (void) { return shmemi.mype; }
+int pshmem_n_pes (void) { return shmemi.initialized ? shmemi.npes : 1; }
+
+void pshmem_barrier_all (void)
+{
+    shmemi_init_check ("shmem_barrier_all");
+    if (shmemi.stream != NULL)
+        SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    shmemi_barrier_set (0, 1, shmemi.npes);
+}
+
+void pshmem_barrier (int PE_start, int logPE_stride, int PE_size, long *pSync)
+{
+    (void) pSync; /* counters live in the bootstrap segment; pSync stays SHMEM_SYNC_VALUE */
+    shmemi_init_check ("shmem_barrier");
+    if (logPE_stride < 0 || logPE_stride > 30 || PE_size < 1 || PE_start < 0 ||
+        PE_start + (long) (PE_size - 1) * (1L << logPE_stride) >= shmemi.npes)
+        shmemi_fatal ("shmem_barrier: active set (%d, %d, %d) outside the %d PEs", PE_start,
+                      logPE_stride, PE_size, shmemi.npes);
+    if (shmemi.stream != NULL)
+        SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    shmemi_barrier_set (PE_start, 1 << logPE_stride, PE_size);
+}
+
+void pshmem_quiet (void)
+{
+    if (shmemi.initialized && shmemi.stream != NULL)
+        SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+}
+
+/* shmem_ names are weak aliases of the pshmem_ ones (PSHMEM, reference
+ * src/profiling/profiling.c and src/reduce/reduce-op.c:291-380) */
+#define WEAK(name) __attribute__ ((weak, alias ("p" #name)))
+void start_pes (int npes) WEAK (start_pes);
+void shmem_init (void) WEAK (shmem_init);
+void shmem_finalize (void) WEAK (shmem_finalize);
+void shmem_global_exit (int status) WEAK (shmem_global_exit);
+int shmem_my_pe (void) WEAK (shmem_my_pe);
+int shmem_n_pes (void) WEAK (shmem_n_pes);
+int _my_pe (void) __attribute__ ((weak, alias ("pshmem_my_pe")));
+int _num_pes (void) __attribute__ ((weak, alias ("pshmem_n_pes")));
+void *shmem_malloc (size_t size) WEAK (shmem_malloc);
+void shmem_free (void *ptr) WEAK (shmem_free);
+void shmem_barrier_all (void) WEAK (shmem_barrier_all);
+void shmem_barrier (int PE_start, int logPE_stride, int PE_size, long *pSync) WEAK (shmem_barrier);
+void shmem_quiet (void) WEAK (shmem_quiet);
+
+/* ---------------------------------------------------------------------- */
+/* extensions                                                              */
+/* ---------------------------------------------------------------------- */
+int shmemx_set_reduce_algorithm (int algorithm)
+{
+    if (algorithm < SHMEMX_REDUCE_AUTO || algorithm > SHMEMX_REDUCE_RCCL)
+        shmemi_fatal ("shmemx_set_reduce_algorithm(%d): unknown algorithm", algorithm);
+    int old = shmemi.algorithm;
+    shmemi.algorithm = algorithm;
+    return old;
+}
+
+int shmemx_get_reduce_algorithm (void) { return shmemi.algorithm; }
+
+int shmemx_device_id (void) { return shmemi.initialized ? shmemi.device : -1; }
+
+void shmemx_device_synchronize (void) { SHMEMI_HIP (hipDeviceSynchronize ()); }
+
+void shmemx_memcpy (void *dst, const void *src, size_t nbytes)
+{
+    if (nbytes == 0)
+        return;
+    SHMEMI_HIP (hipMemcpy (dst, src, nbytes, hipMemcpyDefault));
+}
+
+void shmemx_kernel_timing (int enable)
+{
+    if (enable)
+        SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    shmemi.timing = enable ? 1 : 0;
+    if (enable)
+        shmemi.ntimed = 0;
+}
+
+void shmemi_timed_begin (void)
+{
+    if (!shmemi.timing)
+        return;
+    if (shmemi.ntimed == shmemi.timed_cap) {
+        int cap = shmemi.timed_cap ? 2 * shmemi.timed_cap : 256;
+        hipEvent_t *ev = (hipEvent_t *) realloc (shmemi.ev, sizeof (hipEvent_t) * 2 * (size_t) cap);
+        if (ev == NULL)
+            shmemi_fatal ("out of host memory");
+        for (int i = 2 * shmemi.timed_cap; i < 2 * cap; ++i)
+            SHMEMI_HIP (hipEventCreate (&ev[i]));
+        shmemi.ev = ev;
+        shmemi.timed_cap = cap;
+    }
+    SHMEMI_HIP (hipEventRecord (shmemi.ev[2 * shmemi.ntimed], shmemi.stream));
+}
+
+void shmemi_timed_end (void)
+{
+    if (!shmemi.timing)
+        return;
+    SHMEMI_HIP (hipEventRecord (shmemi.ev[2 * shmemi.ntimed + 1], shmemi.stream));
+    shmemi.ntimed++;
+}
+
+void shmemx_kernel_timing_stats (long *launches, double *total_ms, double *avg_ms)
+{
+    double tot = 0.0;
+    if (shmemi.ntimed > 0)
+        SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    for (int i = 0; i < shmemi.ntimed; ++i) {
+        float ms = 0.f;
+        SHMEMI_HIP (hipEventElapsedTime (&ms, shmemi.ev[2 * i], shmemi.ev[2 * i + 1]));
+        tot += ms;
+    }
+    if (launches) *launches = shmemi.ntimed;
+    if (total_ms) *total_ms = tot;
+    if (avg_ms) *avg_ms = shmemi.ntimed ? tot / shmemi.ntimed : 0.0;
+}

@@ -1,0 +1,114 @@
+/*
+ * shmemi.h -- internal state of the MI355X reduction runtime (host C).
+ *
+ * Counterpart of the reference's per-PE state (src/utils/state.h:83-109)
+ * cut down to what the reduction path needs, plus the GPU side: the HIP
+ * device, the library stream, the device symmetric heap and the peer
+ * mappings of every other PE's heap (xGMI).
+ */
+#ifndef SHMEMI_H
+#define SHMEMI_H 1
+
+#include <stddef.h>
+#include <stdint.h>
+#include <stdatomic.h>
+
+#ifndef __HIP_PLATFORM_AMD__
+#define __HIP_PLATFORM_AMD__ 1
+#endif
+#include <hip/hip_runtime_api.h>
+
+#define SHMEMI_MAX_PES 1024
+#define SHMEMI_ALIGN 256
+
+/* ---- bootstrap segment (POSIX shm, one per job, node-local) ---- */
+struct shmemi_pe_info {
+    int32_t pid;
+    int32_t device;
+    char pci_bus_id[32];
+    hipIpcMemHandle_t heap_handle;
+    uint64_t heap_size;
+    int32_t published;
+    int32_t pad;
+};
+
+struct shmemi_seg {
+    _Atomic uint64_t magic;     /* written last by the creator */
+    int32_t version;
+    int32_t npes;
+    _Atomic int32_t attached;
+    _Atomic int32_t abort_flag;
+    int32_t abort_pe;
+    int32_t abort_status;
+    char abort_msg[256];
+    _Atomic int32_t rccl_id_ready;
+    int32_t pad0;
+    char rccl_id[128];          /* ncclUniqueId from PE 0 */
+    uint64_t info_off;          /* -> struct shmemi_pe_info[npes] */
+    uint64_t flags_off;         /* -> _Atomic uint64_t flags[npes][row] */
+    uint64_t flags_row;         /* words per row (padded) */
+    uint64_t total_size;
+};
+
+/* ---- device heap allocator block ---- */
+struct shmemi_block {
+    size_t off, size;
+    int used;
+    struct shmemi_block *next;
+};
+
+struct shmemi_state {
+    int initialized;
+    int mype, npes;
+    int device;
+    hipStream_t stream;
+    int algorithm;              /* enum shmemx_reduce_algorithm */
+    double barrier_timeout;     /* seconds */
+    int debug;
+
+    /* bootstrap */
+    struct shmemi_seg *seg;
+    size_t seg_size;
+    char seg_name[128];
+    int seg_unlinked;
+    uint64_t *bar_count;        /* [npes]: barriers done with each peer */
+
+    /* device symmetric heap: [user | scratch] */
+    char *heap;                 /* this PE's base */
+    size_t heap_size;           /* total */
+    size_t user_size;           /* user part */
+    size_t scratch_off;         /* = user_size */
+    size_t scratch_chunk;       /* bytes per staging buffer (3 buffers) */
+    char **peer_heap;           /* [npes]: mapped base of every PE's heap */
+    struct shmemi_block *blocks;
+
+    /* host allocations made by shmem_malloc */
+    struct shmemi_hostblk *host_blocks;
+
+    /* RCCL */
+    void *rccl_comm;            /* ncclComm_t of the whole world, lazily */
+
+    /* kernel timing */
+    int timing;
+    int ntimed;
+    int timed_cap;
+    hipEvent_t *ev;             /* 2 per timed launch */
+};
+
+extern struct shmemi_state shmemi;
+
+/* runtime.c */
+void shmemi_fatal (const char *fmt, ...) __attribute__ ((noreturn, format (printf, 1, 2)));
+void shmemi_init_check (const char *fn);
+void shmemi_hip_check (hipError_t e, const char *what);
+void shmemi_barrier_set (int PE_start, int stride, int PE_size);
+int shmemi_in_device_heap (const void *p, size_t nbytes);
+size_t shmemi_heap_offset (const void *p);
+void *shmemi_peer_ptr (int pe, size_t off);
+void shmemi_timed_begin (void);
+void shmemi_timed_end (void);
+int shmemi_rccl_comm (void **comm);
+
+#define SHMEMI_HIP(call) shmemi_hip_check ((call), #call)
+
+#endif /* SHMEMI_H */

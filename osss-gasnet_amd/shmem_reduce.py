@@ -1,0 +1,145 @@
+"""ctypes binding of libshmem_reduce.so for tests and bench.py.
+
+The product is the C library (include/shmem.h, shmemx.h, mi355_reduce.h);
+this module only loads it and marshals numpy arrays and pointers, the way an
+OpenSHMEM test program in C would call it. It never computes a reduction
+itself: if the library is missing, loading fails loudly.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libshmem_reduce.so")
+
+OPS = ["sum", "prod", "and", "or", "xor", "min", "max"]           # enum mi355_op
+DTYPES = ["short", "int", "long", "longlong", "float", "double",   # enum mi355_dtype
+          "longdouble", "complexf", "complexd"]
+NP = {
+    "short": np.int16, "int": np.int32, "long": np.int64, "longlong": np.int64,
+    "float": np.float32, "double": np.float64, "longdouble": np.longdouble,
+    "complexf": np.complex64, "complexd": np.complex128,
+}
+ALGORITHMS = {"auto": 0, "p2p": 1, "exact": 2, "rccl": 3}          # enum shmemx_reduce_algorithm
+SHMEM_REDUCE_SYNC_SIZE = 128
+SHMEM_REDUCE_MIN_WRKDATA_SIZE = 64
+SHMEM_SYNC_VALUE = -1
+
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_i = ctypes.c_int
+
+
+def load(path=LIB_PATH):
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    sig = {
+        "shmem_init": ([], None), "shmem_finalize": ([], None),
+        "shmem_my_pe": ([], _i), "shmem_n_pes": ([], _i),
+        "shmem_malloc": ([_sz], _vp), "shmem_free": ([_vp], None),
+        "shmem_barrier_all": ([], None),
+        "shmem_barrier": ([_i, _i, _i, _vp], None),
+        "shmem_global_exit": ([_i], None),
+        "shmemx_malloc_device": ([_sz], _vp), "shmemx_free_device": ([_vp], None),
+        "shmemx_is_device_symmetric": ([_vp], _i),
+        "shmemx_set_reduce_algorithm": ([_i], _i), "shmemx_get_reduce_algorithm": ([], _i),
+        "shmemx_device_id": ([], _i), "shmemx_device_synchronize": ([], None),
+        "shmemx_memcpy": ([_vp, _vp, _sz], None), "shmemx_wtime": ([], ctypes.c_double),
+        "shmemx_kernel_timing": ([_i], None),
+        "shmemx_kernel_timing_stats": ([ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double),
+                                        ctypes.POINTER(ctypes.c_double)], None),
+        "mi355_dtype_size": ([_i], _sz), "mi355_op_supported": ([_i, _i], _i),
+        "mi355_combine": ([_i, _i, _vp, ctypes.POINTER(_vp), _i, _sz, _vp], _i),
+        "mi355_copy_segments": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_sz), _i, _vp], _i),
+        "mi355_shard_bounds": ([_sz, _sz, _i, _i, ctypes.POINTER(_sz), ctypes.POINTER(_sz)], None),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(lib, name)
+        f.argtypes = args
+        f.restype = res
+    return lib
+
+
+class Shmem:
+    """One PE's view of the library (call init() once per process)."""
+
+    def __init__(self, path=LIB_PATH):
+        self.lib = load(path)
+        self._psync = np.full(SHMEM_REDUCE_SYNC_SIZE, SHMEM_SYNC_VALUE, dtype=np.int64)
+
+    # ---- runtime
+    def init(self):
+        self.lib.shmem_init()
+
+    def finalize(self):
+        self.lib.shmem_finalize()
+
+    def my_pe(self):
+        return self.lib.shmem_my_pe()
+
+    def n_pes(self):
+        return self.lib.shmem_n_pes()
+
+    def barrier_all(self):
+        self.lib.shmem_barrier_all()
+
+    def malloc_device(self, nbytes):
+        return self.lib.shmemx_malloc_device(nbytes)
+
+    def free_device(self, ptr):
+        self.lib.shmemx_free_device(ptr)
+
+    def malloc(self, nbytes):
+        return self.lib.shmem_malloc(nbytes)
+
+    def free(self, ptr):
+        self.lib.shmem_free(ptr)
+
+    def set_algorithm(self, name):
+        return self.lib.shmemx_set_reduce_algorithm(ALGORITHMS[name])
+
+    def sync(self):
+        self.lib.shmemx_device_synchronize()
+
+    # ---- data movement (hipMemcpy, blocking)
+    def put(self, dptr, arr):
+        arr = np.ascontiguousarray(arr)
+        self.lib.shmemx_memcpy(dptr, arr.ctypes.data, arr.nbytes)
+
+    def get(self, dptr, n, dtype):
+        out = np.empty(n, dtype=NP[dtype] if isinstance(dtype, str) else dtype)
+        self.lib.shmemx_memcpy(out.ctypes.data, dptr, out.nbytes)
+        return out
+
+    # ---- the reduction entry points (include/shmem.h)
+    def to_all(self, op, dtype, target, source, nreduce, PE_start=0, logPE_stride=0, PE_size=None,
+               pWrk=None, pSync=None):
+        if PE_size is None:
+            PE_size = self.n_pes()
+        f = getattr(self.lib, f"shmem_{dtype}_{op}_to_all")
+        f.restype = None
+        f.argtypes = [_vp, _vp, _i, _i, _i, _i, _vp, _vp]
+        if pSync is None:
+            pSync = self._psync.ctypes.data
+        f(target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync)
+
+    # ---- the combine layer (include/mi355_reduce.h)
+    def combine(self, op, dtype, dst, srcs, n, stream=None):
+        arr = (_vp * len(srcs))(*srcs)
+        return self.lib.mi355_combine(OPS.index(op), DTYPES.index(dtype), dst, arr, len(srcs), n, stream)
+
+    def kernel_timing(self, enable):
+        self.lib.shmemx_kernel_timing(1 if enable else 0)
+
+    def kernel_timing_stats(self):
+        n, tot, avg = ctypes.c_long(), ctypes.c_double(), ctypes.c_double()
+        self.lib.shmemx_kernel_timing_stats(ctypes.byref(n), ctypes.byref(tot), ctypes.byref(avg))
+        return n.value, tot.value, avg.value
+
+
+def shard_bounds(lib, n, elem_size, nshards, i):
+    lo, hi = _sz(), _sz()
+    lib.mi355_shard_bounds(n, elem_size, nshards, i, ctypes.byref(lo), ctypes.byref(hi))
+    return lo.value, hi.value

@@ -1,0 +1,36 @@
+"""Bit comparison helpers shared by the parity tests (test infrastructure)."""
+import numpy as np
+
+import oracle
+
+FP = {"float", "double", "longdouble", "complexf", "complexd"}
+
+
+def mismatches(got, want, op, dtype):
+    """Indices where got != want. Integer/logical and min/max: every value bit
+    must match. FP sum/prod: bits must match, except that two NaNs match (IEEE
+    754 leaves NaN payload propagation open; the x86 host and gfx950 differ)."""
+    got = np.ascontiguousarray(got, dtype=oracle.NP[dtype])
+    want = np.ascontiguousarray(want, dtype=oracle.NP[dtype])
+    assert got.shape == want.shape, (got.shape, want.shape)
+    if got.size == 0:
+        return np.zeros(0, dtype=np.int64)
+    eq = (oracle.as_value_bytes(got, dtype) == oracle.as_value_bytes(want, dtype)).all(axis=1)
+    if dtype in FP and op in ("sum", "prod"):
+        if dtype.startswith("complex"):
+            nan_ok = ((np.isnan(got.real) & np.isnan(want.real)) | (got.real.view(np.uint8).reshape(len(got), -1) ==
+                      want.real.view(np.uint8).reshape(len(want), -1)).all(axis=1)) & \
+                     ((np.isnan(got.imag) & np.isnan(want.imag)) | (got.imag.view(np.uint8).reshape(len(got), -1) ==
+                      want.imag.view(np.uint8).reshape(len(want), -1)).all(axis=1))
+        else:
+            nan_ok = np.isnan(got) & np.isnan(want)
+        eq = eq | nan_ok
+    return np.nonzero(~eq)[0]
+
+
+def assert_match(got, want, op, dtype, ctx=""):
+    bad = mismatches(got, want, op, dtype)
+    if len(bad):
+        i = bad[0]
+        raise AssertionError(f"{ctx} {op}/{dtype}: {len(bad)} of {len(got)} elements differ; "
+                             f"first at {i}: got {got[i]!r} want {want[i]!r}")

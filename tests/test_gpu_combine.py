@@ -1,0 +1,162 @@
+"""GPU: the combine layer (include/mi355_reduce.h) against the golden vectors
+and the oracle, called through the C ABI on device buffers.
+
+A fold of the sources in order [me, every other member ascending] is exactly
+what the reference computes on member `me` (reduce-op.c:226-264), so one GPU
+reproduces every PE's reference result of a golden case.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from _compare import assert_match
+from test_oracle_golden import load_cases
+
+pytestmark = pytest.mark.gpu
+
+
+class Dev:
+    """Device buffers from the symmetric heap, freed at the end of a test."""
+
+    def __init__(self, shm):
+        self.shm, self.ptrs = shm, []
+
+    def upload(self, arr):
+        p = self.shm.malloc_device(max(arr.nbytes, 16))
+        if arr.nbytes:
+            self.shm.put(p, arr)
+        self.ptrs.append(p)
+        return p
+
+    def empty(self, nbytes):
+        p = self.shm.malloc_device(max(nbytes, 16))
+        self.ptrs.append(p)
+        return p
+
+    def free(self):
+        for p in reversed(self.ptrs):
+            self.shm.free_device(p)
+        self.ptrs = []
+
+
+@pytest.fixture
+def dev(shm):
+    d = Dev(shm)
+    yield d
+    d.free()
+
+
+def gpu_fold(shm, dev, op, dtype, srcs, offset_elems=0):
+    n = len(srcs[0])
+    es = np.dtype(oracle.NP[dtype]).itemsize
+    ptrs = []
+    for s in srcs:
+        pad = np.zeros(offset_elems, dtype=oracle.NP[dtype])
+        ptrs.append(dev.upload(np.concatenate([pad, s])) + offset_elems * es)
+    out = dev.empty((n + offset_elems) * es) + offset_elems * es
+    rc = shm.combine(op, dtype, out, ptrs, n)
+    assert rc == 0, rc
+    shm.sync()
+    return shm.get(out, n, dtype)
+
+
+@pytest.mark.parametrize("op,dtype", oracle.PAIRS)
+def test_combine_reproduces_every_pe_of_golden(shm, dev, op, dtype):
+    for npes, ins, outs in load_cases(op, dtype):
+        if ins.shape[1] == 0:
+            continue
+        for me in range(npes):
+            order = [me] + [i for i in range(npes) if i != me]
+            got = gpu_fold(shm, dev, op, dtype, [ins[i] for i in order])
+            assert_match(got, outs[me], op, dtype, ctx=f"golden npes={npes} me={me}")
+        dev.free()
+
+
+@pytest.mark.parametrize("op,dtype", [("sum", "double"), ("xor", "int"), ("max", "float"), ("prod", "complexf"),
+                                      ("min", "longdouble"), ("sum", "short")])
+@pytest.mark.parametrize("nsrc", [1, 2, 5, 8, 9, 12, 17])
+def test_combine_any_number_of_sources(shm, dev, op, dtype, nsrc):
+    import gen_golden
+    rng = np.random.default_rng(nsrc)
+    srcs = [gen_golden.values(rng, op, dtype, 3001) for _ in range(nsrc)]
+    got = gpu_fold(shm, dev, op, dtype, srcs)
+    assert_match(got, oracle.reduce_pe(op, dtype, srcs, 0), op, dtype, ctx=f"nsrc={nsrc}")
+
+
+@pytest.mark.parametrize("n", [1, 2, 7, 8, 9, 255, 256, 257, 4095, 100003])
+@pytest.mark.parametrize("dtype", ["short", "float", "double", "complexd"])
+def test_combine_sizes_and_tails(shm, dev, n, dtype):
+    import gen_golden
+    rng = np.random.default_rng(n)
+    srcs = [gen_golden.values(rng, "sum", dtype, n) for _ in range(3)]
+    got = gpu_fold(shm, dev, "sum", dtype, srcs)
+    assert_match(got, oracle.reduce_pe("sum", dtype, srcs, 0), "sum", dtype)
+
+
+@pytest.mark.parametrize("off", [1, 3])
+@pytest.mark.parametrize("op,dtype", [("sum", "double"), ("and", "short"), ("min", "float"), ("prod", "int")])
+def test_combine_unaligned_pointers(shm, dev, op, dtype, off):
+    import gen_golden
+    rng = np.random.default_rng(off)
+    srcs = [gen_golden.values(rng, op, dtype, 1000) for _ in range(4)]
+    got = gpu_fold(shm, dev, op, dtype, srcs, offset_elems=off)
+    assert_match(got, oracle.reduce_pe(op, dtype, srcs, 0), op, dtype, ctx=f"offset {off}")
+
+
+def test_longdouble_random_encodings(shm, dev):
+    """Every 16-bit sign/exponent with random significands, all four ops, against
+    the host x87 (the oracle is gcc-compiled long double arithmetic)."""
+    rng = np.random.default_rng(99)
+    n = 200000
+    raw = np.zeros((3, n, 16), dtype=np.uint8)
+    for k in range(3):
+        m = rng.integers(0, 2**64, n, dtype=np.uint64, endpoint=False)
+        se = rng.integers(0, 2**16, n, dtype=np.uint16)
+        # bias half the exponents towards the normal range around 1.0 so sums interact
+        near = rng.random(n) < 0.5
+        se[near] = (se[near] & 0x8000) | (16383 + rng.integers(-70, 70, int(near.sum()))).astype(np.uint16)
+        m[near] |= np.uint64(1 << 63)
+        raw[k, :, 0:8] = m.view(np.uint8).reshape(n, 8)
+        raw[k, :, 8:10] = se.view(np.uint8).reshape(n, 2)
+    srcs = [raw[k].view(np.longdouble).reshape(n) for k in range(3)]
+    for op in ("sum", "prod", "min", "max"):
+        got = gpu_fold(shm, dev, op, "longdouble", srcs)
+        assert_match(got, oracle.reduce_pe(op, "longdouble", srcs, 0), op, "longdouble")
+        dev.free()
+
+
+def test_complex_prod_annex_g_cases(shm, dev):
+    inf, nan = np.inf, np.nan
+    vals = [complex(inf, nan), complex(nan, inf), complex(inf, inf), complex(nan, nan), complex(0, 0),
+            complex(1, 2), complex(-0.0, inf), complex(1e308, 1e308), complex(nan, 0), complex(0, -inf)]
+    a = np.array([x for x in vals for _ in vals], dtype=np.complex128)
+    b = np.array([y for _ in vals for y in vals], dtype=np.complex128)
+    for dtype in ("complexd", "complexf"):
+        srcs = [a.astype(oracle.NP[dtype]), b.astype(oracle.NP[dtype])]
+        got = gpu_fold(shm, dev, "prod", dtype, srcs)
+        assert_match(got, oracle.reduce_pe("prod", dtype, srcs, 0), "prod", dtype)
+        dev.free()
+
+
+def test_full_size_256mib_properties(shm, dev):
+    """At the benchmark size (2^25 doubles = 256 MiB per source):
+    - 2-source double sum equals numpy's IEEE a + b bit for bit,
+    - xor is an involution (a ^ b ^ b == a), and
+    - a one-source fold (copy) is the identity."""
+    n = 1 << 25
+    rng = np.random.default_rng(5)
+    a = rng.standard_normal(n) * np.exp2(rng.integers(-20, 20, n))
+    b = rng.standard_normal(n)
+    pa, pb = dev.upload(a), dev.upload(b)
+    out = dev.empty(8 * n)
+    assert shm.combine("sum", "double", out, [pa, pb], n) == 0
+    shm.sync()
+    got = shm.get(out, n, "double")
+    assert (got.view(np.uint64) == (a + b).view(np.uint64)).all()
+    ai, bi = a.view(np.int64), b.view(np.int64)
+    assert shm.combine("xor", "longlong", out, [pa, pb, pb], n) == 0
+    shm.sync()
+    assert (shm.get(out, n, "longlong") == ai).all()
+    assert shm.combine("sum", "double", out, [pb], n) == 0
+    shm.sync()
+    assert (shm.get(out, n, "double").view(np.uint64) == b.view(np.uint64)).all()

@@ -1,0 +1,157 @@
+"""GPU: the collectives across several PE processes (P2P and EXACT schedules).
+
+The box has one MI355X, so the PEs share it: each PE is its own process with
+its own device heap, peers are mapped through hipIpcOpenMemHandle exactly as
+across GPUs (the xGMI case differs only in where the bytes travel). Each run
+starts N pe_worker.py processes from this (not yet GPU-initialised) pytest
+process, then checks every PE's target against the oracle:
+
+  P2P   every member's result == the reference's result on PE_start
+        (bit-exact, NaN-payloads aside), i.e. identical on all members
+  EXACT member i's result == the reference's result on member i
+"""
+import itertools
+import json
+import os
+import subprocess
+import sys
+import uuid
+
+import numpy as np
+import pytest
+
+import oracle
+from _compare import assert_match
+from _inputs import source
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+pytestmark = [pytest.mark.gpu, pytest.mark.multipe]
+
+
+def run_pes(npes, cases, tmp_path, extra_env=None, timeout=600):
+    spec = tmp_path / "spec.json"
+    spec.write_text(json.dumps({"cases": cases}))
+    env = dict(os.environ)
+    env.update({"SHMEM_NPES": str(npes), "SHMEM_JOB_ID": uuid.uuid4().hex[:12], "SHMEM_DEVICE": "0",
+                "SHMEM_DEVICE_HEAP_SIZE": "96M", "SHMEM_DEVICE_SCRATCH_SIZE": "384K",
+                "SHMEM_BARRIER_TIMEOUT": "120"})
+    env.update(extra_env or {})
+    procs = []
+    for pe in range(npes):
+        e = dict(env, SHMEM_PE=str(pe))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "pe_worker.py"), str(spec), str(tmp_path)],
+                                      env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            out, _ = p.communicate(timeout=timeout)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        outs.append((p.returncode, out))
+    for pe, (rc, out) in enumerate(outs):
+        assert rc == 0, f"PE {pe} exited {rc}:\n{out[-3000:]}"
+    return [np.load(tmp_path / f"pe{pe}.npz") for pe in range(npes)]
+
+
+def members(start, logstride, size):
+    return [start + i * (1 << logstride) for i in range(size)]
+
+
+def check(results, cases):
+    for c in cases:
+        op, dtype, n = c["op"], c["dtype"], c["n"]
+        for s in c["sets"]:
+            mem = members(*s)
+            srcs = [source(op, dtype, n, c["seed"], pe) for pe in mem]
+            for i, pe in enumerate(mem):
+                got = results[pe][str(c["id"])]
+                exact = c.get("algorithm") == "exact"
+                want = oracle.reduce_pe(op, dtype, srcs, i if exact else 0)
+                assert_match(got, want, op, dtype, ctx=f"case {c['id']} {c['mode']} {c.get('algorithm')} "
+                                                        f"set {s} PE {pe}:")
+
+
+def make_cases(pairs, n, sets, mode, algorithm, start_id, seed=11):
+    out = []
+    for k, (op, dtype) in enumerate(pairs):
+        out.append({"id": start_id + k, "op": op, "dtype": dtype, "n": n, "sets": sets, "mode": mode,
+                    "algorithm": algorithm, "seed": seed + start_id + k})
+    return out
+
+
+SOME = [("sum", "double"), ("sum", "float"), ("xor", "int"), ("and", "longlong"), ("max", "float"),
+        ("min", "short"), ("prod", "complexd"), ("sum", "longdouble")]
+
+
+def test_four_pes_all_44_pairs_p2p_and_exact(tmp_path):
+    cases = []
+    cases += make_cases(oracle.PAIRS, 1000, [[0, 0, 4]], "dev", "p2p", 0)
+    cases += make_cases(oracle.PAIRS, 257, [[0, 0, 4]], "dev", "exact", 100)
+    results = run_pes(4, cases, tmp_path)
+    check(results, cases)
+
+
+def test_four_pes_modes_and_active_sets(tmp_path):
+    cases = []
+    cid = 1000
+    for mode, alg in itertools.product(["inplace", "overlap_up", "overlap_down", "host", "unaligned"],
+                                       ["p2p", "exact"]):
+        cases += make_cases(SOME, 515, [[0, 0, 4]], mode, alg, cid)
+        cid += 100
+    # two disjoint strided sets running at once, a 3-PE set, and a set of one
+    cases += make_cases(SOME, 515, [[0, 1, 2], [1, 1, 2]], "dev", "p2p", cid); cid += 100
+    cases += make_cases(SOME, 515, [[1, 0, 3]], "dev", "p2p", cid); cid += 100
+    cases += make_cases(SOME, 515, [[2, 0, 1]], "dev", "p2p", cid); cid += 100
+    # multi-chunk staging (scratch is 3 x 128 KiB): 100k doubles from host memory
+    cases += make_cases([("sum", "double"), ("max", "int")], 100000, [[0, 0, 4]], "host", "p2p", cid); cid += 100
+    cases += make_cases([("sum", "double")], 100000, [[0, 0, 4]], "host", "exact", cid); cid += 100
+    # edge sizes: nothing, one element, fewer elements than PEs x alignment
+    for n in (0, 1, 3, 64):
+        cases += make_cases([("sum", "double"), ("or", "short")], n, [[0, 0, 4]], "dev", "p2p", cid); cid += 100
+    results = run_pes(4, cases, tmp_path)
+    check(results, cases)
+
+
+@pytest.mark.parametrize("npes", [2, 3])
+def test_two_and_three_pes(tmp_path, npes):
+    cases = make_cases(SOME, 4099, [[0, 0, npes]], "dev", "p2p", 0)
+    cases += make_cases(SOME, 333, [[0, 0, npes]], "inplace", "exact", 100)
+    results = run_pes(npes, cases, tmp_path)
+    check(results, cases)
+
+
+def test_eight_pes_one_gpu(tmp_path):
+    cases = make_cases([("sum", "double"), ("and", "longlong"), ("max", "float")], 20000, [[0, 0, 8]],
+                       "dev", "p2p", 0)
+    cases += make_cases([("sum", "double")], 20000, [[0, 1, 4], [1, 1, 4]], "dev", "p2p", 100)
+    results = run_pes(8, cases, tmp_path)
+    check(results, cases)
+
+
+def test_bad_active_set_aborts_every_pe(tmp_path):
+    """A PE outside the active set fails loudly and its peers do not hang."""
+    cases = [{"id": 0, "op": "sum", "dtype": "double", "n": 10, "sets": [[0, 0, 2]], "mode": "dev",
+              "algorithm": "p2p", "seed": 1},
+             # PE 1 calls with a set that excludes it -> fatal; PE 0 waits in a barrier
+             {"id": 1, "op": "sum", "dtype": "double", "n": 10, "sets": [[0, 0, 1], [1, 0, 1]], "mode": "dev",
+              "algorithm": "p2p", "seed": 2, "bad_for_pe1": True}]
+    spec = tmp_path / "spec.json"
+    bad = dict(cases[1])
+    bad["sets"] = [[0, 0, 2]]
+    spec.write_text(json.dumps({"cases": [cases[0], bad]}))
+    env = dict(os.environ, SHMEM_NPES="2", SHMEM_JOB_ID=uuid.uuid4().hex[:12], SHMEM_DEVICE="0",
+               SHMEM_DEVICE_HEAP_SIZE="32M", SHMEM_DEVICE_SCRATCH_SIZE="384K", SHMEM_BARRIER_TIMEOUT="60")
+    code = ("import sys,os; sys.path[:0]=[%r,%r,%r]\n" % (HERE, os.path.join(os.path.dirname(HERE), "osss-gasnet_amd"),
+                                                          os.path.join(os.path.dirname(HERE), "oracle")) +
+            "import shmem_reduce\nshm=shmem_reduce.Shmem(); shm.init(); d=shm.malloc_device(1024)\n"
+            "pe=shm.my_pe()\n"
+            "shm.to_all('sum','double',d,d,10,0,0,2)\n"
+            "if pe==1: shm.to_all('sum','double',d,d,10,0,0,1)\n"
+            "else: shm.to_all('sum','double',d,d,10,0,0,2)\n")
+    procs = [subprocess.Popen([sys.executable, "-c", code], env=dict(env, SHMEM_PE=str(pe)),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for pe in range(2)]
+    outs = [p.communicate(timeout=120) for p in procs]
+    assert procs[1].returncode != 0 and "not in the active set" in outs[1][0]
+    assert procs[0].returncode != 0 and "aborting" in outs[0][0]
