@@ -99,17 +99,39 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    # timed region: K steps, barrier + device synchronize on both sides
     shm.barrier_all()
     shm.sync()
-    shm.kernel_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     shm.sync()
     t_local = time.perf_counter() - t0
     shm.barrier_all()
+
+    # kernel duration: the same K steps again with a HIP event pair attached to
+    # each dominant kernel launch (hipExtLaunchKernel stamps on the library's
+    # stream). Kept out of the region above: attaching events adds ~12 us of
+    # host-side latency per call (tools/overhead.py), not kernel time.
+    shm.kernel_timing(True)
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    shm.sync()
+    t_local_ev = time.perf_counter() - t1
+    shm.barrier_all()
     nk, k_total_ms, k_avg_ms = shm.kernel_timing_stats()
     shm.kernel_timing(False)
+
+    # the many-small-bucket regime (BASELINE config 5 shape: 64 KiB per call)
+    small_n, small_calls = 8192, 1000
+    for _ in range(20):
+        shm.to_all("sum", "double", dst, src, small_n, 0, 0, npes)
+    shm.barrier_all()
+    ts0 = time.perf_counter()
+    for _ in range(small_calls):
+        shm.to_all("sum", "double", dst, src, small_n, 0, 0, npes)
+    t_small = (time.perf_counter() - ts0) / small_calls
 
     # max over PEs, through the library's own host-staged double max reduction
     tbuf = np.array([t_local], dtype=np.float64)
@@ -145,7 +167,7 @@ def main():
     roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                 "kernel": kname, "alg_bytes_per_launch": alg_bytes, "kernel_avg_us": round(k_avg_ms * 1e3, 2),
-                "launches_timed": nk}
+                "launches_timed": nk, "ms_per_step_with_events": round(t_local_ev / args.steps * 1e3, 4)}
     traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(traffic_file):
         try:
@@ -176,6 +198,8 @@ def main():
             "per_pe_gib_s": round(S / t_step / GIB, 2),
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "small_call": {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small * 1e6, 2),
+                           "calls": small_calls, "note": "64 KiB shmem_double_sum_to_all back-to-back (PE 0 clock)"},
             "check": check,
         }
         print(json.dumps(out), flush=True)

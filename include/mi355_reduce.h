@@ -72,6 +72,12 @@ int mi355_combine (int op, int dtype, void *dst, const void *const *srcs,
 int mi355_copy_segments (void *const *dsts, const void *const *srcs,
                          const size_t *nbytes, int nseg, void *stream);
 
+/* Attach a pair of HIP events (hipEvent_t, created by the caller with timing
+ * enabled) to the NEXT kernel this layer launches from the calling thread:
+ * the runtime stamps that kernel's own start and end (hipExtLaunchKernel),
+ * adding no marker packet to the stream. NULL, NULL cancels. */
+void mi355_time_next_launch (void *start_event, void *stop_event);
+
 /* Shard i of nshards for n elements of elem_size bytes: the P2P schedule's
  * partition (contiguous, shard starts 256-byte aligned, trailing shards may
  * be empty). Host-only arithmetic, callable without a GPU. */

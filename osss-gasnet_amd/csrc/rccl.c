@@ -88,9 +88,9 @@ int shmemi_rccl_allreduce (int op, int dtype, const void *src, void *dst, size_t
     }
     void *comm = NULL;
     shmemi_rccl_comm (&comm);
-    shmemi_timed_begin ();
+    shmemi_timed_marker (0);
     ncclResult_t r = ncclAllReduce (src, dst, count, t, o, (ncclComm_t) comm, shmemi.stream);
-    shmemi_timed_end ();
+    shmemi_timed_marker (1);
     if (r != ncclSuccess)
         return -1;
     SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));

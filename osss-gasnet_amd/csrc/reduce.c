@@ -287,7 +287,7 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
     const size_t nbytes = n * es;
     const int kt = ptr_kind (target, nbytes), ks = ptr_kind (source, nbytes);
     if (kt != PK_HOST || ks != PK_HOST)
-        SHMEMI_HIP (hipDeviceSynchronize ()); /* the caller's kernels that wrote source are done */
+        shmemi_order_after_caller (s.size > 1);
 
     const int overlap = target != source && ranges_overlap ((size_t) target, (size_t) source, nbytes);
     const int use_rccl = shmemi.algorithm == SHMEMX_REDUCE_RCCL && s.size == shmemi.npes && s.size > 1 &&

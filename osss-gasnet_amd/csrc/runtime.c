@@ -35,6 +35,7 @@
 #include <unistd.h>
 
 #include "pshmem.h"
+#include "mi355_reduce.h"
 #include "shmem.h"
 #include "shmemx.h"
 #include "shmemi.h"
@@ -731,6 +732,19 @@ void shmemx_kernel_timing (int enable)
         shmemi.ntimed = 0;
 }
 
+/* Device-resident buffers: the caller's kernels that wrote them must be done
+ * before the reduction reads them (and, for PE_size > 1, before a peer GPU
+ * does after the barrier). hipDeviceSynchronize on an idle device costs next
+ * to nothing (tools/overhead.py: 13-14 us per 1-PE call with or without it),
+ * while recording an event on the legacy null stream costs 12-17 us. */
+void shmemi_order_after_caller (int host_wait)
+{
+    (void) host_wait;
+    SHMEMI_HIP (hipDeviceSynchronize ());
+}
+
+/* Kernel timing without marker packets: the next kernel the combine layer
+ * launches carries the event pair itself (hipExtLaunchKernel stamps). */
 void shmemi_timed_begin (void)
 {
     if (!shmemi.timing)
@@ -745,15 +759,30 @@ void shmemi_timed_begin (void)
         shmemi.ev = ev;
         shmemi.timed_cap = cap;
     }
-    SHMEMI_HIP (hipEventRecord (shmemi.ev[2 * shmemi.ntimed], shmemi.stream));
+    mi355_time_next_launch (shmemi.ev[2 * shmemi.ntimed], shmemi.ev[2 * shmemi.ntimed + 1]);
 }
 
 void shmemi_timed_end (void)
 {
     if (!shmemi.timing)
         return;
-    SHMEMI_HIP (hipEventRecord (shmemi.ev[2 * shmemi.ntimed + 1], shmemi.stream));
+    mi355_time_next_launch (NULL, NULL);
     shmemi.ntimed++;
+}
+
+/* For launches the combine layer does not make (ncclAllReduce): markers. */
+void shmemi_timed_marker (int end)
+{
+    if (!shmemi.timing)
+        return;
+    if (!end) {
+        shmemi_timed_begin ();
+        mi355_time_next_launch (NULL, NULL);
+        SHMEMI_HIP (hipEventRecord (shmemi.ev[2 * shmemi.ntimed], shmemi.stream));
+    } else {
+        SHMEMI_HIP (hipEventRecord (shmemi.ev[2 * shmemi.ntimed + 1], shmemi.stream));
+        shmemi.ntimed++;
+    }
 }
 
 void shmemx_kernel_timing_stats (long *launches, double *total_ms, double *avg_ms)

@@ -105,8 +105,10 @@ void shmemi_barrier_set (int PE_start, int stride, int PE_size);
 int shmemi_in_device_heap (const void *p, size_t nbytes);
 size_t shmemi_heap_offset (const void *p);
 void *shmemi_peer_ptr (int pe, size_t off);
+void shmemi_order_after_caller (int host_wait);
 void shmemi_timed_begin (void);
 void shmemi_timed_end (void);
+void shmemi_timed_marker (int end);
 int shmemi_rccl_comm (void **comm);
 
 #define SHMEMI_HIP(call) shmemi_hip_check ((call), #call)

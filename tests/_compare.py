@@ -18,10 +18,11 @@ def mismatches(got, want, op, dtype):
     eq = (oracle.as_value_bytes(got, dtype) == oracle.as_value_bytes(want, dtype)).all(axis=1)
     if dtype in FP and op in ("sum", "prod"):
         if dtype.startswith("complex"):
-            nan_ok = ((np.isnan(got.real) & np.isnan(want.real)) | (got.real.view(np.uint8).reshape(len(got), -1) ==
-                      want.real.view(np.uint8).reshape(len(want), -1)).all(axis=1)) & \
-                     ((np.isnan(got.imag) & np.isnan(want.imag)) | (got.imag.view(np.uint8).reshape(len(got), -1) ==
-                      want.imag.view(np.uint8).reshape(len(want), -1)).all(axis=1))
+            def part_ok(g, w):
+                g, w = np.ascontiguousarray(g), np.ascontiguousarray(w)
+                return (np.isnan(g) & np.isnan(w)) | (g.view(np.uint8).reshape(len(g), g.itemsize) ==
+                                                      w.view(np.uint8).reshape(len(w), w.itemsize)).all(axis=1)
+            nan_ok = part_ok(got.real, want.real) & part_ok(got.imag, want.imag)
         else:
             nan_ok = np.isnan(got) & np.isnan(want)
         eq = eq | nan_ok

@@ -64,9 +64,9 @@ def test_overlap_larger_than_scratch(shm):
     """Overlap handling is chunked through scratch (3 MiB here) in memmove order."""
     n = 3 << 20  # 24 MiB of doubles
     x = np.arange(n, dtype=np.float64)
-    base = shm.malloc_device((n + 1024) * 8)
+    base = shm.malloc_device((n + 2048) * 8)
     for delta in (777, -777):
-        src = base + 512 * 8
+        src = base + 1024 * 8
         shm.put(src, x)
         tgt = src + delta * 8
         shm.to_all("sum", "double", tgt, src, n, 0, 0, 1)
