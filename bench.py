@@ -67,6 +67,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--host", action="store_true",
+                    help="source/target in host memory (shmem_malloc, page-locked): the rate includes the "
+                         "H2D/D2H staging copies (DESIGN.md); not the headline metric")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -90,9 +93,16 @@ def main():
     shm.init()
     shm.set_algorithm(args.algorithm)
     me, npes = shm.my_pe(), shm.n_pes()
-    src = shm.malloc_device(S)
-    dst = shm.malloc_device(S)
-    shm.put(src, synth(me, np.arange(n, dtype=np.uint64)))
+    if args.host:
+        import ctypes
+        src, dst = shm.malloc(S), shm.malloc(S)
+        x = synth(me, np.arange(n, dtype=np.uint64))
+        ctypes.memmove(src, x.ctypes.data, S)
+        del x
+    else:
+        src = shm.malloc_device(S)
+        dst = shm.malloc_device(S)
+        shm.put(src, synth(me, np.arange(n, dtype=np.uint64)))
 
     def step():
         shm.to_all("sum", "double", dst, src, n, 0, 0, npes)
@@ -145,7 +155,12 @@ def main():
     check = "skipped"
     if not args.no_check:
         idx = np.unique(np.random.default_rng(me).integers(0, n, 1 << 16).astype(np.uint64))
-        got_full = shm.get(dst, n, "double")
+        if args.host:
+            import ctypes
+            got_full = np.empty(n)
+            ctypes.memmove(got_full.ctypes.data, dst, S)
+        else:
+            got_full = shm.get(dst, n, "double")
         got = got_full[idx.astype(np.int64)]
         import oracle
         srcs = [synth(p, idx) for p in range(npes)]
@@ -169,7 +184,7 @@ def main():
                 "kernel": kname, "alg_bytes_per_launch": alg_bytes, "kernel_avg_us": round(k_avg_ms * 1e3, 2),
                 "launches_timed": nk, "ms_per_step_with_events": round(t_local_ev / args.steps * 1e3, 4)}
     traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(traffic_file):
+    if os.path.exists(traffic_file) and not args.host:
         try:
             tr = json.load(open(traffic_file)).get(f"n{npes}_{args.mib}mib")
             if tr:
@@ -180,7 +195,8 @@ def main():
 
     if me == 0:
         out = {
-            "metric": "GiB/s reduced (device-resident), shmem_double_sum_to_all @256MiB, 1/2/4/8 GPU",
+            "metric": ("GiB/s reduced (host-staged incl. H2D/D2H), shmem_double_sum_to_all @256MiB" if args.host else
+                       "GiB/s reduced (device-resident), shmem_double_sum_to_all @256MiB, 1/2/4/8 GPU"),
             "value": round(npes * S / t_step / GIB, 2),
             "unit": "GiB/s",
             "n_gpus": npes,
@@ -193,7 +209,7 @@ def main():
             "dtype": "f64",
             "data": "synthetic (splitmix64 full-mantissa doubles, device-resident symmetric heap)",
             "config": {"workload": f"shmem_double_sum_to_all, {npes} PE = {npes} GPU, {args.mib} MiB "
-                                   f"device-resident array per PE", "nreduce": n, "bytes_per_pe": S,
+                                   f"{'host-memory (staged)' if args.host else 'device-resident'} array per PE", "nreduce": n, "bytes_per_pe": S,
                        "algorithm": args.algorithm, "parallelism": f"pe{npes}"},
             "per_pe_gib_s": round(S / t_step / GIB, 2),
             "roofline": roofline,
@@ -203,8 +219,12 @@ def main():
             "check": check,
         }
         print(json.dumps(out), flush=True)
-    shm.free_device(dst)
-    shm.free_device(src)
+    if args.host:
+        shm.free(dst)
+        shm.free(src)
+    else:
+        shm.free_device(dst)
+        shm.free_device(src)
     shm.finalize()
 
 

@@ -177,7 +177,7 @@ __device__ __forceinline__ void st16(u32x4 *p, u32x4 v) {
 // Vector path: every pointer 16-byte aligned. Each lane owns UNROLL vectors
 // spaced one block apart (so a wave touches contiguous 1 KiB per source per
 // step) and issues all NSRC*UNROLL loads before combining.
-template <int OP, typename T, int NSRC, int UNROLL>
+template <int OP, typename T, int NSRC, int UNROLL, int POL>
 __global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
     constexpr int V = 16 / sizeof(T);
     const u32x4 *s[NSRC];
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
             const uint64_t i = base + (uint64_t)u * kBlock;
             if (i < nvec) {
 #pragma unroll
-                for (int k = 0; k < NSRC; ++k) x[u][k].v = ld16<POL_NT>(s[k] + i);
+                for (int k = 0; k < NSRC; ++k) x[u][k].v = ld16<POL>(s[k] + i);
             }
         }
 #pragma unroll
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
 #pragma unroll
                     for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[u][k].e[e]);
                 }
-                st16<POL_NT>(d + i, acc.v);
+                st16<POL>(d + i, acc.v);
             }
         }
     }
@@ -321,18 +321,25 @@ int device_cus() {
 // kBlocksPerCU resident blocks per CU (grid-stride covers the rest).
 constexpr int kBlocksPerCU = 8;
 
-unsigned grid_for(uint64_t units_per_block_pass, uint64_t units) {
+unsigned grid_for(uint64_t units_per_block_pass, uint64_t units, int blocks_per_cu = kBlocksPerCU) {
     uint64_t want = (units + units_per_block_pass - 1) / units_per_block_pass;
-    uint64_t cap = (uint64_t)device_cus() * kBlocksPerCU;
+    uint64_t cap = (uint64_t)device_cus() * blocks_per_cu;
     if (want < 1) want = 1;
     return (unsigned)(want < cap ? want : cap);
 }
 
-// Loads in flight per lane ~ 8 x 16 B whatever NSRC is.
-template <int NSRC>
-constexpr int unroll_for() {
-    return NSRC == 1 ? 8 : NSRC == 2 ? 4 : NSRC <= 4 ? 2 : 1;
-}
+// Launch shape per source count, from tools/hbm_sweep.hip on MI355X (256 MiB
+// per source, fold of double sums; GB/s counts (k+1) x 256 MiB):
+//   k=2: 4 vectors/lane, 1 block/CU, non-temporal loads      6.56 TB/s
+//   k=3: 2 vectors/lane, 1 block/CU, non-temporal both       6.28 TB/s
+//   k=4: 1 vector/lane,  2 blocks/CU, non-temporal both      6.18 TB/s
+//   k=8: 1 vector/lane,  2 blocks/CU, non-temporal both      5.85 TB/s
+// Fewer, fuller blocks beat 8 blocks/CU by 5-10 % on every k.
+template <int NSRC> struct Shape {
+    static constexpr int unroll = NSRC == 2 ? 4 : NSRC == 3 ? 2 : 1;
+    static constexpr int blocks_per_cu = NSRC <= 3 ? 1 : 2;
+    static constexpr int policy = NSRC == 2 ? POL_NT_LOAD : POL_NT;
+};
 
 template <int OP, typename T, int NSRC>
 int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st) {
@@ -345,11 +352,11 @@ int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st) {
     }
     constexpr int V = 16 / sizeof(T);
     if ((orbits & 15) == 0) {
-        constexpr int U = unroll_for<NSRC>();
+        using S = Shape<NSRC>;
         p.nvec = n / V;
         p.tail = (uint32_t)(n % V);
-        const unsigned grid = grid_for((uint64_t)kBlock * U, p.nvec);
-        return launch(combine_vec<OP, T, NSRC, U>, dim3(grid), st, p);
+        const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, S::blocks_per_cu);
+        return launch(combine_vec<OP, T, NSRC, S::unroll, S::policy>, dim3(grid), st, p);
     }
     p.nvec = n;
     p.tail = 0;
