@@ -1,0 +1,36 @@
+"""A C program written against the reference's API builds and links against
+libshmem_reduce.so (CPU), and runs on 1 and 3 PEs (GPU)."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIBDIR = os.path.join(ROOT, "osss-gasnet_amd", "lib")
+
+
+def build(tmp_path):
+    exe = str(tmp_path / "reduce_example")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "examples", "reduce_example.c"), "-L", LIBDIR, "-lshmem_reduce",
+                    f"-Wl,-rpath,{LIBDIR}", "-o", exe], check=True)
+    return exe
+
+
+def test_c_program_compiles_and_links(tmp_path):
+    exe = build(tmp_path)
+    out = subprocess.check_output(["nm", "-u", exe], text=True)
+    assert "shmem_int_sum_to_all" in out and "shmem_double_max_to_all" in out
+
+
+@pytest.mark.gpu
+@pytest.mark.multipe
+@pytest.mark.parametrize("npes", [1, 3])
+def test_c_program_runs(tmp_path, npes):
+    exe = build(tmp_path)
+    env = dict(os.environ, SHMEM_DEVICE_HEAP_SIZE="16M", SHMEM_DEVICE_SCRATCH_SIZE="3M")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "oshrun"), "-np", str(npes), "--same-device",
+                        exe], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count(": ok") == npes, r.stdout
