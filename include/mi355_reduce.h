@@ -78,6 +78,19 @@ int mi355_copy_segments (void *const *dsts, const void *const *srcs,
  * adding no marker packet to the stream. NULL, NULL cancels. */
 void mi355_time_next_launch (void *start_event, void *stop_event);
 
+/* Attach a completion signal to the NEXT kernel this layer launches from the
+ * calling thread: when every block of it has finished and its stores are
+ * written back to memory, one lane stores `epoch` to *flag (system scope).
+ * `count` is a 4-byte device word holding 0 (the kernel leaves it at 0);
+ * `flag` a device-visible pointer to host-coherent memory (hipHostMalloc
+ * coherent + mapped). The host spins on *flag instead of synchronizing the
+ * stream. Pass NULL flag to cancel. */
+void mi355_signal_next_launch (unsigned *count, unsigned *flag, unsigned epoch);
+
+/* Launch a one-block kernel whose only job is to carry the armed signal:
+ * the host learns that everything queued on `stream` before it is done. */
+int mi355_signal_launch (void *stream);
+
 /* Shard i of nshards for n elements of elem_size bytes: the P2P schedule's
  * partition (contiguous, shard starts 256-byte aligned, trailing shards may
  * be empty). Host-only arithmetic, callable without a GPU. */

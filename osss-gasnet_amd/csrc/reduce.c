@@ -44,24 +44,42 @@ struct aset {
 
 static int aset_pe (const struct aset *s, int i) { return s->start + i * s->stride; }
 
-static void combine_or_die (int op, int dtype, void *dst, const void *const *srcs, int nsrc, size_t n)
+/* Launch the fold and wait for its completion signal (the kernel's last
+ * block writes a host-coherent word; ~4 us sooner than a stream sync). */
+static void combine_wait (int op, int dtype, void *dst, const void *const *srcs, int nsrc, size_t n, int timed)
 {
-    shmemi_timed_begin ();
+    if (timed)
+        shmemi_timed_begin ();
+    shmemi_arm_signal ();
     int rc = mi355_combine (op, dtype, dst, srcs, nsrc, n, shmemi.stream);
-    shmemi_timed_end ();
+    if (timed)
+        shmemi_timed_end ();
     if (rc != 0)
         shmemi_fatal ("combine kernel launch failed (op %d, dtype %d, %d sources, %zu elements): %d",
                       op, dtype, nsrc, n, rc);
+    shmemi_wait_signal ();
 }
 
-static void copy_or_die (void *const *dsts, const void *const *srcs, const size_t *nbytes, int nseg)
+/* Byte copies, 64 segments per launch; the last launch carries the signal. */
+static void copy_wait (void *const *dsts, const void *const *srcs, const size_t *nbytes, int nseg, int timed)
 {
+    if (nseg <= 0)
+        return;
     for (int base = 0; base < nseg; base += 64) {
-        int k = nseg - base < 64 ? nseg - base : 64;
+        const int k = nseg - base < 64 ? nseg - base : 64;
+        const int last = base + k == nseg;
+        if (last) {
+            if (timed)
+                shmemi_timed_begin ();
+            shmemi_arm_signal ();
+        }
         int rc = mi355_copy_segments (dsts + base, srcs + base, nbytes + base, k, shmemi.stream);
+        if (last && timed)
+            shmemi_timed_end ();
         if (rc != 0)
             shmemi_fatal ("copy kernel launch failed: %d", rc);
     }
+    shmemi_wait_signal ();
 }
 
 static void sync_stream (void) { SHMEMI_HIP (hipStreamSynchronize (shmemi.stream)); }
@@ -90,15 +108,11 @@ void mi355_shard_bounds (size_t n, size_t es, int size, int i, size_t *lo, size_
 static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
                        const struct aset *s)
 {
-    const void *srcs[SHMEMI_MAX_PES > 64 ? 64 : SHMEMI_MAX_PES];
-    const void **sp = srcs;
-    const void **heap_srcs = NULL;
-    if (s->size > 64) {
-        heap_srcs = (const void **) malloc (sizeof (void *) * (size_t) s->size);
-        if (heap_srcs == NULL)
-            shmemi_fatal ("out of host memory");
-        sp = heap_srcs;
-    }
+    const void **sp = (const void **) malloc (sizeof (void *) * (size_t) s->size);
+    void **dsts = (void **) malloc (sizeof (void *) * (size_t) s->size);
+    size_t *nb = (size_t *) malloc (sizeof (size_t) * (size_t) s->size);
+    if (sp == NULL || dsts == NULL || nb == NULL)
+        shmemi_fatal ("out of host memory");
     size_t lo, hi;
     mi355_shard_bounds (n, es, s->size, s->me, &lo, &hi);
 
@@ -106,15 +120,11 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
     if (hi > lo) {
         for (int i = 0; i < s->size; ++i)
             sp[i] = shmemi_peer_ptr (aset_pe (s, i), src_off + lo * es);
-        combine_or_die (op, dtype, shmemi_peer_ptr (shmemi.mype, dst_off + lo * es), sp, s->size, hi - lo);
-        sync_stream ();
+        combine_wait (op, dtype, shmemi_peer_ptr (shmemi.mype, dst_off + lo * es), sp, s->size, hi - lo, 1);
     }
     shmemi_barrier_set (s->start, s->stride, s->size); /* every shard is reduced */
 
-    /* gather the other members' shards from their targets */
-    void *dsts[64];
-    const void *gsrc[64];
-    size_t nb[64];
+    /* gather the other members' shards from their targets: one launch */
     int k = 0;
     for (int i = 0; i < s->size; ++i) {
         if (i == s->me)
@@ -124,24 +134,20 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
         if (h <= l)
             continue;
         dsts[k] = shmemi_peer_ptr (shmemi.mype, dst_off + l * es);
-        gsrc[k] = shmemi_peer_ptr (aset_pe (s, i), dst_off + l * es);
+        sp[k] = shmemi_peer_ptr (aset_pe (s, i), dst_off + l * es);
         nb[k] = (h - l) * es;
-        if (++k == 64) {
-            copy_or_die (dsts, gsrc, nb, k);
-            k = 0;
-        }
+        ++k;
     }
-    if (k > 0)
-        copy_or_die (dsts, gsrc, nb, k);
-    sync_stream ();
+    copy_wait (dsts, sp, nb, k, 0);
     shmemi_barrier_set (s->start, s->stride, s->size); /* peers are done reading us */
-    free (heap_srcs);
+    free (nb);
+    free (dsts);
+    free (sp);
 }
 
 /* EXACT: fold everything in this PE's reference order into dst; dst must
  * not overlap any source (callers route overlaps through scratch). */
-static void exact_into (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
-                        const struct aset *s)
+static void exact_into (int op, int dtype, size_t dst_off, size_t src_off, size_t n, const struct aset *s)
 {
     const void **sp = (const void **) malloc (sizeof (void *) * (size_t) s->size);
     if (sp == NULL)
@@ -151,10 +157,8 @@ static void exact_into (int op, int dtype, size_t es, size_t dst_off, size_t src
     for (int i = 0; i < s->size; ++i)
         if (i != s->me)
             sp[k++] = shmemi_peer_ptr (aset_pe (s, i), src_off);
-    combine_or_die (op, dtype, shmemi_peer_ptr (shmemi.mype, dst_off), sp, s->size, n);
-    sync_stream ();
+    combine_wait (op, dtype, shmemi_peer_ptr (shmemi.mype, dst_off), sp, s->size, n, 1);
     free (sp);
-    (void) es;
 }
 
 /* timed: the copy is the call's dominant kernel (the PE_size == 1 identity) */
@@ -163,11 +167,7 @@ static void copy_local (size_t dst_off, size_t src_off, size_t nbytes, int timed
     void *d = shmemi_peer_ptr (shmemi.mype, dst_off);
     const void *sv = shmemi_peer_ptr (shmemi.mype, src_off);
     size_t nb = nbytes;
-    if (timed)
-        shmemi_timed_begin ();
-    copy_or_die (&d, &sv, &nb, 1);
-    if (timed)
-        shmemi_timed_end ();
+    copy_wait (&d, &sv, &nb, 1, timed);
 }
 
 /* Reduce n elements at symmetric offsets. Handles aliasing like the
@@ -187,7 +187,6 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
             return;
         if (!overlap) {
             copy_local (dst_off, src_off, nbytes, 1);
-            sync_stream ();
             return;
         }
     } else if (!exact && (same || !overlap)) {
@@ -195,7 +194,7 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
         return;
     } else if (exact && !overlap) {
         shmemi_barrier_set (s->start, s->stride, s->size);
-        exact_into (op, dtype, es, dst_off, src_off, n, s);
+        exact_into (op, dtype, dst_off, src_off, n, s);
         shmemi_barrier_set (s->start, s->stride, s->size);
         return;
     }
@@ -216,11 +215,10 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
             p2p_range (op, dtype, es, tmp_off, src_off + b * es, cn, s);
         } else {
             shmemi_barrier_set (s->start, s->stride, s->size);
-            exact_into (op, dtype, es, tmp_off, src_off + b * es, cn, s);
+            exact_into (op, dtype, tmp_off, src_off + b * es, cn, s);
             shmemi_barrier_set (s->start, s->stride, s->size);
         }
         copy_local (dst_off + b * es, tmp_off, cn * es, 0);
-        sync_stream ();
         /* nobody reads our target chunk; the next chunk's first barrier orders
          * our write before any peer reads the source bytes it may cover */
     }

@@ -65,6 +65,7 @@ struct shmemi_state {
     int algorithm;              /* enum shmemx_reduce_algorithm */
     double barrier_timeout;     /* seconds */
     int debug;
+    int entry_sync;             /* SHMEM_ENTRY_SYNC: hipDeviceSynchronize on entry */
 
     /* bootstrap */
     struct shmemi_seg *seg;
@@ -88,6 +89,11 @@ struct shmemi_state {
     /* RCCL */
     void *rccl_comm;            /* ncclComm_t of the whole world, lazily */
 
+    /* completion signal: host-coherent word the last block of a kernel writes */
+    unsigned *sig_flag;         /* hipHostMalloc coherent+mapped, same address on both sides */
+    unsigned *sig_count;        /* device word, 0 between launches */
+    unsigned sig_epoch;
+
     /* kernel timing */
     int timing;
     int ntimed;
@@ -106,6 +112,8 @@ int shmemi_in_device_heap (const void *p, size_t nbytes);
 size_t shmemi_heap_offset (const void *p);
 void *shmemi_peer_ptr (int pe, size_t off);
 void shmemi_order_after_caller (int host_wait);
+void shmemi_arm_signal (void);
+void shmemi_wait_signal (void);
 void shmemi_timed_begin (void);
 void shmemi_timed_end (void);
 void shmemi_timed_marker (int end);

@@ -68,6 +68,17 @@ class Shmem:
     def __init__(self, path=LIB_PATH):
         self.lib = load(path)
         self._psync = np.full(SHMEM_REDUCE_SYNC_SIZE, SHMEM_SYNC_VALUE, dtype=np.int64)
+        self._psync_ptr = self._psync.ctypes.data
+        self._fns = {}
+
+    def _reduction(self, op, dtype):
+        f = self._fns.get((op, dtype))
+        if f is None:
+            f = getattr(self.lib, f"shmem_{dtype}_{op}_to_all")
+            f.restype = None
+            f.argtypes = [_vp, _vp, _i, _i, _i, _i, _vp, _vp]
+            self._fns[(op, dtype)] = f
+        return f
 
     # ---- runtime
     def init(self):
@@ -118,12 +129,9 @@ class Shmem:
                pWrk=None, pSync=None):
         if PE_size is None:
             PE_size = self.n_pes()
-        f = getattr(self.lib, f"shmem_{dtype}_{op}_to_all")
-        f.restype = None
-        f.argtypes = [_vp, _vp, _i, _i, _i, _i, _vp, _vp]
         if pSync is None:
-            pSync = self._psync.ctypes.data
-        f(target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync)
+            pSync = self._psync_ptr
+        self._reduction(op, dtype)(target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync)
 
     # ---- the combine layer (include/mi355_reduce.h)
     def combine(self, op, dtype, dst, srcs, n, stream=None):

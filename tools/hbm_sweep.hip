@@ -21,12 +21,15 @@ typedef double f64x2 __attribute__((ext_vector_type(2)));
 
 template <int POL>
 __device__ __forceinline__ u32x4 ld(const u32x4 *p) {
-    if constexpr (POL & 1) return __builtin_nontemporal_load(p);
+    if constexpr ((POL < 4 || POL == 7) && (POL & 1)) return __builtin_nontemporal_load(p);
     else return *p;
 }
 template <int POL>
 __device__ __forceinline__ void st(u32x4 *p, u32x4 v) {
-    if constexpr (POL & 2) __builtin_nontemporal_store(v, p);
+    if constexpr (POL == 4) asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 5) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 6 || POL == 7) asm volatile("global_store_dwordx4 %0, %1, off nt sc1" :: "v"(p), "v"(v) : "memory");
+    else if constexpr (POL & 2) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
 
@@ -144,31 +147,18 @@ int main(int argc, char **argv) {
     double us_memcpy = time_it([&] { CHECK(hipMemcpyAsync(bufs[1], bufs[0], bytes, hipMemcpyDeviceToDevice, 0)); }, 20);
     printf("hipMemcpyAsync D2D %zu MiB: %.1f us  %.0f GB/s (read+write)\n", mib, us_memcpy, 2.0 * bytes / (us_memcpy * 1e-6) / 1e9);
 
-    run_copy<256, 8, 2>(bufs[0], bufs[1], nvec, bytes);
-    run_copy<256, 12, 2>(bufs[0], bufs[1], nvec, bytes);
-    run_copy<256, 16, 2>(bufs[0], bufs[1], nvec, bytes);
-    run_copy<512, 8, 2>(bufs[0], bufs[1], nvec, bytes);
-    run_copy<256, 4, 2>(bufs[0], bufs[1], nvec, bytes);
-    run_copy<1024, 4, 2>(bufs[0], bufs[1], nvec, bytes);
-
+    run_copy<256, 8, 6>(bufs[0], bufs[1], nvec, bytes);
+    run_copy<256, 8, 7>(bufs[0], bufs[1], nvec, bytes);
     const u32x4 *srcs[8];
     for (int k = 0; k < 8; ++k) srcs[k] = bufs[k];
-    run_fold<256, 4, 2, 2>(srcs, bufs[8], nvec, bytes);
     run_fold<256, 4, 2, 1>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 4, 2, 3>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 8, 2, 2>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 8, 2, 3>(srcs, bufs[8], nvec, bytes);
+    run_fold<256, 4, 2, 7>(srcs, bufs[8], nvec, bytes);
     run_fold<256, 2, 3, 3>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 2, 3, 2>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 4, 3, 3>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 2, 4, 2>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 2, 4, 3>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 4, 4, 3>(srcs, bufs[8], nvec, bytes);
+    run_fold<256, 2, 3, 7>(srcs, bufs[8], nvec, bytes);
     run_fold<256, 1, 4, 3>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 1, 8, 2>(srcs, bufs[8], nvec, bytes);
+    run_fold<256, 1, 4, 7>(srcs, bufs[8], nvec, bytes);
     run_fold<256, 1, 8, 3>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 2, 8, 3>(srcs, bufs[8], nvec, bytes);
-    run_fold<512, 1, 8, 3>(srcs, bufs[8], nvec, bytes);
+    run_fold<256, 1, 8, 7>(srcs, bufs[8], nvec, bytes);
 
     std::sort(results.begin(), results.end(), [](const Res &a, const Res &b) {
         int c = strcmp(a.name, b.name);
