@@ -82,8 +82,6 @@ static void copy_wait (void *const *dsts, const void *const *srcs, const size_t 
     shmemi_wait_signal ();
 }
 
-static void sync_stream (void) { SHMEMI_HIP (hipStreamSynchronize (shmemi.stream)); }
-
 static int ranges_overlap (size_t a, size_t b, size_t nbytes)
 {
     return a < b + nbytes && b < a + nbytes;
@@ -250,6 +248,67 @@ static int ptr_kind (const void *p, size_t nbytes)
     return PK_HOST;
 }
 
+/* Buffers outside the device heap: stream them through scratch in chunks,
+ * double-buffered so the copy-in of chunk k+1 (stream in) and the copy-out of
+ * chunk k-1 (stream out) run while chunk k is reduced: with host buffers the
+ * two PCIe directions then work at the same time.
+ *   A0/A1 = halves of scratch A (sources), B0/B1 = halves of scratch B (results)
+ * PE_size == 1 is the identity: each chunk goes in to A and straight back out. */
+static void staged (int op, int dtype, const char *fn, void *target, const void *source, size_t n,
+                    const struct aset *s, int ks, int kt, int use_rccl)
+{
+    const size_t es = mi355_dtype_size (dtype);
+    const size_t half = shmemi.scratch_chunk / 2 / SHMEMI_ALIGN * SHMEMI_ALIGN;
+    const size_t per = half / es;
+    const size_t nchunks = (n + per - 1) / per;
+    const size_t a_off[2] = {shmemi.scratch_off, shmemi.scratch_off + half};
+    const size_t b_off[2] = {shmemi.scratch_off + shmemi.scratch_chunk,
+                             shmemi.scratch_off + shmemi.scratch_chunk + half};
+    const hipMemcpyKind in_kind = ks == PK_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
+    const hipMemcpyKind out_kind = kt == PK_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    const int identity = s->size == 1;
+
+#define CHUNK_N(k) (n - (k) * per < per ? n - (k) * per : per)
+    for (size_t k = 0; k < nchunks + 1; ++k) {
+        /* copy-in of chunk k (issued one chunk ahead of its reduction) */
+        if (k < nchunks) {
+            const int j = (int) (k & 1);
+            if (k >= 2) /* A[j] was last read by the copy-out (identity) or reduction of chunk k-2 */
+                SHMEMI_HIP (hipStreamWaitEvent (shmemi.stream_in, shmemi.ev_out[j], 0));
+            SHMEMI_HIP (hipMemcpyAsync (shmemi.heap + a_off[j], (const char *) source + k * per * es,
+                                        CHUNK_N (k) * es, in_kind, shmemi.stream_in));
+            SHMEMI_HIP (hipEventRecord (shmemi.ev_in[j], shmemi.stream_in));
+        }
+        if (k == 0)
+            continue;
+        /* reduce and copy out chunk c = k - 1 */
+        const size_t c = k - 1;
+        const int j = (int) (c & 1);
+        const size_t cn = CHUNK_N (c);
+        size_t out_off = a_off[j];
+        if (identity) {
+            SHMEMI_HIP (hipStreamWaitEvent (shmemi.stream_out, shmemi.ev_in[j], 0));
+        } else {
+            SHMEMI_HIP (hipEventSynchronize (shmemi.ev_in[j])); /* peers read A[j] after the barrier */
+            if (c >= 2) /* B[j] is still being copied out for chunk c-2 */
+                SHMEMI_HIP (hipStreamWaitEvent (shmemi.stream, shmemi.ev_out[j], 0));
+            out_off = b_off[j];
+            if (use_rccl) {
+                if (shmemi_rccl_allreduce (op, dtype, shmemi.heap + a_off[j], shmemi.heap + b_off[j], cn) != 0)
+                    shmemi_fatal ("%s: ncclAllReduce failed", fn);
+            } else {
+                reduce_symmetric (op, dtype, es, b_off[j], a_off[j], cn, s);
+            }
+        }
+        SHMEMI_HIP (hipMemcpyAsync ((char *) target + c * per * es, shmemi.heap + out_off, cn * es, out_kind,
+                                    shmemi.stream_out));
+        SHMEMI_HIP (hipEventRecord (shmemi.ev_out[j], shmemi.stream_out));
+    }
+#undef CHUNK_N
+    SHMEMI_HIP (hipStreamSynchronize (shmemi.stream_out));
+    SHMEMI_HIP (hipStreamSynchronize (shmemi.stream_in));
+}
+
 static void reduce_impl (int op, int dtype, const char *fn, void *target, const void *source,
                          int nreduce, int PE_start, int logPE_stride, int PE_size, long *pSync)
 {
@@ -300,29 +359,7 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
         return;
     }
 
-    /* staged: source -> scratch A, reduce into scratch B, B -> target */
-    const size_t a_off = shmemi.scratch_off, b_off = shmemi.scratch_off + shmemi.scratch_chunk;
-    const size_t per = shmemi.scratch_chunk / es;
-    for (size_t b = 0; b < n; b += per) {
-        const size_t cn = n - b < per ? n - b : per;
-        const hipMemcpyKind in_kind = ks == PK_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
-        const hipMemcpyKind out_kind = kt == PK_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
-        SHMEMI_HIP (hipMemcpyAsync (shmemi.heap + a_off, (const char *) source + b * es, cn * es, in_kind,
-                                    shmemi.stream));
-        sync_stream ();
-        size_t out_off = b_off;
-        if (s.size == 1) {
-            out_off = a_off; /* identity: copy straight back out */
-        } else if (use_rccl) {
-            if (shmemi_rccl_allreduce (op, dtype, shmemi.heap + a_off, shmemi.heap + b_off, cn) != 0)
-                shmemi_fatal ("%s: ncclAllReduce failed", fn);
-        } else {
-            reduce_symmetric (op, dtype, es, b_off, a_off, cn, &s);
-        }
-        SHMEMI_HIP (hipMemcpyAsync ((char *) target + b * es, shmemi.heap + out_off, cn * es, out_kind,
-                                    shmemi.stream));
-        sync_stream ();
-    }
+    staged (op, dtype, fn, target, source, n, &s, ks, kt, use_rccl);
 }
 
 /* ---------------------------------------------------------------------- */

@@ -612,6 +612,12 @@ void pshmem_init (void)
     SHMEMI_HIP (hipSetDevice (shmemi.device));
     /* blocking: ordered after the null stream, see shmemi_order_after_caller */
     SHMEMI_HIP (hipStreamCreateWithFlags (&shmemi.stream, hipStreamDefault));
+    SHMEMI_HIP (hipStreamCreateWithFlags (&shmemi.stream_in, hipStreamDefault));
+    SHMEMI_HIP (hipStreamCreateWithFlags (&shmemi.stream_out, hipStreamDefault));
+    for (int i = 0; i < 2; ++i) {
+        SHMEMI_HIP (hipEventCreateWithFlags (&shmemi.ev_in[i], hipEventDisableTiming));
+        SHMEMI_HIP (hipEventCreateWithFlags (&shmemi.ev_out[i], hipEventDisableTiming));
+    }
     heap_init ();
     signal_init ();
 
@@ -683,8 +689,15 @@ void pshmem_finalize (void)
         shmemi.ev = NULL;
         shmemi.timed_cap = 0;
     }
-    if (shmemi.stream != NULL)
+    if (shmemi.stream != NULL) {
+        for (int i = 0; i < 2; ++i) {
+            (void) hipEventDestroy (shmemi.ev_in[i]);
+            (void) hipEventDestroy (shmemi.ev_out[i]);
+        }
+        (void) hipStreamDestroy (shmemi.stream_in);
+        (void) hipStreamDestroy (shmemi.stream_out);
         (void) hipStreamDestroy (shmemi.stream);
+    }
     shmemi.stream = NULL;
     if (shmemi.seg != NULL) {
         munmap (shmemi.seg, shmemi.seg_size);

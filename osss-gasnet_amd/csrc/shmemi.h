@@ -62,6 +62,8 @@ struct shmemi_state {
     int mype, npes;
     int device;
     hipStream_t stream;
+    hipStream_t stream_in, stream_out;  /* staging copies (blocking streams) */
+    hipEvent_t ev_in[2], ev_out[2];
     int algorithm;              /* enum shmemx_reduce_algorithm */
     double barrier_timeout;     /* seconds */
     int debug;
