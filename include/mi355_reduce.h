@@ -91,6 +91,40 @@ void mi355_signal_next_launch (unsigned *count, unsigned *flag, unsigned epoch);
  * the host learns that everything queued on `stream` before it is done. */
 int mi355_signal_launch (void *stream);
 
+/* ---- one-launch P2P reduction for small messages (fused.hip) ----
+ * Signal region: per PE, MI355_SIG_WORDS 8-byte words of uncached device
+ * memory mapped into every peer; all zero before first use. */
+#define MI355_FUSED_MAX_MEMBERS 32
+#define MI355_FUSED_MAX_BLOCKS 256
+#define MI355_SIG_ARRIVE 0       /* [PE]: pair count of the last call the PE arrived at */
+#define MI355_SIG_RSDONE 1024    /* [PE]: ... whose shard the PE has reduced           */
+#define MI355_SIG_AGDONE 2048    /* [PE]: ... whose gather the PE has finished         */
+#define MI355_SIG_RS_COUNT 3072  /* local block counters (own 128-byte lines)          */
+#define MI355_SIG_AG_COUNT 3088
+#define MI355_SIG_ERROR 3104
+#define MI355_SIG_WORDS 3120
+
+typedef struct MI355FusedArgs {
+    int op, dtype;
+    int nmembers, me;                 /* active-set size, this PE's index in it   */
+    unsigned long long n;             /* elements                                 */
+    unsigned long long shard;         /* elements per shard; shard*esize % 16 == 0 */
+    const void *src[MI355_FUSED_MAX_MEMBERS];        /* members' sources (mapped) */
+    void *dst[MI355_FUSED_MAX_MEMBERS];              /* members' targets (mapped) */
+    unsigned long long *sig[MI355_FUSED_MAX_MEMBERS];/* members' signal regions   */
+    unsigned long long count[MI355_FUSED_MAX_MEMBERS]; /* pair count per member  */
+    int pe[MI355_FUSED_MAX_MEMBERS];  /* members' PE numbers (signal slot index)  */
+    unsigned *host_flag;              /* host-coherent completion word            */
+    unsigned epoch;                   /* stored there when done (| 1u<<31: timeout) */
+    unsigned long long timeout_ticks; /* bound on every wait, 100 MHz ticks       */
+} MI355FusedArgs;
+
+/* Reduce-scatter + all-gather of n elements over the members in ONE launch:
+ * every member ends with the fold, in member order, of all members' sources
+ * (the reference's result on the first member). Every member must make the
+ * matching call; buffers 16-byte aligned; dst == src or disjoint. */
+int mi355_fused_allreduce (const MI355FusedArgs *args, void *stream);
+
 /* Shard i of nshards for n elements of elem_size bytes: the P2P schedule's
  * partition (contiguous, shard starts 256-byte aligned, trailing shards may
  * be empty). Host-only arithmetic, callable without a GPU. */

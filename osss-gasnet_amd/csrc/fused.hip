@@ -1,0 +1,254 @@
+// fused.hip -- the whole P2P reduction of a small message in ONE launch.
+//
+// The multi-launch schedule (reduce.c) pays, per call, three host barriers and
+// three launch/completion round trips (~6.5 us each on MI355X). For the
+// many-small-bucket regime (BASELINE config 5: 4096 x 64 KiB on 8 GPUs) that
+// fixed cost is the whole call. Here every cross-PE step is a device-side
+// flag exchange instead, through each PE's signal region (uncached device
+// memory, mapped into every peer over xGMI), and the host waits once:
+//
+//   arrive   lane q of block 0 stores this call's pair count into member q's
+//            ARRIVE[my PE]; every block waits until ARRIVE[q] holds member
+//            q's count for every member (its source is ready: the kernel runs
+//            after the work queued before it on the same stream), then
+//            acquires at system scope (invalidates this CU's stale lines)
+//   reduce   fold shard `me` of every member's source, in active-set order
+//            (the reference's PE_start order), into this PE's target shard,
+//            with system-scope write-through stores
+//   rsdone   the last block of the grid publishes RSDONE[my PE] to every
+//            member; every block waits for all members' RSDONE, acquires
+//   gather   copy the other members' shards from their targets
+//   agdone   the last block publishes AGDONE, waits for every member's AGDONE
+//            (nobody reads this PE's buffers any more) and stores the call's
+//            epoch to the host-coherent flag
+//
+// Pair counts instead of a reset protocol: PE p's slot for PE q only ever
+// grows by one per reduction both take part in, so a member that runs ahead
+// into the next call can never satisfy a wait of the current one too early
+// (the same argument as the host barrier in runtime.c).
+//
+// All blocks of the grid must be co-resident (they wait on each other's last
+// block): the grid is at most kFusedMaxBlocks, far below one block per CU.
+// Every wait is bounded by p.timeout_ticks of the 100 MHz real-time counter.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ops.h"
+
+namespace {
+
+using namespace mi355;
+
+constexpr int kBlock = 256;
+
+__device__ __forceinline__ void st_sys_u64(unsigned long long *p, unsigned long long v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ unsigned long long ld_sys_u64(const unsigned long long *p) {
+    return __hip_atomic_load(const_cast<unsigned long long *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+// 16-byte store, write-through to memory at system scope: a peer reads it
+// over xGMI after the flag that follows it
+__device__ __forceinline__ void st16_sys(u32x4 *p, u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+}
+
+// Wait until slot `base + pe[i]` of this PE's signal region holds count[i]
+// for every member i; lanes i < nmembers of wave 0 poll one member each.
+__device__ bool wait_members(const MI355FusedArgs &a, const unsigned long long *mine, int base, bool include_self) {
+    bool ok = true;
+    if (threadIdx.x < 64) {
+        const int i = threadIdx.x;
+        bool need = i < a.nmembers && (include_self || i != a.me);
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        unsigned spins = 0;
+        while (true) {
+            bool done = !need || ld_sys_u64(mine + base + a.pe[i]) >= a.count[i];
+            if (__all(done)) break;
+            if ((++spins & 63u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+                ok = false;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (i == 0) {
+            // acquire at system scope: drop this CU's stale copies of peer data
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    return ok;
+}
+
+// Count this block in on a local counter; true for the grid's last block.
+__device__ bool last_block(unsigned long long *counter) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    __shared__ int is_last;
+    if (threadIdx.x == 0) {
+        const uint64_t prev = __hip_atomic_fetch_add(counter, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        is_last = prev + 1 == gridDim.x;
+        if (is_last) st_sys_u64(counter, 0);
+    }
+    __syncthreads();
+    return is_last != 0;
+}
+
+__device__ void publish(const MI355FusedArgs &a, int base) {
+    // lanes of wave 0: one member each (this PE included)
+    if (threadIdx.x < a.nmembers)
+        st_sys_u64(a.sig[threadIdx.x] + base + a.pe[a.me], a.count[threadIdx.x]);
+}
+
+template <int OP, typename T>
+__global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
+    constexpr int V = 16 / sizeof(T);
+    unsigned long long *mine = a.sig[a.me];
+    __shared__ int ok_all;
+    if (threadIdx.x == 0) ok_all = 1;
+
+    // ---- arrive
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < a.nmembers && threadIdx.x != a.me)
+            st_sys_u64(a.sig[threadIdx.x] + MI355_SIG_ARRIVE + a.pe[a.me], a.count[threadIdx.x]);
+    }
+    __syncthreads();
+    if (!wait_members(a, mine, MI355_SIG_ARRIVE, false)) ok_all = 0;
+    __syncthreads();
+    if (!ok_all) goto fail;
+
+    {
+        // ---- reduce shard `me`
+        const uint64_t lo = (uint64_t)a.me * a.shard;
+        const uint64_t hi = lo + a.shard < a.n ? lo + a.shard : a.n;
+        if (hi > lo) {
+            const uint64_t nv = (hi - lo) / V;
+            const int nm = a.nmembers;
+            u32x4 *d = (u32x4 *)((char *)a.dst[a.me] + lo * sizeof(T));
+            for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < nv;
+                 v += (uint64_t)gridDim.x * kBlock) {
+                Pack<T> acc, x;
+                acc.v = ((const u32x4 *)((const char *)a.src[0] + lo * sizeof(T)))[v];
+                for (int k = 1; k < nm; ++k) {
+                    x.v = ((const u32x4 *)((const char *)a.src[k] + lo * sizeof(T)))[v];
+#pragma unroll
+                    for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x.e[e]);
+                }
+                st16_sys(d + v, acc.v);
+            }
+            const uint64_t tail0 = lo + nv * V;
+            if (tail0 < hi && blockIdx.x == 0 && threadIdx.x < hi - tail0) {
+                const uint64_t i = tail0 + threadIdx.x;
+                T acc = ((const T *)a.src[0])[i];
+                for (int k = 1; k < nm; ++k) acc = apply<OP>(acc, ((const T *)a.src[k])[i]);
+                ((T *)a.dst[a.me])[i] = acc;
+            }
+            if (tail0 < hi && blockIdx.x == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // plain tail stores
+            }
+        }
+        if (last_block(mine + MI355_SIG_RS_COUNT)) publish(a, MI355_SIG_RSDONE);
+
+        // ---- every shard is reduced
+        if (!wait_members(a, mine, MI355_SIG_RSDONE, true)) ok_all = 0;
+        __syncthreads();
+        if (!ok_all) goto fail;
+
+        // ---- gather the other shards: one grid-stride loop over all of them
+        const uint64_t shard_v = a.shard / V;  // a.shard is a multiple of V
+        const uint64_t total_v = shard_v * (uint64_t)a.nmembers;
+        bool tail_plain = false;
+        for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < total_v;
+             g += (uint64_t)gridDim.x * kBlock) {
+            const int j = (int)(g / shard_v);
+            if (j == a.me) continue;
+            const uint64_t e0 = (uint64_t)j * a.shard + (g - (uint64_t)j * shard_v) * V;
+            if (e0 >= a.n) continue;
+            if (e0 + V <= a.n) {
+                const u32x4 v = *(const u32x4 *)((const char *)a.dst[j] + e0 * sizeof(T));
+                st16_sys((u32x4 *)((char *)a.dst[a.me] + e0 * sizeof(T)), v);
+            } else {
+                for (uint64_t e = e0; e < a.n; ++e) ((T *)a.dst[a.me])[e] = ((const T *)a.dst[j])[e];
+                tail_plain = true;
+            }
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (__syncthreads_or(tail_plain) && threadIdx.x == 0)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the element tail went through L2
+        if (last_block(mine + MI355_SIG_AG_COUNT)) {
+            publish(a, MI355_SIG_AGDONE);
+            __syncthreads();
+            const bool ok = wait_members(a, mine, MI355_SIG_AGDONE, true);
+            if (threadIdx.x == 0) {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __hip_atomic_store(a.host_flag, ok ? a.epoch : (a.epoch | 0x80000000u), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+        }
+        return;
+    }
+fail:
+    if (threadIdx.x == 0) {
+        st_sys_u64(mine + MI355_SIG_ERROR, 1);
+        __hip_atomic_store(a.host_flag, a.epoch | 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+template <typename T>
+int launch_op(const MI355FusedArgs &a, unsigned grid, hipStream_t st) {
+    switch (a.op) {
+#define CASE(O)                                                                        \
+    case O:                                                                            \
+        if constexpr (valid_pair<O, T>()) {                                           \
+            hipLaunchKernelGGL((fused_allreduce<O, T>), dim3(grid), dim3(kBlock), 0, st, a); \
+            break;                                                                     \
+        } else {                                                                       \
+            return MI355_E_UNSUP;                                                      \
+        }
+        CASE(MI355_OP_SUM)
+        CASE(MI355_OP_PROD)
+        CASE(MI355_OP_AND)
+        CASE(MI355_OP_OR)
+        CASE(MI355_OP_XOR)
+        CASE(MI355_OP_MIN)
+        CASE(MI355_OP_MAX)
+#undef CASE
+    default: return MI355_E_INVAL;
+    }
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+}  // namespace
+
+extern "C" int mi355_fused_allreduce(const MI355FusedArgs *a, void *stream) {
+    if (a == nullptr || !mi355_op_supported(a->op, a->dtype)) return MI355_E_UNSUP;
+    if (a->nmembers < 2 || a->nmembers > MI355_FUSED_MAX_MEMBERS || a->me < 0 || a->me >= a->nmembers)
+        return MI355_E_INVAL;
+    const size_t es = mi355_dtype_size(a->dtype);
+    if (a->shard == 0 || (a->shard * es) % 16 != 0 || a->host_flag == nullptr) return MI355_E_INVAL;
+    for (int i = 0; i < a->nmembers; ++i)
+        if (a->src[i] == nullptr || a->dst[i] == nullptr || a->sig[i] == nullptr ||
+            (((uintptr_t)a->src[i] | (uintptr_t)a->dst[i]) & 15) != 0)
+            return MI355_E_INVAL;
+    // enough blocks for the larger of the two legs, all of them co-resident
+    const uint64_t vecs = (a->shard * es / 16) * (uint64_t)(a->nmembers - 1);
+    uint64_t grid = (vecs + kBlock - 1) / kBlock;
+    if (grid < 1) grid = 1;
+    if (grid > MI355_FUSED_MAX_BLOCKS) grid = MI355_FUSED_MAX_BLOCKS;
+    hipStream_t st = (hipStream_t)stream;
+    switch (a->dtype) {
+    case MI355_SHORT: return launch_op<int16_t>(*a, (unsigned)grid, st);
+    case MI355_INT: return launch_op<int32_t>(*a, (unsigned)grid, st);
+    case MI355_LONG:
+    case MI355_LONGLONG: return launch_op<int64_t>(*a, (unsigned)grid, st);
+    case MI355_FLOAT: return launch_op<float>(*a, (unsigned)grid, st);
+    case MI355_DOUBLE: return launch_op<double>(*a, (unsigned)grid, st);
+    case MI355_LONGDOUBLE: return launch_op<x80>(*a, (unsigned)grid, st);
+    case MI355_COMPLEXF: return launch_op<cplxf>(*a, (unsigned)grid, st);
+    case MI355_COMPLEXD: return launch_op<cplxd>(*a, (unsigned)grid, st);
+    default: return MI355_E_INVAL;
+    }
+}

@@ -87,12 +87,19 @@ static int ranges_overlap (size_t a, size_t b, size_t nbytes)
     return a < b + nbytes && b < a + nbytes;
 }
 
-/* Shard bounds of member i for n elements of es bytes over `size` members. */
-void mi355_shard_bounds (size_t n, size_t es, int size, int i, size_t *lo, size_t *hi)
+/* Elements per shard: ceil(n / size) rounded up so every shard starts on a
+ * 256-byte boundary. */
+static size_t shard_chunk (size_t n, size_t es, int size)
 {
     size_t align = es >= 256 ? 1 : 256 / es;
     size_t chunk = (n + (size_t) size - 1) / (size_t) size;
-    chunk = (chunk + align - 1) / align * align;
+    return (chunk + align - 1) / align * align;
+}
+
+/* Shard bounds of member i for n elements of es bytes over `size` members. */
+void mi355_shard_bounds (size_t n, size_t es, int size, int i, size_t *lo, size_t *hi)
+{
+    const size_t chunk = shard_chunk (n, es, size);
     size_t l = (size_t) i * chunk;
     *lo = l < n ? l : n;
     *hi = l + chunk < n ? l + chunk : n;
@@ -143,6 +150,46 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
     free (sp);
 }
 
+/* The fused one-launch schedule (fused.hip) applies: small enough, few
+ * enough members, 16-byte aligned symmetric offsets, dst == src or disjoint. */
+static int fused_eligible (size_t es, size_t dst_off, size_t src_off, size_t n, const struct aset *s)
+{
+    return s->size > 1 && s->size <= MI355_FUSED_MAX_MEMBERS && n * es <= shmemi.fused_max &&
+           shmemi.sigmem != NULL && ((dst_off | src_off) & 15) == 0 && es <= 256 &&
+           (dst_off == src_off || !ranges_overlap (dst_off, src_off, n * es)) &&
+           shmemi.algorithm != SHMEMX_REDUCE_EXACT;
+}
+
+static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
+                         const struct aset *s)
+{
+    MI355FusedArgs a;
+    memset (&a, 0, sizeof a);
+    a.op = op;
+    a.dtype = dtype;
+    a.nmembers = s->size;
+    a.me = s->me;
+    a.n = n;
+    a.shard = shard_chunk (n, es, s->size);
+    for (int i = 0; i < s->size; ++i) {
+        const int pe = aset_pe (s, i);
+        a.pe[i] = pe;
+        a.src[i] = shmemi_peer_ptr (pe, src_off);
+        a.dst[i] = shmemi_peer_ptr (pe, dst_off);
+        a.sig[i] = shmemi.peer_sig[pe];
+        a.count[i] = ++shmemi.fused_count[pe];
+    }
+    a.host_flag = shmemi.sig_flag;
+    a.epoch = shmemi_next_epoch ();
+    a.timeout_ticks = (unsigned long long) (shmemi.barrier_timeout * 1e8);
+    const int rc = mi355_fused_allreduce (&a, shmemi.stream);
+    if (rc != 0)
+        shmemi_fatal ("fused reduction launch failed (op %d, dtype %d, %d PEs, %zu elements): %d", op, dtype,
+                      s->size, n, rc);
+    if (shmemi_wait_flag (a.epoch) != a.epoch)
+        shmemi_fatal ("fused reduction timed out waiting for the other PEs of the active set");
+}
+
 /* EXACT: fold everything in this PE's reference order into dst; dst must
  * not overlap any source (callers route overlaps through scratch). */
 static void exact_into (int op, int dtype, size_t dst_off, size_t src_off, size_t n, const struct aset *s)
@@ -188,7 +235,10 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
             return;
         }
     } else if (!exact && (same || !overlap)) {
-        p2p_range (op, dtype, es, dst_off, src_off, n, s);
+        if (fused_eligible (es, dst_off, src_off, n, s))
+            fused_range (op, dtype, es, dst_off, src_off, n, s);
+        else
+            p2p_range (op, dtype, es, dst_off, src_off, n, s);
         return;
     } else if (exact && !overlap) {
         shmemi_barrier_set (s->start, s->stride, s->size);
@@ -343,8 +393,11 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
         shmemi_fatal ("%s: NULL target or source", fn);
     const size_t nbytes = n * es;
     const int kt = ptr_kind (target, nbytes), ks = ptr_kind (source, nbytes);
+    /* the fused kernel learns on the device that peers' sources are ready */
+    const int fused = kt == PK_DEV_SYM && ks == PK_DEV_SYM &&
+                      fused_eligible (es, shmemi_heap_offset (target), shmemi_heap_offset (source), n, &s);
     if (kt != PK_HOST || ks != PK_HOST)
-        shmemi_order_after_caller (s.size > 1);
+        shmemi_order_after_caller (s.size > 1 && !fused);
 
     const int overlap = target != source && ranges_overlap ((size_t) target, (size_t) source, nbytes);
     const int use_rccl = shmemi.algorithm == SHMEMX_REDUCE_RCCL && s.size == shmemi.npes && s.size > 1 &&

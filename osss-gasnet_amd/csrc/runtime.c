@@ -352,27 +352,41 @@ static void signal_init (void)
     shmemi.sig_epoch = 0;
 }
 
+/* Epochs live in the low 31 bits; bit 31 marks a kernel-side timeout. */
+unsigned shmemi_next_epoch (void)
+{
+    shmemi.sig_epoch = (shmemi.sig_epoch + 1) & 0x7fffffffu;
+    if (shmemi.sig_epoch == 0)
+        shmemi.sig_epoch = 1;
+    return shmemi.sig_epoch;
+}
+
 /* Arm the completion signal for the next kernel the combine layer launches. */
 void shmemi_arm_signal (void)
 {
-    if (++shmemi.sig_epoch == 0)
-        shmemi.sig_epoch = 1;
-    mi355_signal_next_launch (shmemi.sig_count, shmemi.sig_flag, shmemi.sig_epoch);
+    mi355_signal_next_launch (shmemi.sig_count, shmemi.sig_flag, shmemi_next_epoch ());
 }
 
-/* Wait for the armed kernel's last block. A kernel that faults never
- * signals: the stream is polled now and then so its error surfaces. */
 void shmemi_wait_signal (void)
 {
-    const unsigned want = shmemi.sig_epoch;
+    if (shmemi_wait_flag (shmemi.sig_epoch) != shmemi.sig_epoch)
+        shmemi_fatal ("kernel reported a timeout");
+}
+
+/* Wait until the host-coherent flag carries `want` (in its low 31 bits) and
+ * return it. A kernel that faults never signals: the stream is polled now and
+ * then so its error surfaces. */
+unsigned shmemi_wait_flag (unsigned want)
+{
     unsigned spins = 0;
     double t0 = 0.0;
-    while (__atomic_load_n (shmemi.sig_flag, __ATOMIC_ACQUIRE) != want) {
+    unsigned v;
+    while (((v = __atomic_load_n (shmemi.sig_flag, __ATOMIC_ACQUIRE)) & 0x7fffffffu) != want) {
         if ((++spins & 4095u) == 0) {
             hipError_t e = hipStreamQuery (shmemi.stream);
             if (e != hipSuccess && e != hipErrorNotReady)
                 shmemi_fatal ("kernel failed: %s", hipGetErrorString (e));
-            if (e == hipSuccess && __atomic_load_n (shmemi.sig_flag, __ATOMIC_ACQUIRE) != want)
+            if (e == hipSuccess && (__atomic_load_n (shmemi.sig_flag, __ATOMIC_ACQUIRE) & 0x7fffffffu) != want)
                 shmemi_fatal ("stream drained but the completion signal %u never arrived", want);
             if (t0 == 0.0)
                 t0 = now_s ();
@@ -383,6 +397,25 @@ void shmemi_wait_signal (void)
             __builtin_ia32_pause ();
         }
     }
+    return v;
+}
+
+/* Signal region of the fused kernel: uncached (fine-grained) device memory,
+ * so peers' stores over xGMI and this GPU's polls meet in memory. */
+static void sigmem_init (void)
+{
+    void *p = NULL;
+    const size_t bytes = 65536;
+    _Static_assert (MI355_SIG_WORDS * 8 <= 65536, "signal region too small");
+    SHMEMI_HIP (hipExtMallocWithFlags (&p, bytes, hipDeviceMallocUncached));
+    SHMEMI_HIP (hipMemset (p, 0, bytes));
+    SHMEMI_HIP (hipDeviceSynchronize ());
+    shmemi.sigmem = (unsigned long long *) p;
+    shmemi.peer_sig = (unsigned long long **) calloc ((size_t) shmemi.npes, sizeof (void *));
+    shmemi.fused_count = (unsigned long long *) calloc ((size_t) shmemi.npes, sizeof (unsigned long long));
+    if (shmemi.peer_sig == NULL || shmemi.fused_count == NULL)
+        shmemi_fatal ("out of host memory");
+    shmemi.peer_sig[shmemi.mype] = shmemi.sigmem;
 }
 
 /* Publish this PE's heap and map every peer's (after the info barrier). */
@@ -394,6 +427,7 @@ static void heap_exchange (void)
     if (hipDeviceGetPCIBusId (me->pci_bus_id, (int) sizeof me->pci_bus_id, shmemi.device) != hipSuccess)
         me->pci_bus_id[0] = '\0';
     SHMEMI_HIP (hipIpcGetMemHandle (&me->heap_handle, shmemi.heap));
+    SHMEMI_HIP (hipIpcGetMemHandle (&me->sig_handle, shmemi.sigmem));
     me->heap_size = shmemi.heap_size;
     __atomic_store_n (&me->published, 1, __ATOMIC_RELEASE);
     shmemi_barrier_set (0, 1, shmemi.npes);
@@ -427,6 +461,11 @@ static void heap_exchange (void)
             shmemi_fatal ("hipIpcOpenMemHandle for PE %d (GPU %s) failed: %s", pe,
                           pi->pci_bus_id, hipGetErrorString (e));
         shmemi.peer_heap[pe] = (char *) p;
+        p = NULL;
+        e = hipIpcOpenMemHandle (&p, pi->sig_handle, hipIpcMemLazyEnablePeerAccess);
+        if (e != hipSuccess)
+            shmemi_fatal ("hipIpcOpenMemHandle (signal region) for PE %d failed: %s", pe, hipGetErrorString (e));
+        shmemi.peer_sig[pe] = (unsigned long long *) p;
     }
     shmemi_barrier_set (0, 1, shmemi.npes);
 }
@@ -620,6 +659,8 @@ void pshmem_init (void)
     }
     heap_init ();
     signal_init ();
+    sigmem_init ();
+    shmemi.fused_max = env_size ("SHMEM_FUSED_MAX_BYTES", (size_t) 1 << 20);
 
     if (shmemi.npes > 1) {
         bootstrap_attach ();
@@ -655,9 +696,12 @@ void pshmem_finalize (void)
         shmemi_rccl_destroy ();
     }
     if (shmemi.peer_heap != NULL) {
-        for (int pe = 0; pe < shmemi.npes; ++pe)
+        for (int pe = 0; pe < shmemi.npes; ++pe) {
             if (pe != shmemi.mype && shmemi.peer_heap[pe] != NULL)
                 (void) hipIpcCloseMemHandle (shmemi.peer_heap[pe]);
+            if (pe != shmemi.mype && shmemi.peer_sig != NULL && shmemi.peer_sig[pe] != NULL)
+                (void) hipIpcCloseMemHandle (shmemi.peer_sig[pe]);
+        }
         /* the peers may still read this heap until they have closed theirs */
         shmem_barrier_all ();
         free (shmemi.peer_heap);
@@ -676,6 +720,13 @@ void pshmem_finalize (void)
     if (shmemi.heap != NULL)
         (void) hipFree (shmemi.heap);
     shmemi.heap = NULL;
+    if (shmemi.sigmem != NULL)
+        (void) hipFree (shmemi.sigmem);
+    shmemi.sigmem = NULL;
+    free (shmemi.peer_sig);
+    free (shmemi.fused_count);
+    shmemi.peer_sig = NULL;
+    shmemi.fused_count = NULL;
     if (shmemi.sig_flag != NULL)
         (void) hipHostFree (shmemi.sig_flag);
     if (shmemi.sig_count != NULL)

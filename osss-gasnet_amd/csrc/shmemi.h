@@ -27,6 +27,7 @@ struct shmemi_pe_info {
     int32_t device;
     char pci_bus_id[32];
     hipIpcMemHandle_t heap_handle;
+    hipIpcMemHandle_t sig_handle;
     uint64_t heap_size;
     int32_t published;
     int32_t pad;
@@ -91,6 +92,12 @@ struct shmemi_state {
     /* RCCL */
     void *rccl_comm;            /* ncclComm_t of the whole world, lazily */
 
+    /* signal region for the fused kernel: uncached device memory, mapped by peers */
+    unsigned long long *sigmem;
+    unsigned long long **peer_sig;  /* [npes] */
+    unsigned long long *fused_count;/* [npes]: fused reductions shared with each PE */
+    size_t fused_max;           /* SHMEM_FUSED_MAX_BYTES: largest message on the fused path */
+
     /* completion signal: host-coherent word the last block of a kernel writes */
     unsigned *sig_flag;         /* hipHostMalloc coherent+mapped, same address on both sides */
     unsigned *sig_count;        /* device word, 0 between launches */
@@ -116,6 +123,8 @@ void *shmemi_peer_ptr (int pe, size_t off);
 void shmemi_order_after_caller (int host_wait);
 void shmemi_arm_signal (void);
 void shmemi_wait_signal (void);
+unsigned shmemi_next_epoch (void);
+unsigned shmemi_wait_flag (unsigned epoch);
 void shmemi_timed_begin (void);
 void shmemi_timed_end (void);
 void shmemi_timed_marker (int end);

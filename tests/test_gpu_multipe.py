@@ -85,15 +85,19 @@ SOME = [("sum", "double"), ("sum", "float"), ("xor", "int"), ("and", "longlong")
         ("min", "short"), ("prod", "complexd"), ("sum", "longdouble")]
 
 
-def test_four_pes_all_44_pairs_p2p_and_exact(tmp_path):
+@pytest.mark.parametrize("fused_max", ["1M", "0"], ids=["fused", "multi-launch"])
+def test_four_pes_all_44_pairs_p2p_and_exact(tmp_path, fused_max):
+    """Every pair on 4 PEs, through the one-launch fused kernel (messages up to
+    1 MiB) and through the multi-launch shard schedule (fused path disabled)."""
     cases = []
     cases += make_cases(oracle.PAIRS, 1000, [[0, 0, 4]], "dev", "p2p", 0)
     cases += make_cases(oracle.PAIRS, 257, [[0, 0, 4]], "dev", "exact", 100)
-    results = run_pes(4, cases, tmp_path)
+    results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_FUSED_MAX_BYTES": fused_max})
     check(results, cases)
 
 
-def test_four_pes_modes_and_active_sets(tmp_path):
+@pytest.mark.parametrize("fused_max", ["1M", "0"], ids=["fused", "multi-launch"])
+def test_four_pes_modes_and_active_sets(tmp_path, fused_max):
     cases = []
     cid = 1000
     for mode, alg in itertools.product(["inplace", "overlap_up", "overlap_down", "host", "unaligned"],
@@ -110,7 +114,7 @@ def test_four_pes_modes_and_active_sets(tmp_path):
     # edge sizes: nothing, one element, fewer elements than PEs x alignment
     for n in (0, 1, 3, 64):
         cases += make_cases([("sum", "double"), ("or", "short")], n, [[0, 0, 4]], "dev", "p2p", cid); cid += 100
-    results = run_pes(4, cases, tmp_path)
+    results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_FUSED_MAX_BYTES": fused_max})
     check(results, cases)
 
 
@@ -126,6 +130,8 @@ def test_eight_pes_one_gpu(tmp_path):
     cases = make_cases([("sum", "double"), ("and", "longlong"), ("max", "float")], 20000, [[0, 0, 8]],
                        "dev", "p2p", 0)
     cases += make_cases([("sum", "double")], 20000, [[0, 1, 4], [1, 1, 4]], "dev", "p2p", 100)
+    # above the fused limit: the multi-launch schedule, in the same run
+    cases += make_cases([("sum", "double"), ("xor", "int")], 300000, [[0, 0, 8]], "dev", "p2p", 200)
     results = run_pes(8, cases, tmp_path)
     check(results, cases)
 
