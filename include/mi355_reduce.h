@@ -102,7 +102,8 @@ int mi355_signal_launch (void *stream);
 #define MI355_SIG_RS_COUNT 3072  /* local block counters (own 128-byte lines)          */
 #define MI355_SIG_AG_COUNT 3088
 #define MI355_SIG_ERROR 3104
-#define MI355_SIG_WORDS 3120
+#define MI355_SIG_SELFTEST 3200  /* [PE]: init-time interconnect check */
+#define MI355_SIG_WORDS 4224
 
 typedef struct MI355FusedArgs {
     int op, dtype;
@@ -124,6 +125,12 @@ typedef struct MI355FusedArgs {
  * (the reference's result on the first member). Every member must make the
  * matching call; buffers 16-byte aligned; dst == src or disjoint. */
 int mi355_fused_allreduce (const MI355FusedArgs *args, void *stream);
+
+/* One-block kernels for the init-time interconnect check: store `value` to
+ * each of n (peer-mapped) words at system scope; load n words at system scope
+ * into out[] (device memory). n <= 1024. */
+int mi355_poke (unsigned long long *const *dst, int n, unsigned long long value, void *stream);
+int mi355_peek (const unsigned long long *const *src, int n, unsigned long long *out, void *stream);
 
 /* Shard i of nshards for n elements of elem_size bytes: the P2P schedule's
  * partition (contiguous, shard starts 256-byte aligned, trailing shards may

@@ -221,7 +221,48 @@ int launch_op(const MI355FusedArgs &a, unsigned grid, hipStream_t st) {
     return e == hipSuccess ? 0 : (int)e;
 }
 
+constexpr int kMaxPoke = 1024;
+struct PokeParams {
+    unsigned long long *ptr[kMaxPoke];
+    unsigned long long value;
+    unsigned long long *out;
+    int n;
+};
+
+__global__ __launch_bounds__(kBlock) void poke_kernel(PokeParams p) {
+    for (int i = threadIdx.x; i < p.n; i += kBlock) st_sys_u64(p.ptr[i], p.value);
+}
+
+__global__ __launch_bounds__(kBlock) void peek_kernel(PokeParams p) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    for (int i = threadIdx.x; i < p.n; i += kBlock) p.out[i] = ld_sys_u64(p.ptr[i]);
+}
+
 }  // namespace
+
+extern "C" int mi355_poke(unsigned long long *const *dst, int n, unsigned long long value, void *stream) {
+    if (n < 0 || n > kMaxPoke || (n > 0 && dst == nullptr)) return MI355_E_INVAL;
+    if (n == 0) return 0;
+    PokeParams p{};
+    for (int i = 0; i < n; ++i) p.ptr[i] = dst[i];
+    p.value = value;
+    p.n = n;
+    hipLaunchKernelGGL(poke_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, p);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+extern "C" int mi355_peek(const unsigned long long *const *src, int n, unsigned long long *out, void *stream) {
+    if (n < 0 || n > kMaxPoke || (n > 0 && (src == nullptr || out == nullptr))) return MI355_E_INVAL;
+    if (n == 0) return 0;
+    PokeParams p{};
+    for (int i = 0; i < n; ++i) p.ptr[i] = const_cast<unsigned long long *>(src[i]);
+    p.out = out;
+    p.n = n;
+    hipLaunchKernelGGL(peek_kernel, dim3(1), dim3(kBlock), 0, (hipStream_t)stream, p);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
 
 extern "C" int mi355_fused_allreduce(const MI355FusedArgs *a, void *stream) {
     if (a == nullptr || !mi355_op_supported(a->op, a->dtype)) return MI355_E_UNSUP;

@@ -50,7 +50,7 @@ struct shmemi_hostblk {
 };
 
 #define SEG_MAGIC 0x4d49333535534d45ull /* "MI355SME" */
-#define SEG_VERSION 1
+#define SEG_VERSION 2
 
 static double now_s (void)
 {
@@ -470,6 +470,84 @@ static void heap_exchange (void)
     shmemi_barrier_set (0, 1, shmemi.npes);
 }
 
+/* Interconnect check at init (PE_size > 1): every PE stores a value into
+ * every peer's signal region over the peer mapping (what the fused kernel's
+ * flags do) and reads a marker from every peer's heap (what the reduce-scatter
+ * does). All PEs learn every PE's outcome through the bootstrap segment and
+ * take the same decision: signal stores not seen -> fused path off;
+ * peer heap reads wrong -> RCCL schedule (or a loud failure without it). */
+static void interconnect_selftest (void)
+{
+    const int np = shmemi.npes, me = shmemi.mype;
+    if (np > 1024)
+        return;
+    const size_t mark_off = shmemi.scratch_off + 3 * shmemi.scratch_chunk - 8;
+    const unsigned long long mark = 0x5E1F7E5700000000ull + (unsigned long long) me;
+    SHMEMI_HIP (hipMemcpy (shmemi.heap + mark_off, &mark, 8, hipMemcpyHostToDevice));
+    shmemi_barrier_set (0, 1, np);
+
+    unsigned long long **ptrs = (unsigned long long **) calloc ((size_t) np, sizeof (void *));
+    unsigned long long *host = (unsigned long long *) calloc ((size_t) np, sizeof (unsigned long long));
+    unsigned long long *dev = NULL;
+    if (ptrs == NULL || host == NULL)
+        shmemi_fatal ("out of host memory");
+    SHMEMI_HIP (hipMalloc ((void **) &dev, sizeof (unsigned long long) * (size_t) np));
+    int k = 0;
+    for (int q = 0; q < np; ++q)
+        if (q != me)
+            ptrs[k++] = shmemi.peer_sig[q] + MI355_SIG_SELFTEST + me;
+    if (mi355_poke (ptrs, k, 0xA11CE00000000000ull + (unsigned long long) me, shmemi.stream) != 0)
+        shmemi_fatal ("self-test poke launch failed");
+    SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    shmemi_barrier_set (0, 1, np);
+
+    int sig_ok = 1, heap_ok = 1;
+    for (int q = 0; q < np; ++q)
+        ptrs[q] = shmemi.sigmem + MI355_SIG_SELFTEST + q;
+    if (mi355_peek ((const unsigned long long *const *) ptrs, np, dev, shmemi.stream) != 0)
+        shmemi_fatal ("self-test peek launch failed");
+    SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    SHMEMI_HIP (hipMemcpy (host, dev, sizeof (unsigned long long) * (size_t) np, hipMemcpyDeviceToHost));
+    for (int q = 0; q < np; ++q)
+        if (q != me && host[q] != 0xA11CE00000000000ull + (unsigned long long) q)
+            sig_ok = 0;
+    for (int q = 0; q < np; ++q)
+        ptrs[q] = (unsigned long long *) (shmemi.peer_heap[q] + mark_off);
+    if (mi355_peek ((const unsigned long long *const *) ptrs, np, dev, shmemi.stream) != 0)
+        shmemi_fatal ("self-test peek launch failed");
+    SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    SHMEMI_HIP (hipMemcpy (host, dev, sizeof (unsigned long long) * (size_t) np, hipMemcpyDeviceToHost));
+    for (int q = 0; q < np; ++q)
+        if (host[q] != 0x5E1F7E5700000000ull + (unsigned long long) q)
+            heap_ok = 0;
+    (void) hipFree (dev);
+    free (host);
+    free (ptrs);
+
+    __atomic_store_n (&seg_info (me)->selftest, sig_ok | (heap_ok << 1), __ATOMIC_RELEASE);
+    shmemi_barrier_set (0, 1, np);
+    int all_sig = 1, all_heap = 1;
+    for (int q = 0; q < np; ++q) {
+        const int r = __atomic_load_n (&seg_info (q)->selftest, __ATOMIC_ACQUIRE);
+        all_sig &= r & 1;
+        all_heap &= (r >> 1) & 1;
+    }
+    if (!all_sig) {
+        if (me == 0)
+            fprintf (stderr, "[shmem] warning: peer signal-region stores are not visible; "
+                             "the fused small-message kernel is disabled\n");
+        shmemi.fused_max = 0;
+    }
+    if (!all_heap) {
+        if (me == 0)
+            fprintf (stderr, "[shmem] warning: peer heap reads returned wrong data; "
+                             "using the RCCL schedule\n");
+        shmemi.algorithm = SHMEMX_REDUCE_RCCL;
+        shmemi.p2p_broken = 1;
+    }
+    shmemi_barrier_set (0, 1, np);
+}
+
 void *shmemx_malloc_device (size_t size)
 {
     shmemi_init_check ("shmemx_malloc_device");
@@ -665,6 +743,7 @@ void pshmem_init (void)
     if (shmemi.npes > 1) {
         bootstrap_attach ();
         heap_exchange ();
+        interconnect_selftest ();
         if (shmemi.mype == 0 && !shmemi.seg_unlinked) {
             shm_unlink (shmemi.seg_name); /* every PE is attached: drop the name */
             shmemi.seg_unlinked = 1;

@@ -30,7 +30,7 @@ struct shmemi_pe_info {
     hipIpcMemHandle_t sig_handle;
     uint64_t heap_size;
     int32_t published;
-    int32_t pad;
+    int32_t selftest;           /* bit 0: signal region stores seen, bit 1: heap reads ok */
 };
 
 struct shmemi_seg {
@@ -69,6 +69,7 @@ struct shmemi_state {
     double barrier_timeout;     /* seconds */
     int debug;
     int entry_sync;             /* SHMEM_ENTRY_SYNC: hipDeviceSynchronize on entry */
+    int p2p_broken;             /* init self-test: peer heap reads failed */
 
     /* bootstrap */
     struct shmemi_seg *seg;
