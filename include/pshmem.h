@@ -27,6 +27,43 @@ void pshmem_barrier_all (void);
 void pshmem_barrier (int PE_start, int logPE_stride, int PE_size, long *pSync);
 void pshmem_quiet (void);
 
+void pshmem_putmem (void *dest, const void *src, size_t nelems, int pe);
+void pshmem_getmem (void *dest, const void *src, size_t nelems, int pe);
+void pshmem_put32 (void *dest, const void *src, size_t nelems, int pe);
+void pshmem_put64 (void *dest, const void *src, size_t nelems, int pe);
+void pshmem_put128 (void *dest, const void *src, size_t nelems, int pe);
+void pshmem_get32 (void *dest, const void *src, size_t nelems, int pe);
+void pshmem_get64 (void *dest, const void *src, size_t nelems, int pe);
+void pshmem_get128 (void *dest, const void *src, size_t nelems, int pe);
+void pshmem_char_put (char *dest, const char *src, size_t nelems, int pe);
+void pshmem_short_put (short *dest, const short *src, size_t nelems, int pe);
+void pshmem_int_put (int *dest, const int *src, size_t nelems, int pe);
+void pshmem_long_put (long *dest, const long *src, size_t nelems, int pe);
+void pshmem_longlong_put (long long *dest, const long long *src, size_t nelems, int pe);
+void pshmem_longdouble_put (long double *dest, const long double *src, size_t nelems, int pe);
+void pshmem_double_put (double *dest, const double *src, size_t nelems, int pe);
+void pshmem_float_put (float *dest, const float *src, size_t nelems, int pe);
+void pshmem_char_get (char *dest, const char *src, size_t nelems, int pe);
+void pshmem_short_get (short *dest, const short *src, size_t nelems, int pe);
+void pshmem_int_get (int *dest, const int *src, size_t nelems, int pe);
+void pshmem_long_get (long *dest, const long *src, size_t nelems, int pe);
+void pshmem_longlong_get (long long *dest, const long long *src, size_t nelems, int pe);
+void pshmem_longdouble_get (long double *dest, const long double *src, size_t nelems, int pe);
+void pshmem_double_get (double *dest, const double *src, size_t nelems, int pe);
+void pshmem_float_get (float *dest, const float *src, size_t nelems, int pe);
+void pshmem_broadcast64 (void *target, const void *source, size_t nelems, int PE_root, int PE_start,
+                         int logPE_stride, int PE_size, long *pSync);
+void pshmem_broadcast32 (void *target, const void *source, size_t nelems, int PE_root, int PE_start,
+                         int logPE_stride, int PE_size, long *pSync);
+void pshmem_fcollect64 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                        int PE_size, long *pSync);
+void pshmem_fcollect32 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                        int PE_size, long *pSync);
+void pshmem_collect64 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                       int PE_size, long *pSync);
+void pshmem_collect32 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                       int PE_size, long *pSync);
+
     void pshmem_short_sum_to_all (short *target, short *source,
             int nreduce, int PE_start, int logPE_stride, int PE_size,
             short *pWrk, long *pSync);

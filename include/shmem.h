@@ -73,6 +73,50 @@ void shmem_barrier_all (void);
 void shmem_barrier (int PE_start, int logPE_stride, int PE_size, long *pSync);
 void shmem_quiet (void);
 
+/* ---- one-sided put/get (reference src/shmem.h:395-470); the remote
+ *      address must be in the device symmetric heap (shmemx_malloc_device) ---- */
+void shmem_putmem (void *dest, const void *src, size_t nelems, int pe);
+void shmem_getmem (void *dest, const void *src, size_t nelems, int pe);
+void shmem_put32 (void *dest, const void *src, size_t nelems, int pe);
+void shmem_put64 (void *dest, const void *src, size_t nelems, int pe);
+void shmem_put128 (void *dest, const void *src, size_t nelems, int pe);
+void shmem_get32 (void *dest, const void *src, size_t nelems, int pe);
+void shmem_get64 (void *dest, const void *src, size_t nelems, int pe);
+void shmem_get128 (void *dest, const void *src, size_t nelems, int pe);
+void shmem_char_put (char *dest, const char *src, size_t nelems, int pe);
+void shmem_short_put (short *dest, const short *src, size_t nelems, int pe);
+void shmem_int_put (int *dest, const int *src, size_t nelems, int pe);
+void shmem_long_put (long *dest, const long *src, size_t nelems, int pe);
+void shmem_longlong_put (long long *dest, const long long *src, size_t nelems, int pe);
+void shmem_longdouble_put (long double *dest, const long double *src, size_t nelems, int pe);
+void shmem_double_put (double *dest, const double *src, size_t nelems, int pe);
+void shmem_float_put (float *dest, const float *src, size_t nelems, int pe);
+void shmem_char_get (char *dest, const char *src, size_t nelems, int pe);
+void shmem_short_get (short *dest, const short *src, size_t nelems, int pe);
+void shmem_int_get (int *dest, const int *src, size_t nelems, int pe);
+void shmem_long_get (long *dest, const long *src, size_t nelems, int pe);
+void shmem_longlong_get (long long *dest, const long long *src, size_t nelems, int pe);
+void shmem_longdouble_get (long double *dest, const long double *src, size_t nelems, int pe);
+void shmem_double_get (double *dest, const double *src, size_t nelems, int pe);
+void shmem_float_get (float *dest, const float *src, size_t nelems, int pe);
+
+/* ---- broadcast / collect (reference src/shmem.h:1746-1779); sources in the
+ *      device symmetric heap ---- */
+#define SHMEM_COLLECT_SYNC_SIZE (128L / SHMEM_INTERNAL_F2C_SCALE)
+#define _SHMEM_COLLECT_SYNC_SIZE SHMEM_COLLECT_SYNC_SIZE
+void shmem_broadcast64 (void *target, const void *source, size_t nelems, int PE_root, int PE_start,
+                        int logPE_stride, int PE_size, long *pSync);
+void shmem_broadcast32 (void *target, const void *source, size_t nelems, int PE_root, int PE_start,
+                        int logPE_stride, int PE_size, long *pSync);
+void shmem_fcollect64 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                       int PE_size, long *pSync);
+void shmem_fcollect32 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                       int PE_size, long *pSync);
+void shmem_collect64 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                      int PE_size, long *pSync);
+void shmem_collect32 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                      int PE_size, long *pSync);
+
 /* ---- reductions: target = op-fold over the active set of source ---- */
     void shmem_short_sum_to_all (short *target, short *source,
             int nreduce, int PE_start, int logPE_stride, int PE_size,

@@ -115,3 +115,25 @@ def as_value_bytes(a, dtype):
     a = np.ascontiguousarray(a, dtype=NP[dtype])
     b = a.view(np.uint8).reshape(len(a), a.itemsize)
     return b[:, :value_bytes(dtype)]
+
+
+# ---------------------------------------------------------------------------
+# data-movement collectives: restated semantics
+# ---------------------------------------------------------------------------
+def broadcast(srcs, root, targets_before):
+    """reference src/broadcast/broadcast-linear.c:61-82: every member but the
+    root gets the root's source; the root's target keeps its old contents."""
+    return [t.copy() if i == root else srcs[root].copy() for i, t in enumerate(targets_before)]
+
+
+def fcollect(srcs):
+    """reference src/fcollect/fcollect-linear.c:60-93: member i's block lands
+    at offset i * nelems, in active-set order, on every member."""
+    out = np.concatenate(srcs) if srcs else np.zeros(0)
+    return [out.copy() for _ in srcs]
+
+
+def collect(srcs):
+    """reference src/collect/collect-linear.c:60-156: like fcollect with
+    per-member lengths; offsets are the running sum in active-set order."""
+    return fcollect(srcs)

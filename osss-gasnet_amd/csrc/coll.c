@@ -1,0 +1,363 @@
+/*
+ * coll.c -- the data-movement neighbours of the reduction path (SURVEY.md
+ * section 8f rows 3-4): one-sided put/get and the broadcast / collect /
+ * fcollect collectives, over the same device symmetric heap and peer
+ * mappings as the reductions.
+ *
+ * Reference semantics followed:
+ *   shmem_putmem/getmem, put/get32/64/128, shmem_<T>_put/get
+ *       src/ptp/putget.c:116-256 -> shmemi_comms_put_bulk / get_bulk: blocking
+ *       byte copies to/from a symmetric address on another PE
+ *   shmem_broadcast32/64   src/broadcast/broadcast.c:69-110,
+ *       linear form broadcast-linear.c:61-82: barrier, then every PE but the
+ *       root copies the root's source into its target; the root's target is
+ *       untouched (the reference's default tree form, broadcast-tree.c, also
+ *       overwrites the non-root PEs' SOURCE with the data as it forwards it;
+ *       that side effect is not part of the API and is not reproduced)
+ *   shmem_fcollect32/64    src/fcollect/fcollect-linear.c:60-93: PE i's
+ *       nelems elements land at offset i*nelems of every member's target
+ *   shmem_collect32/64     src/collect/collect-linear.c:60-156: like fcollect
+ *       with per-PE counts; offsets are the running sum in active-set order
+ *
+ * The remote side of put/get, and every collective's source, must be in the
+ * device symmetric heap (shmemx_malloc_device): that is where peers can read
+ * it over xGMI. Local sides may be any host or device memory. Put/get go
+ * through hipMemcpy on peer-mapped pointers (the HIP runtime's P2P copy
+ * contract makes the bytes visible to the peer's later kernels). The
+ * collectives PULL: every PE reads the members' sources over xGMI into its
+ * own target, between two barriers -- the same producer/consumer pattern as
+ * the reduction's all-gather leg.
+ */
+#define _GNU_SOURCE
+#include <complex.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "mi355_reduce.h"
+#include "pshmem.h"
+#include "shmem.h"
+#include "shmemx.h"
+#include "shmemi.h"
+
+/* ---------------------------------------------------------------------- */
+/* helpers                                                                 */
+/* ---------------------------------------------------------------------- */
+static void check_pe (const char *fn, int pe)
+{
+    if (pe < 0 || pe >= shmemi.npes)
+        shmemi_fatal ("%s: PE %d outside 0..%d", fn, pe, shmemi.npes - 1);
+}
+
+/* Address of symmetric object `sym` (nbytes long) on PE `pe`. */
+static void *remote_addr (const char *fn, const void *sym, size_t nbytes, int pe)
+{
+    if (pe == shmemi.mype)
+        return (void *) sym;
+    if (!shmemi_in_device_heap (sym, nbytes))
+        shmemi_fatal ("%s: remote address %p is not in the device symmetric heap "
+                      "(allocate it with shmemx_malloc_device)", fn, sym);
+    return shmemi_peer_ptr (pe, shmemi_heap_offset (sym));
+}
+
+static void blocking_copy (void *dst, const void *src, size_t nbytes)
+{
+    if (nbytes == 0 || dst == src)
+        return;
+    SHMEMI_HIP (hipMemcpyAsync (dst, src, nbytes, hipMemcpyDefault, shmemi.stream));
+    SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+}
+
+static void put_bytes (const char *fn, void *dest, const void *src, size_t nbytes, int pe)
+{
+    shmemi_init_check (fn);
+    check_pe (fn, pe);
+    if (shmemi.heap == NULL)
+        shmemi_fatal ("%s: no GPU (SHMEM_BOOTSTRAP_ONLY)", fn);
+    if (nbytes == 0)
+        return;
+    blocking_copy (remote_addr (fn, dest, nbytes, pe), src, nbytes);
+}
+
+static void get_bytes (const char *fn, void *dest, const void *src, size_t nbytes, int pe)
+{
+    shmemi_init_check (fn);
+    check_pe (fn, pe);
+    if (shmemi.heap == NULL)
+        shmemi_fatal ("%s: no GPU (SHMEM_BOOTSTRAP_ONLY)", fn);
+    if (nbytes == 0)
+        return;
+    blocking_copy (dest, remote_addr (fn, src, nbytes, pe), nbytes);
+}
+
+/* ---------------------------------------------------------------------- */
+/* put / get                                                               */
+/* ---------------------------------------------------------------------- */
+void pshmem_putmem (void *dest, const void *src, size_t nelems, int pe)
+{
+    put_bytes ("shmem_putmem", dest, src, nelems, pe);
+}
+void pshmem_getmem (void *dest, const void *src, size_t nelems, int pe)
+{
+    get_bytes ("shmem_getmem", dest, src, nelems, pe);
+}
+void pshmem_put32 (void *dest, const void *src, size_t nelems, int pe)
+{
+    put_bytes ("shmem_put32", dest, src, 4 * nelems, pe);
+}
+void pshmem_put64 (void *dest, const void *src, size_t nelems, int pe)
+{
+    put_bytes ("shmem_put64", dest, src, 8 * nelems, pe);
+}
+void pshmem_put128 (void *dest, const void *src, size_t nelems, int pe)
+{
+    put_bytes ("shmem_put128", dest, src, 16 * nelems, pe);
+}
+void pshmem_get32 (void *dest, const void *src, size_t nelems, int pe)
+{
+    get_bytes ("shmem_get32", dest, src, 4 * nelems, pe);
+}
+void pshmem_get64 (void *dest, const void *src, size_t nelems, int pe)
+{
+    get_bytes ("shmem_get64", dest, src, 8 * nelems, pe);
+}
+void pshmem_get128 (void *dest, const void *src, size_t nelems, int pe)
+{
+    get_bytes ("shmem_get128", dest, src, 16 * nelems, pe);
+}
+
+#define TYPED_PUTGET(Name, Type)                                                                    \
+    void pshmem_##Name##_put (Type *dest, const Type *src, size_t nelems, int pe)                   \
+    {                                                                                               \
+        put_bytes ("shmem_" #Name "_put", dest, src, sizeof (Type) * nelems, pe);                  \
+    }                                                                                               \
+    void pshmem_##Name##_get (Type *dest, const Type *src, size_t nelems, int pe)                   \
+    {                                                                                               \
+        get_bytes ("shmem_" #Name "_get", dest, src, sizeof (Type) * nelems, pe);                  \
+    }                                                                                               \
+    void shmem_##Name##_put (Type *dest, const Type *src, size_t nelems, int pe)                    \
+        __attribute__ ((weak, alias ("pshmem_" #Name "_put")));                                     \
+    void shmem_##Name##_get (Type *dest, const Type *src, size_t nelems, int pe)                    \
+        __attribute__ ((weak, alias ("pshmem_" #Name "_get")));
+
+TYPED_PUTGET (char, char)
+TYPED_PUTGET (short, short)
+TYPED_PUTGET (int, int)
+TYPED_PUTGET (long, long)
+TYPED_PUTGET (longlong, long long)
+TYPED_PUTGET (longdouble, long double)
+TYPED_PUTGET (double, double)
+TYPED_PUTGET (float, float)
+
+/* ---------------------------------------------------------------------- */
+/* collectives                                                             */
+/* ---------------------------------------------------------------------- */
+struct cset {
+    int start, stride, size, me;
+};
+
+static struct cset make_set (const char *fn, int PE_start, int logPE_stride, int PE_size)
+{
+    shmemi_init_check (fn);
+    if (shmemi.heap == NULL)
+        shmemi_fatal ("%s: no GPU (SHMEM_BOOTSTRAP_ONLY)", fn);
+    if (logPE_stride < 0 || logPE_stride > 30 || PE_size < 1 || PE_start < 0 ||
+        PE_start + (long) (PE_size - 1) * (1L << logPE_stride) >= shmemi.npes)
+        shmemi_fatal ("%s: active set (PE_start %d, logPE_stride %d, PE_size %d) outside the %d PEs", fn,
+                      PE_start, logPE_stride, PE_size, shmemi.npes);
+    struct cset s = {PE_start, 1 << logPE_stride, PE_size, -1};
+    for (int i = 0; i < PE_size; ++i)
+        if (PE_start + i * s.stride == shmemi.mype)
+            s.me = i;
+    if (s.me < 0)
+        shmemi_fatal ("%s: PE %d is not in the active set (PE_start %d, logPE_stride %d, PE_size %d)", fn,
+                      shmemi.mype, PE_start, logPE_stride, PE_size);
+    return s;
+}
+
+static int is_device_ptr (const void *p)
+{
+    if (shmemi_in_device_heap (p, 0))
+        return 1;
+    hipPointerAttribute_t a;
+    memset (&a, 0, sizeof a);
+    hipError_t e = hipPointerGetAttributes (&a, p);
+    (void) hipGetLastError ();
+    return e == hipSuccess && (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged);
+}
+
+/* Pull nseg byte ranges from peers into local memory: one copy kernel (with
+ * the completion signal) when the destination is device memory, DMA copies
+ * otherwise. */
+static void pull (void **dsts, const void **srcs, size_t *nbytes, int nseg)
+{
+    int dev = 1;
+    for (int i = 0; i < nseg; ++i)
+        dev &= is_device_ptr (dsts[i]);
+    if (dev) {
+        for (int base = 0; base < nseg; base += 64) {
+            const int k = nseg - base < 64 ? nseg - base : 64;
+            const int last = base + k == nseg;
+            if (last)
+                shmemi_arm_signal ();
+            int rc = mi355_copy_segments (dsts + base, srcs + base, nbytes + base, k, shmemi.stream);
+            if (rc != 0)
+                shmemi_fatal ("copy kernel launch failed: %d", rc);
+        }
+        shmemi_wait_signal ();
+    } else {
+        for (int i = 0; i < nseg; ++i)
+            if (nbytes[i] != 0)
+                SHMEMI_HIP (hipMemcpyAsync (dsts[i], srcs[i], nbytes[i], hipMemcpyDefault, shmemi.stream));
+        SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    }
+}
+
+static void collective_entry (const char *fn, const void *source, size_t nbytes, const struct cset *s)
+{
+    if (nbytes != 0 && !shmemi_in_device_heap (source, nbytes))
+        shmemi_fatal ("%s: source %p is not in the device symmetric heap (allocate it with "
+                      "shmemx_malloc_device)", fn, source);
+    shmemi_order_after_caller (1);
+    shmemi_barrier_set (s->start, s->stride, s->size); /* every source is ready */
+}
+
+static void broadcast_bytes (const char *fn, void *target, const void *source, size_t nbytes, int PE_root,
+                             int PE_start, int logPE_stride, int PE_size)
+{
+    struct cset s = make_set (fn, PE_start, logPE_stride, PE_size);
+    if (PE_root < 0 || PE_root >= PE_size)
+        shmemi_fatal ("%s: PE_root %d outside the active set of %d PEs", fn, PE_root, PE_size);
+    const int root = PE_start + PE_root * s.stride;
+    collective_entry (fn, source, nbytes, &s);
+    if (shmemi.mype != root && nbytes != 0) {
+        void *d = target;
+        const void *src = shmemi_peer_ptr (root, shmemi_heap_offset (source));
+        pull (&d, &src, &nbytes, 1);
+    }
+    shmemi_barrier_set (s.start, s.stride, s.size); /* nobody reads the root's source any more */
+}
+
+void pshmem_broadcast32 (void *target, const void *source, size_t nelems, int PE_root, int PE_start,
+                         int logPE_stride, int PE_size, long *pSync)
+{
+    (void) pSync;
+    broadcast_bytes ("shmem_broadcast32", target, source, 4 * nelems, PE_root, PE_start, logPE_stride, PE_size);
+}
+
+void pshmem_broadcast64 (void *target, const void *source, size_t nelems, int PE_root, int PE_start,
+                         int logPE_stride, int PE_size, long *pSync)
+{
+    (void) pSync;
+    broadcast_bytes ("shmem_broadcast64", target, source, 8 * nelems, PE_root, PE_start, logPE_stride, PE_size);
+}
+
+/* counts[i] bytes from member i land at the running offset in target */
+static void gather_bytes (void *target, const void *source, const size_t *counts, const struct cset *s)
+{
+    void **dsts = (void **) malloc (sizeof (void *) * (size_t) s->size);
+    const void **srcs = (const void **) malloc (sizeof (void *) * (size_t) s->size);
+    size_t *nb = (size_t *) malloc (sizeof (size_t) * (size_t) s->size);
+    if (dsts == NULL || srcs == NULL || nb == NULL)
+        shmemi_fatal ("out of host memory");
+    size_t off = 0;
+    int k = 0;
+    for (int i = 0; i < s->size; ++i) {
+        const int pe = s->start + i * s->stride;
+        if (counts[i] != 0) {
+            dsts[k] = (char *) target + off;
+            srcs[k] = shmemi_peer_ptr (pe, shmemi_heap_offset (source));
+            nb[k] = counts[i];
+            ++k;
+        }
+        off += counts[i];
+    }
+    if (k > 0)
+        pull (dsts, srcs, nb, k);
+    free (nb);
+    free (srcs);
+    free (dsts);
+}
+
+static void fcollect_bytes (const char *fn, void *target, const void *source, size_t nbytes, int PE_start,
+                            int logPE_stride, int PE_size)
+{
+    struct cset s = make_set (fn, PE_start, logPE_stride, PE_size);
+    collective_entry (fn, source, nbytes, &s);
+    size_t *counts = (size_t *) malloc (sizeof (size_t) * (size_t) s.size);
+    if (counts == NULL)
+        shmemi_fatal ("out of host memory");
+    for (int i = 0; i < s.size; ++i)
+        counts[i] = nbytes;
+    gather_bytes (target, source, counts, &s);
+    free (counts);
+    shmemi_barrier_set (s.start, s.stride, s.size); /* nobody reads our source any more */
+}
+
+void pshmem_fcollect32 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                        int PE_size, long *pSync)
+{
+    (void) pSync;
+    fcollect_bytes ("shmem_fcollect32", target, source, 4 * nelems, PE_start, logPE_stride, PE_size);
+}
+
+void pshmem_fcollect64 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                        int PE_size, long *pSync)
+{
+    (void) pSync;
+    fcollect_bytes ("shmem_fcollect64", target, source, 8 * nelems, PE_start, logPE_stride, PE_size);
+}
+
+/* collect: the per-PE byte counts travel through the bootstrap segment; the
+ * closing barrier keeps a count alive until every member has read it */
+static void collect_bytes (const char *fn, void *target, const void *source, size_t nbytes, int PE_start,
+                           int logPE_stride, int PE_size)
+{
+    struct cset s = make_set (fn, PE_start, logPE_stride, PE_size);
+    shmemi_publish_count (nbytes);
+    collective_entry (fn, source, nbytes, &s);
+    size_t *counts = (size_t *) malloc (sizeof (size_t) * (size_t) s.size);
+    if (counts == NULL)
+        shmemi_fatal ("out of host memory");
+    for (int i = 0; i < s.size; ++i)
+        counts[i] = shmemi_peer_count (s.start + i * s.stride);
+    gather_bytes (target, source, counts, &s);
+    free (counts);
+    shmemi_barrier_set (s.start, s.stride, s.size);
+}
+
+void pshmem_collect32 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                       int PE_size, long *pSync)
+{
+    (void) pSync;
+    collect_bytes ("shmem_collect32", target, source, 4 * nelems, PE_start, logPE_stride, PE_size);
+}
+
+void pshmem_collect64 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                       int PE_size, long *pSync)
+{
+    (void) pSync;
+    collect_bytes ("shmem_collect64", target, source, 8 * nelems, PE_start, logPE_stride, PE_size);
+}
+
+#define WEAK(name) __attribute__ ((weak, alias ("p" #name)))
+void shmem_putmem (void *dest, const void *src, size_t nelems, int pe) WEAK (shmem_putmem);
+void shmem_getmem (void *dest, const void *src, size_t nelems, int pe) WEAK (shmem_getmem);
+void shmem_put32 (void *dest, const void *src, size_t nelems, int pe) WEAK (shmem_put32);
+void shmem_put64 (void *dest, const void *src, size_t nelems, int pe) WEAK (shmem_put64);
+void shmem_put128 (void *dest, const void *src, size_t nelems, int pe) WEAK (shmem_put128);
+void shmem_get32 (void *dest, const void *src, size_t nelems, int pe) WEAK (shmem_get32);
+void shmem_get64 (void *dest, const void *src, size_t nelems, int pe) WEAK (shmem_get64);
+void shmem_get128 (void *dest, const void *src, size_t nelems, int pe) WEAK (shmem_get128);
+void shmem_broadcast32 (void *target, const void *source, size_t nelems, int PE_root, int PE_start,
+                        int logPE_stride, int PE_size, long *pSync) WEAK (shmem_broadcast32);
+void shmem_broadcast64 (void *target, const void *source, size_t nelems, int PE_root, int PE_start,
+                        int logPE_stride, int PE_size, long *pSync) WEAK (shmem_broadcast64);
+void shmem_fcollect32 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                       int PE_size, long *pSync) WEAK (shmem_fcollect32);
+void shmem_fcollect64 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                       int PE_size, long *pSync) WEAK (shmem_fcollect64);
+void shmem_collect32 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                      int PE_size, long *pSync) WEAK (shmem_collect32);
+void shmem_collect64 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
+                      int PE_size, long *pSync) WEAK (shmem_collect64);

@@ -50,7 +50,7 @@ struct shmemi_hostblk {
 };
 
 #define SEG_MAGIC 0x4d49333535534d45ull /* "MI355SME" */
-#define SEG_VERSION 2
+#define SEG_VERSION 3
 
 static double now_s (void)
 {
@@ -546,6 +546,24 @@ static void interconnect_selftest (void)
         shmemi.p2p_broken = 1;
     }
     shmemi_barrier_set (0, 1, np);
+}
+
+/* shmem_collect's per-PE counts, read by the other members after a barrier */
+static size_t local_count;
+
+void shmemi_publish_count (size_t nbytes)
+{
+    if (shmemi.seg == NULL)
+        local_count = nbytes;
+    else
+        __atomic_store_n (&seg_info (shmemi.mype)->collect_bytes, (uint64_t) nbytes, __ATOMIC_RELEASE);
+}
+
+size_t shmemi_peer_count (int pe)
+{
+    if (shmemi.seg == NULL)
+        return local_count;
+    return (size_t) __atomic_load_n (&seg_info (pe)->collect_bytes, __ATOMIC_ACQUIRE);
 }
 
 void *shmemx_malloc_device (size_t size)

@@ -31,6 +31,7 @@ struct shmemi_pe_info {
     uint64_t heap_size;
     int32_t published;
     int32_t selftest;           /* bit 0: signal region stores seen, bit 1: heap reads ok */
+    uint64_t collect_bytes;     /* this PE's contribution to the current shmem_collect */
 };
 
 struct shmemi_seg {
@@ -130,6 +131,8 @@ void shmemi_timed_begin (void);
 void shmemi_timed_end (void);
 void shmemi_timed_marker (int end);
 int shmemi_rccl_comm (void **comm);
+void shmemi_publish_count (size_t nbytes);
+size_t shmemi_peer_count (int pe);
 
 #define SHMEMI_HIP(call) shmemi_hip_check ((call), #call)
 

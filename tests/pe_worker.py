@@ -23,17 +23,93 @@ def members(start, logstride, size):
     return [start + i * (1 << logstride) for i in range(size)]
 
 
+def dm_source(c, pe):
+    """Source block of PE pe for a data-movement case (collect: length varies by PE)."""
+    import _inputs
+    bits = c["bits"]
+    n = c["n"] if c["kind"] != "collect" else ((c["n"] + pe) % 4) * 37
+    rng = np.random.default_rng(c["seed"] * 1009 + pe)
+    return rng.integers(-2**(bits - 1), 2**(bits - 1), n, dtype=np.int32 if bits == 32 else np.int64)
+
+
+def run_datamove(shm, c, me, da, db, ha, hb, results):
+    import ctypes
+    kind, bits = c["kind"], c["bits"]
+    dt = np.int32 if bits == 32 else np.int64
+    es = bits // 8
+    s = None
+    for cand in c["sets"]:
+        if me in members(*cand):
+            s = cand
+    if s is None:
+        return
+    start, logstride, size = s
+    mem = members(*s)
+    x = dm_source(c, me)
+    tgt_host = c.get("target") == "host"
+    tgt = hb if tgt_host else db
+    cap = c["cap"]
+    sentinel = np.full(cap, -7, dtype=dt)
+    if tgt_host:
+        ctypes.memmove(tgt, sentinel.ctypes.data, sentinel.nbytes)
+    else:
+        shm.put(tgt, sentinel)
+    if len(x):
+        shm.put(da, x)
+    psync = shm._psync_ptr
+    L = shm.lib
+    vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    if kind == "broadcast":
+        f = getattr(L, f"shmem_broadcast{bits}")
+        f.argtypes = [vp, vp, sz, i, i, i, i, vp]
+        f(tgt, da, c["n"], c["root"], start, logstride, size, psync)
+    elif kind in ("fcollect", "collect"):
+        f = getattr(L, f"shmem_{kind}{bits}")
+        f.argtypes = [vp, vp, sz, i, i, i, vp]
+        f(tgt, da, len(x), start, logstride, size, psync)
+    elif kind == "putget":
+        # put my block into the next member's target at my slot, barrier, then
+        # get the previous member's block from its source
+        nxt, prv = mem[(mem.index(me) + 1) % size], mem[(mem.index(me) - 1) % size]
+        L.shmem_barrier(start, logstride, size, psync)  # every target holds its sentinel
+        f = getattr(L, f"shmem_put{bits}")
+        f.argtypes = [vp, vp, sz, i]
+        g = getattr(L, f"shmem_get{bits}")
+        g.argtypes = [vp, vp, sz, i]
+        f(db + mem.index(me) * c["n"] * es, da, c["n"], nxt)
+        L.shmem_barrier(start, logstride, size, psync)
+        g(hb if tgt_host else db + size * c["n"] * es, da, c["n"], prv)
+        L.shmem_barrier(start, logstride, size, psync)
+        if tgt_host:
+            got2 = np.empty(c["n"], dtype=dt)
+            ctypes.memmove(got2.ctypes.data, hb, got2.nbytes)
+        else:
+            got2 = shm.get(db + size * c["n"] * es, c["n"], dt)
+        results[str(c["id"]) + "_get"] = got2
+        tgt_host = False
+        tgt = db
+    if tgt_host:
+        got = np.empty(cap, dtype=dt)
+        ctypes.memmove(got.ctypes.data, tgt, got.nbytes)
+    else:
+        got = shm.get(tgt, cap, dt)
+    results[str(c["id"])] = got
+
+
 def main():
     spec = json.load(open(sys.argv[1]))
     outdir = sys.argv[2]
     shm = shmem_reduce.Shmem()
     shm.init()
     me = shm.my_pe()
-    maxb = max((c["n"] + 16) * 16 for c in spec["cases"])
+    maxb = max(max(c["n"] + 16, c.get("cap", 0)) * 16 for c in spec["cases"])
     da, db = shm.malloc_device(maxb), shm.malloc_device(maxb)
     ha, hb = shm.malloc(maxb), shm.malloc(maxb)
     results = {}
     for c in spec["cases"]:
+        if c.get("kind", "reduce") != "reduce":
+            run_datamove(shm, c, me, da, db, ha, hb, results)
+            continue
         mine = None
         for s in c["sets"]:
             if me in members(*s):

@@ -1,0 +1,67 @@
+"""GPU: put/get, broadcast, fcollect and collect across PE processes
+(SURVEY.md 8f rows 3-4), checked against the oracle's restatement of the
+reference semantics (oracle.broadcast / fcollect / collect)."""
+import numpy as np
+import pytest
+
+import oracle
+from pe_worker import dm_source
+from test_gpu_multipe import members, run_pes
+
+pytestmark = [pytest.mark.gpu, pytest.mark.multipe]
+
+
+def case(cid, kind, bits, n, sets, **kw):
+    c = {"id": cid, "kind": kind, "bits": bits, "n": n, "sets": sets, "seed": 500 + cid, "cap": 4096,
+         "op": "sum", "dtype": "long"}  # op/dtype only size the worker's buffers
+    c.update(kw)
+    return c
+
+
+def check_dm(results, cases):
+    for c in cases:
+        dt = np.int32 if c["bits"] == 32 else np.int64
+        for s in c["sets"]:
+            mem = members(*s)
+            srcs = [dm_source(c, pe) for pe in mem]
+            cap = c["cap"]
+            sentinel = np.full(cap, -7, dtype=dt)
+            if c["kind"] == "broadcast":
+                want = oracle.broadcast([x for x in srcs], c["root"], [sentinel[:len(srcs[0])]] * len(mem))
+                for i, pe in enumerate(mem):
+                    got = results[pe][str(c["id"])]
+                    assert (got[:len(want[i])] == want[i]).all(), (c, pe)
+                    assert (got[len(want[i]):] == -7).all(), (c, pe)
+            elif c["kind"] in ("fcollect", "collect"):
+                want = (oracle.fcollect if c["kind"] == "fcollect" else oracle.collect)(srcs)
+                for i, pe in enumerate(mem):
+                    got = results[pe][str(c["id"])]
+                    assert (got[:len(want[i])] == want[i]).all(), (c, pe)
+                    assert (got[len(want[i]):] == -7).all(), (c, pe)
+            elif c["kind"] == "putget":
+                n, size = c["n"], len(mem)
+                for i, pe in enumerate(mem):
+                    got = results[pe][str(c["id"])]
+                    prv = (i - 1) % size
+                    assert (got[prv * n:(prv + 1) * n] == srcs[prv]).all(), (c, pe)
+                    assert (results[pe][str(c["id"]) + "_get"] == srcs[prv]).all(), (c, pe)
+
+
+def test_collectives_four_pes(tmp_path):
+    cases = []
+    cid = 0
+    for bits in (32, 64):
+        for root in (0, 2, 3):
+            cases.append(case(cid, "broadcast", bits, 300, [[0, 0, 4]], root=root)); cid += 1
+        cases.append(case(cid, "broadcast", bits, 257, [[0, 1, 2], [1, 1, 2]], root=1)); cid += 1
+        cases.append(case(cid, "broadcast", bits, 0, [[0, 0, 4]], root=1)); cid += 1
+        cases.append(case(cid, "broadcast", bits, 129, [[0, 0, 4]], root=1, target="host")); cid += 1
+        cases.append(case(cid, "fcollect", bits, 200, [[0, 0, 4]])); cid += 1
+        cases.append(case(cid, "fcollect", bits, 33, [[1, 0, 3]])); cid += 1
+        cases.append(case(cid, "fcollect", bits, 100, [[0, 0, 4]], target="host")); cid += 1
+        cases.append(case(cid, "collect", bits, 4, [[0, 0, 4]])); cid += 1  # PE 0 contributes nothing
+        cases.append(case(cid, "collect", bits, 3, [[0, 1, 2], [1, 1, 2]])); cid += 1
+        cases.append(case(cid, "putget", bits, 100, [[0, 0, 4]])); cid += 1
+        cases.append(case(cid, "putget", bits, 64, [[0, 0, 4]], target="host")); cid += 1
+    results = run_pes(4, cases, tmp_path)
+    check_dm(results, cases)
