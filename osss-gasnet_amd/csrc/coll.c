@@ -21,10 +21,15 @@
  *
  * The remote side of put/get, and every collective's source, must be in the
  * device symmetric heap (shmemx_malloc_device): that is where peers can read
- * it over xGMI. Local sides may be any host or device memory. Put/get go
- * through hipMemcpy on peer-mapped pointers (the HIP runtime's P2P copy
- * contract makes the bytes visible to the peer's later kernels). The
- * collectives PULL: every PE reads the members' sources over xGMI into its
+ * it over xGMI. Local sides may be any host or device memory. A put goes
+ * through hipMemcpy on the peer-mapped pointer (the HIP runtime's P2P copy
+ * contract makes the bytes visible to the peer's later kernels: a push into
+ * another GPU's memory must not be left to this library's own kernels, whose
+ * write-through only reaches memory, not the peer's L2). A get into device
+ * memory, and every collective, PULLS with the streaming copy kernel: every
+ * PE reads the members' sources over xGMI into its own target, between two
+ * barriers -- the same producer/consumer pattern as the reduction's
+ * all-gather leg. Host-memory local sides use hipMemcpy. The collectives: every PE reads the members' sources over xGMI into its
  * own target, between two barriers -- the same producer/consumer pattern as
  * the reduction's all-gather leg.
  */
@@ -68,6 +73,9 @@ static void blocking_copy (void *dst, const void *src, size_t nbytes)
     SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
 }
 
+static int is_device_ptr (const void *p);
+static void pull (void **dsts, const void **srcs, size_t *nbytes, int nseg);
+
 static void put_bytes (const char *fn, void *dest, const void *src, size_t nbytes, int pe)
 {
     shmemi_init_check (fn);
@@ -87,7 +95,15 @@ static void get_bytes (const char *fn, void *dest, const void *src, size_t nbyte
         shmemi_fatal ("%s: no GPU (SHMEM_BOOTSTRAP_ONLY)", fn);
     if (nbytes == 0)
         return;
-    blocking_copy (dest, remote_addr (fn, src, nbytes, pe), nbytes);
+    const void *from = remote_addr (fn, src, nbytes, pe);
+    if (is_device_ptr (dest) && dest != from) {
+        /* device <- (peer) device: the streaming copy kernel pulls over xGMI
+         * (2-3x the rate of hipMemcpy's D2D path, profiles/r01/coll_bench) */
+        shmemi_order_after_caller (0);
+        pull (&dest, &from, &nbytes, 1);
+    } else {
+        blocking_copy (dest, from, nbytes);
+    }
 }
 
 /* ---------------------------------------------------------------------- */
