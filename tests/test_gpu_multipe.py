@@ -161,3 +161,24 @@ def test_bad_active_set_aborts_every_pe(tmp_path):
     outs = [p.communicate(timeout=120) for p in procs]
     assert procs[1].returncode != 0 and "not in the active set" in outs[1][0]
     assert procs[0].returncode != 0 and "aborting" in outs[0][0]
+
+
+def test_random_sequence_stress(tmp_path):
+    """300 back-to-back reductions with random op/type, size (0 .. 300k elements,
+    across the fused/multi-launch threshold), buffer mode, schedule and active
+    set -- including two disjoint sets running at once -- on 4 PEs. Catches
+    races between consecutive calls (a PE racing ahead into the next call)."""
+    rng = np.random.default_rng(2026)
+    sets_choices = [[[0, 0, 4]], [[0, 1, 2], [1, 1, 2]], [[1, 0, 3]], [[0, 0, 2], [2, 0, 2]], [[0, 0, 4]]]
+    cases = []
+    for cid in range(300):
+        op, dtype = oracle.PAIRS[rng.integers(len(oracle.PAIRS))]
+        n = int(rng.choice([0, 1, 7, 64, 1000, 8191, 40000, 150000, 300000]))
+        mode = str(rng.choice(["dev", "dev", "inplace", "host"]))
+        alg = str(rng.choice(["p2p", "p2p", "p2p", "exact"]))
+        sets = sets_choices[rng.integers(len(sets_choices))]
+        cases.append({"id": cid, "op": op, "dtype": dtype, "n": n, "sets": sets, "mode": mode,
+                      "algorithm": alg, "seed": 7000 + cid})
+    results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_DEVICE_HEAP_SIZE": "64M",
+                                                     "SHMEM_DEVICE_SCRATCH_SIZE": "3M"})
+    check(results, cases)
