@@ -289,16 +289,24 @@ unsigned grid_for(uint64_t units_per_block_pass, uint64_t units, int blocks_per_
     return (unsigned)(want < cap ? want : cap);
 }
 
-// Launch shape per source count, from tools/hbm_sweep.hip on MI355X (256 MiB
-// per source, fold of double sums; GB/s counts (k+1) x 256 MiB):
-//   k=2: 4 vectors/lane, 1 block/CU, non-temporal loads      6.56 TB/s
-//   k=3: 2 vectors/lane, 1 block/CU, non-temporal both       6.28 TB/s
-//   k=4: 1 vector/lane,  2 blocks/CU, non-temporal both      6.18 TB/s
-//   k=8: 1 vector/lane,  2 blocks/CU, non-temporal both      5.85 TB/s
-// Fewer, fuller blocks beat 8 blocks/CU by 5-10 % on every k.
-template <int NSRC> struct Shape {
-    static constexpr int unroll = NSRC == 2 ? 4 : NSRC == 3 ? 2 : 1;
-    static constexpr int blocks_per_cu = NSRC <= 3 ? 1 : 2;
+// Launch shape per source count, from tools/hbm_sweep.hip and
+// tools/fold_bench.py on MI355X (256 MiB per source, double sums,
+// non-temporal loads + `nt sc1` stores; GB/s counts (k+1) x 256 MiB;
+// profiles/r01/hbm_sweep_v5.txt, fold_bench_k_sources.jsonl):
+//   k=2: 1 vector/lane,  2 blocks/CU     6.4 TB/s
+//   k=3: 2 vectors/lane, 1 block/CU      6.5 TB/s
+//   k=4: 1 vector/lane,  1 block/CU      6.2-6.3 TB/s
+//   k=8: 4 vectors/lane, 8 blocks/CU     5.8-5.9 TB/s (k=5..7 take k=8's
+//        depth at half the blocks)
+// Box-to-box spread is +-3 %, so neighbours within that band are ties.
+// Long double is VALU-bound (x87 arithmetic in software): it wants many
+// waves to hide ALU latency, not deep per-lane load queues.
+template <int NSRC, typename T> struct Shape {
+    static constexpr bool alu_heavy = std::is_same<T, x80>::value;
+    static constexpr int unroll =
+        alu_heavy ? 1 : NSRC == 2 ? 1 : NSRC == 3 ? 2 : NSRC == 4 ? 1 : NSRC < 8 ? 2 : 4;
+    static constexpr int blocks_per_cu =
+        alu_heavy ? 8 : NSRC == 2 ? 2 : NSRC == 3 ? 1 : NSRC == 4 ? 1 : NSRC < 8 ? 4 : 8;
     static constexpr int policy = POL_NT_LOAD;
 };
 
@@ -313,7 +321,7 @@ int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, b
     }
     constexpr int V = 16 / sizeof(T);
     if ((orbits & 15) == 0) {
-        using S = Shape<NSRC>;
+        using S = Shape<NSRC, T>;
         p.nvec = n / V;
         p.tail = (uint32_t)(n % V);
         const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, S::blocks_per_cu);

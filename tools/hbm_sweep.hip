@@ -147,18 +147,22 @@ int main(int argc, char **argv) {
     double us_memcpy = time_it([&] { CHECK(hipMemcpyAsync(bufs[1], bufs[0], bytes, hipMemcpyDeviceToDevice, 0)); }, 20);
     printf("hipMemcpyAsync D2D %zu MiB: %.1f us  %.0f GB/s (read+write)\n", mib, us_memcpy, 2.0 * bytes / (us_memcpy * 1e-6) / 1e9);
 
-    run_copy<256, 8, 6>(bufs[0], bufs[1], nvec, bytes);
-    run_copy<256, 8, 7>(bufs[0], bufs[1], nvec, bytes);
     const u32x4 *srcs[8];
     for (int k = 0; k < 8; ++k) srcs[k] = bufs[k];
-    run_fold<256, 4, 2, 1>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 4, 2, 7>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 2, 3, 3>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 2, 3, 7>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 1, 4, 3>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 1, 4, 7>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 1, 8, 3>(srcs, bufs[8], nvec, bytes);
-    run_fold<256, 1, 8, 7>(srcs, bufs[8], nvec, bytes);
+    // folds with the library's store (nt sc1): pol 6 = plain loads, 7 = nt loads
+#define FOLDS(K)                                              \
+    run_fold<256, 1, K, 6>(srcs, bufs[8], nvec, bytes);       \
+    run_fold<256, 1, K, 7>(srcs, bufs[8], nvec, bytes);       \
+    run_fold<256, 2, K, 6>(srcs, bufs[8], nvec, bytes);       \
+    run_fold<256, 2, K, 7>(srcs, bufs[8], nvec, bytes);       \
+    run_fold<256, 4, K, 6>(srcs, bufs[8], nvec, bytes);       \
+    run_fold<256, 4, K, 7>(srcs, bufs[8], nvec, bytes);       \
+    run_fold<512, 1, K, 7>(srcs, bufs[8], nvec, bytes);       \
+    run_fold<512, 2, K, 7>(srcs, bufs[8], nvec, bytes);
+    FOLDS(2)
+    FOLDS(3)
+    FOLDS(4)
+    FOLDS(8)
 
     std::sort(results.begin(), results.end(), [](const Res &a, const Res &b) {
         int c = strcmp(a.name, b.name);
