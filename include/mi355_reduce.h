@@ -93,17 +93,24 @@ int mi355_signal_launch (void *stream);
 
 /* ---- one-launch P2P reduction for small messages (fused.hip) ----
  * Signal region: per PE, MI355_SIG_WORDS 8-byte words of uncached device
- * memory mapped into every peer; all zero before first use. */
+ * memory mapped into every peer; all zero before first use. It holds
+ * MI355_SIG_CHANNELS independent channels -- 0 for host-launched calls, 1 for
+ * stream-ordered ones -- so the two kinds never share pair counts and may be
+ * in flight at the same time. Offsets below are within a channel; the caller
+ * passes sig[] pointers already offset to the channel's base. */
 #define MI355_FUSED_MAX_MEMBERS 32
 #define MI355_FUSED_MAX_BLOCKS 256
 #define MI355_SIG_ARRIVE 0       /* [PE]: pair count of the last call the PE arrived at */
 #define MI355_SIG_RSDONE 1024    /* [PE]: ... whose shard the PE has reduced           */
 #define MI355_SIG_AGDONE 2048    /* [PE]: ... whose gather the PE has finished         */
-#define MI355_SIG_RS_COUNT 3072  /* local block counters (own 128-byte lines)          */
-#define MI355_SIG_AG_COUNT 3088
-#define MI355_SIG_ERROR 3104
-#define MI355_SIG_SELFTEST 3200  /* [PE]: init-time interconnect check */
-#define MI355_SIG_WORDS 4224
+#define MI355_SIG_CALLS 3072     /* [PE]: this PE's pair count of calls with the PE    */
+#define MI355_SIG_RS_COUNT 4096  /* local block counters (own 128-byte lines)          */
+#define MI355_SIG_AG_COUNT 4112
+#define MI355_SIG_ERROR 4128
+#define MI355_SIG_CHANNEL_WORDS 4160
+#define MI355_SIG_CHANNELS 2
+#define MI355_SIG_SELFTEST (MI355_SIG_CHANNELS * MI355_SIG_CHANNEL_WORDS) /* [PE]: init-time check */
+#define MI355_SIG_WORDS (MI355_SIG_SELFTEST + 1024)
 
 typedef struct MI355FusedArgs {
     int op, dtype;
@@ -113,18 +120,30 @@ typedef struct MI355FusedArgs {
     const void *src[MI355_FUSED_MAX_MEMBERS];        /* members' sources (mapped) */
     void *dst[MI355_FUSED_MAX_MEMBERS];              /* members' targets (mapped) */
     unsigned long long *sig[MI355_FUSED_MAX_MEMBERS];/* members' signal regions   */
-    unsigned long long count[MI355_FUSED_MAX_MEMBERS]; /* pair count per member  */
     int pe[MI355_FUSED_MAX_MEMBERS];  /* members' PE numbers (signal slot index)  */
-    unsigned *host_flag;              /* host-coherent completion word            */
+    unsigned *host_flag;              /* host-coherent completion word, or NULL   */
     unsigned epoch;                   /* stored there when done (| 1u<<31: timeout) */
+    unsigned *err_flag;               /* host-coherent; set to 1 on a timeout, or NULL */
     unsigned long long timeout_ticks; /* bound on every wait, 100 MHz ticks       */
 } MI355FusedArgs;
 
 /* Reduce-scatter + all-gather of n elements over the members in ONE launch:
  * every member ends with the fold, in member order, of all members' sources
  * (the reference's result on the first member). Every member must make the
- * matching call; buffers 16-byte aligned; dst == src or disjoint. */
+ * matching call; buffers 16-byte aligned; dst == src or disjoint.
+ *
+ * Pair counts live on the device (MI355_SIG_CALLS): the kernel reads them at
+ * its start and advances them when every member is done, so the call needs
+ * no host state and replays correctly from a captured HIP graph. The
+ * collectives of one PE on one channel (this and mi355_device_barrier) must
+ * run one at a time, in the same order on every member. */
 int mi355_fused_allreduce (const MI355FusedArgs *args, void *stream);
+
+/* Device-side barrier over the members (one 64-lane block): ordered on
+ * `stream` after the work queued before it, and the work queued after it
+ * runs once every member has reached its matching barrier. Uses
+ * nmembers/me/sig/pe/err_flag/host_flag/epoch/timeout_ticks of args. */
+int mi355_device_barrier (const MI355FusedArgs *args, void *stream);
 
 /* One-block kernels for the init-time interconnect check: store `value` to
  * each of n (peer-mapped) words at system scope; load n words at system scope

@@ -61,6 +61,157 @@ void shmemx_kernel_timing (int enable);        /* enable resets the counters */
  * launches timed since the last enable. Synchronizes the stream. */
 void shmemx_kernel_timing_stats (long *launches, double *total_ms, double *avg_ms);
 
+/* Stream-ordered collectives. Enqueued on `stream` (a hipStream_t; NULL =
+ * the null stream) and return at once: the reduction runs after the work
+ * queued on that stream before it, and the work queued after it sees the
+ * result. Cross-PE ordering is device-side (a one-launch fused kernel for
+ * messages up to SHMEM_FUSED_MAX_BYTES, else fold and gather kernels between
+ * one-block device barriers), so a call can be captured into a HIP graph and
+ * replayed; every replay is one more collective for all members.
+ *   - target and source lie in the device symmetric heap, equal or disjoint
+ *   - PE_size <= 32; P2P schedule (results identical on all members, equal
+ *     to the reference's on PE_start) whatever the reduce algorithm setting
+ *   - every member enqueues the same sequence of stream-ordered collectives,
+ *     and one PE's run one at a time: issue them on one stream (or order the
+ *     streams); host-side calls may run meanwhile (separate device flags)
+ *   - a device-side wait that times out (SHMEM_BARRIER_TIMEOUT) is reported
+ *     by the next shmem_barrier_all / shmem_quiet / stream-ordered call
+ * pWrk and pSync are accepted for symmetry with shmem_*_to_all and unused. */
+void shmemx_barrier_on_stream (int PE_start, int logPE_stride, int PE_size, void *stream);
+void shmemx_short_sum_to_all_on_stream (short *target, short *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        short *pWrk, long *pSync, void *stream);
+void shmemx_int_sum_to_all_on_stream (int *target, int *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        int *pWrk, long *pSync, void *stream);
+void shmemx_long_sum_to_all_on_stream (long *target, long *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long *pWrk, long *pSync, void *stream);
+void shmemx_longlong_sum_to_all_on_stream (long long *target, long long *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long long *pWrk, long *pSync, void *stream);
+void shmemx_float_sum_to_all_on_stream (float *target, float *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        float *pWrk, long *pSync, void *stream);
+void shmemx_double_sum_to_all_on_stream (double *target, double *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        double *pWrk, long *pSync, void *stream);
+void shmemx_longdouble_sum_to_all_on_stream (long double *target, long double *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long double *pWrk, long *pSync, void *stream);
+void shmemx_complexf_sum_to_all_on_stream (COMPLEXIFY (float) *target, COMPLEXIFY (float) *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        COMPLEXIFY (float) *pWrk, long *pSync, void *stream);
+void shmemx_complexd_sum_to_all_on_stream (COMPLEXIFY (double) *target, COMPLEXIFY (double) *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        COMPLEXIFY (double) *pWrk, long *pSync, void *stream);
+void shmemx_short_prod_to_all_on_stream (short *target, short *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        short *pWrk, long *pSync, void *stream);
+void shmemx_int_prod_to_all_on_stream (int *target, int *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        int *pWrk, long *pSync, void *stream);
+void shmemx_long_prod_to_all_on_stream (long *target, long *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long *pWrk, long *pSync, void *stream);
+void shmemx_longlong_prod_to_all_on_stream (long long *target, long long *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long long *pWrk, long *pSync, void *stream);
+void shmemx_float_prod_to_all_on_stream (float *target, float *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        float *pWrk, long *pSync, void *stream);
+void shmemx_double_prod_to_all_on_stream (double *target, double *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        double *pWrk, long *pSync, void *stream);
+void shmemx_longdouble_prod_to_all_on_stream (long double *target, long double *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long double *pWrk, long *pSync, void *stream);
+void shmemx_complexf_prod_to_all_on_stream (COMPLEXIFY (float) *target, COMPLEXIFY (float) *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        COMPLEXIFY (float) *pWrk, long *pSync, void *stream);
+void shmemx_complexd_prod_to_all_on_stream (COMPLEXIFY (double) *target, COMPLEXIFY (double) *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        COMPLEXIFY (double) *pWrk, long *pSync, void *stream);
+void shmemx_short_and_to_all_on_stream (short *target, short *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        short *pWrk, long *pSync, void *stream);
+void shmemx_int_and_to_all_on_stream (int *target, int *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        int *pWrk, long *pSync, void *stream);
+void shmemx_long_and_to_all_on_stream (long *target, long *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long *pWrk, long *pSync, void *stream);
+void shmemx_longlong_and_to_all_on_stream (long long *target, long long *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long long *pWrk, long *pSync, void *stream);
+void shmemx_short_or_to_all_on_stream (short *target, short *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        short *pWrk, long *pSync, void *stream);
+void shmemx_int_or_to_all_on_stream (int *target, int *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        int *pWrk, long *pSync, void *stream);
+void shmemx_long_or_to_all_on_stream (long *target, long *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long *pWrk, long *pSync, void *stream);
+void shmemx_longlong_or_to_all_on_stream (long long *target, long long *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long long *pWrk, long *pSync, void *stream);
+void shmemx_short_xor_to_all_on_stream (short *target, short *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        short *pWrk, long *pSync, void *stream);
+void shmemx_int_xor_to_all_on_stream (int *target, int *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        int *pWrk, long *pSync, void *stream);
+void shmemx_long_xor_to_all_on_stream (long *target, long *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long *pWrk, long *pSync, void *stream);
+void shmemx_longlong_xor_to_all_on_stream (long long *target, long long *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long long *pWrk, long *pSync, void *stream);
+void shmemx_short_max_to_all_on_stream (short *target, short *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        short *pWrk, long *pSync, void *stream);
+void shmemx_int_max_to_all_on_stream (int *target, int *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        int *pWrk, long *pSync, void *stream);
+void shmemx_long_max_to_all_on_stream (long *target, long *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long *pWrk, long *pSync, void *stream);
+void shmemx_longlong_max_to_all_on_stream (long long *target, long long *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long long *pWrk, long *pSync, void *stream);
+void shmemx_float_max_to_all_on_stream (float *target, float *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        float *pWrk, long *pSync, void *stream);
+void shmemx_double_max_to_all_on_stream (double *target, double *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        double *pWrk, long *pSync, void *stream);
+void shmemx_longdouble_max_to_all_on_stream (long double *target, long double *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long double *pWrk, long *pSync, void *stream);
+void shmemx_short_min_to_all_on_stream (short *target, short *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        short *pWrk, long *pSync, void *stream);
+void shmemx_int_min_to_all_on_stream (int *target, int *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        int *pWrk, long *pSync, void *stream);
+void shmemx_long_min_to_all_on_stream (long *target, long *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long *pWrk, long *pSync, void *stream);
+void shmemx_longlong_min_to_all_on_stream (long long *target, long long *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long long *pWrk, long *pSync, void *stream);
+void shmemx_float_min_to_all_on_stream (float *target, float *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        float *pWrk, long *pSync, void *stream);
+void shmemx_double_min_to_all_on_stream (double *target, double *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        double *pWrk, long *pSync, void *stream);
+void shmemx_longdouble_min_to_all_on_stream (long double *target, long double *source,
+        int nreduce, int PE_start, int logPE_stride, int PE_size,
+        long double *pWrk, long *pSync, void *stream);
+
+
 #ifdef __cplusplus
 }
 #endif

@@ -23,9 +23,13 @@
 //            epoch to the host-coherent flag
 //
 // Pair counts instead of a reset protocol: PE p's slot for PE q only ever
-// grows by one per reduction both take part in, so a member that runs ahead
+// grows by one per collective both take part in, so a member that runs ahead
 // into the next call can never satisfy a wait of the current one too early
-// (the same argument as the host barrier in runtime.c).
+// (the same argument as the host barrier in runtime.c). The counts are kept
+// on the device (CALLS[q] of this PE's region): every block reads them when it
+// starts, and the last block advances them once all members are done -- by
+// then every block has started, so none can read an advanced count. No host
+// state is involved, which is what lets a captured HIP graph replay the call.
 //
 // All blocks of the grid must be co-resident (they wait on each other's last
 // block): the grid is at most kFusedMaxBlocks, far below one block per CU.
@@ -53,9 +57,16 @@ __device__ __forceinline__ void st16_sys(u32x4 *p, u32x4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
 }
 
-// Wait until slot `base + pe[i]` of this PE's signal region holds count[i]
+// This call's pair count with every member (lanes of wave 0, into LDS).
+__device__ void load_counts(const MI355FusedArgs &a, const unsigned long long *mine, unsigned long long *cnt) {
+    if (threadIdx.x < a.nmembers) cnt[threadIdx.x] = ld_sys_u64(mine + MI355_SIG_CALLS + a.pe[threadIdx.x]) + 1;
+    __syncthreads();
+}
+
+// Wait until slot `base + pe[i]` of this PE's signal region holds cnt[i]
 // for every member i; lanes i < nmembers of wave 0 poll one member each.
-__device__ bool wait_members(const MI355FusedArgs &a, const unsigned long long *mine, int base, bool include_self) {
+__device__ bool wait_members(const MI355FusedArgs &a, const unsigned long long *mine, const unsigned long long *cnt,
+                             int base, bool include_self) {
     bool ok = true;
     if (threadIdx.x < 64) {
         const int i = threadIdx.x;
@@ -63,7 +74,7 @@ __device__ bool wait_members(const MI355FusedArgs &a, const unsigned long long *
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         unsigned spins = 0;
         while (true) {
-            bool done = !need || ld_sys_u64(mine + base + a.pe[i]) >= a.count[i];
+            bool done = !need || ld_sys_u64(mine + base + a.pe[i]) >= cnt[i];
             if (__all(done)) break;
             if ((++spins & 63u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
                 ok = false;
@@ -94,10 +105,25 @@ __device__ bool last_block(unsigned long long *counter) {
     return is_last != 0;
 }
 
-__device__ void publish(const MI355FusedArgs &a, int base) {
+__device__ void publish(const MI355FusedArgs &a, const unsigned long long *cnt, int base) {
     // lanes of wave 0: one member each (this PE included)
-    if (threadIdx.x < a.nmembers)
-        st_sys_u64(a.sig[threadIdx.x] + base + a.pe[a.me], a.count[threadIdx.x]);
+    if (threadIdx.x < a.nmembers) st_sys_u64(a.sig[threadIdx.x] + base + a.pe[a.me], cnt[threadIdx.x]);
+}
+
+// Advance the pair counts (the call is over on every member), then report.
+__device__ void finish(const MI355FusedArgs &a, unsigned long long *mine, const unsigned long long *cnt, bool ok) {
+    if (ok && threadIdx.x < a.nmembers) st_sys_u64(mine + MI355_SIG_CALLS + a.pe[threadIdx.x], cnt[threadIdx.x]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (!ok) {
+            st_sys_u64(mine + MI355_SIG_ERROR, 1);
+            if (a.err_flag) __hip_atomic_store(a.err_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (a.host_flag)
+            __hip_atomic_store(a.host_flag, ok ? a.epoch : (a.epoch | 0x80000000u), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
 }
 
 template <int OP, typename T>
@@ -105,15 +131,17 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
     constexpr int V = 16 / sizeof(T);
     unsigned long long *mine = a.sig[a.me];
     __shared__ int ok_all;
+    __shared__ unsigned long long cnt[MI355_FUSED_MAX_MEMBERS];
     if (threadIdx.x == 0) ok_all = 1;
+    load_counts(a, mine, cnt);
 
     // ---- arrive
     if (blockIdx.x == 0) {
         if (threadIdx.x < a.nmembers && threadIdx.x != a.me)
-            st_sys_u64(a.sig[threadIdx.x] + MI355_SIG_ARRIVE + a.pe[a.me], a.count[threadIdx.x]);
+            st_sys_u64(a.sig[threadIdx.x] + MI355_SIG_ARRIVE + a.pe[a.me], cnt[threadIdx.x]);
     }
     __syncthreads();
-    if (!wait_members(a, mine, MI355_SIG_ARRIVE, false)) ok_all = 0;
+    if (!wait_members(a, mine, cnt, MI355_SIG_ARRIVE, false)) ok_all = 0;
     __syncthreads();
     if (!ok_all) goto fail;
 
@@ -149,10 +177,10 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
                 if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // plain tail stores
             }
         }
-        if (last_block(mine + MI355_SIG_RS_COUNT)) publish(a, MI355_SIG_RSDONE);
+        if (last_block(mine + MI355_SIG_RS_COUNT)) publish(a, cnt, MI355_SIG_RSDONE);
 
         // ---- every shard is reduced
-        if (!wait_members(a, mine, MI355_SIG_RSDONE, true)) ok_all = 0;
+        if (!wait_members(a, mine, cnt, MI355_SIG_RSDONE, true)) ok_all = 0;
         __syncthreads();
         if (!ok_all) goto fail;
 
@@ -178,22 +206,30 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
         if (__syncthreads_or(tail_plain) && threadIdx.x == 0)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the element tail went through L2
         if (last_block(mine + MI355_SIG_AG_COUNT)) {
-            publish(a, MI355_SIG_AGDONE);
+            publish(a, cnt, MI355_SIG_AGDONE);
             __syncthreads();
-            const bool ok = wait_members(a, mine, MI355_SIG_AGDONE, true);
-            if (threadIdx.x == 0) {
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                __hip_atomic_store(a.host_flag, ok ? a.epoch : (a.epoch | 0x80000000u), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_SYSTEM);
-            }
+            if (!wait_members(a, mine, cnt, MI355_SIG_AGDONE, true)) ok_all = 0;
+            __syncthreads();
+            finish(a, mine, cnt, ok_all != 0);
         }
         return;
     }
 fail:
-    if (threadIdx.x == 0) {
-        st_sys_u64(mine + MI355_SIG_ERROR, 1);
-        __hip_atomic_store(a.host_flag, a.epoch | 0x80000000u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    finish(a, mine, cnt, false);
+}
+
+// Device barrier: one block; lanes of wave 0 handle one member each.
+__global__ __launch_bounds__(64) void device_barrier(MI355FusedArgs a) {
+    unsigned long long *mine = a.sig[a.me];
+    __shared__ unsigned long long cnt[MI355_FUSED_MAX_MEMBERS];
+    load_counts(a, mine, cnt);
+    // the work queued before this kernel completed (kernel boundary); make
+    // it visible at system scope before peers are told
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    if (threadIdx.x < a.nmembers && threadIdx.x != a.me)
+        st_sys_u64(a.sig[threadIdx.x] + MI355_SIG_ARRIVE + a.pe[a.me], cnt[threadIdx.x]);
+    const bool ok = wait_members(a, mine, cnt, MI355_SIG_ARRIVE, false);
+    finish(a, mine, cnt, ok);
 }
 
 template <typename T>
@@ -269,10 +305,11 @@ extern "C" int mi355_fused_allreduce(const MI355FusedArgs *a, void *stream) {
     if (a->nmembers < 2 || a->nmembers > MI355_FUSED_MAX_MEMBERS || a->me < 0 || a->me >= a->nmembers)
         return MI355_E_INVAL;
     const size_t es = mi355_dtype_size(a->dtype);
-    if (a->shard == 0 || (a->shard * es) % 16 != 0 || a->host_flag == nullptr) return MI355_E_INVAL;
+    if (a->shard == 0 || (a->shard * es) % 16 != 0) return MI355_E_INVAL;
     for (int i = 0; i < a->nmembers; ++i)
         if (a->src[i] == nullptr || a->dst[i] == nullptr || a->sig[i] == nullptr ||
-            (((uintptr_t)a->src[i] | (uintptr_t)a->dst[i]) & 15) != 0)
+            (((uintptr_t)a->src[i] | (uintptr_t)a->dst[i]) & 15) != 0 || a->pe[i] < 0 ||
+            a->pe[i] >= MI355_SIG_RSDONE)
             return MI355_E_INVAL;
     // enough blocks for the larger of the two legs, all of them co-resident
     const uint64_t vecs = (a->shard * es / 16) * (uint64_t)(a->nmembers - 1);
@@ -292,4 +329,15 @@ extern "C" int mi355_fused_allreduce(const MI355FusedArgs *a, void *stream) {
     case MI355_COMPLEXD: return launch_op<cplxd>(*a, (unsigned)grid, st);
     default: return MI355_E_INVAL;
     }
+}
+
+extern "C" int mi355_device_barrier(const MI355FusedArgs *a, void *stream) {
+    if (a == nullptr || a->nmembers < 1 || a->nmembers > MI355_FUSED_MAX_MEMBERS || a->me < 0 ||
+        a->me >= a->nmembers)
+        return MI355_E_INVAL;
+    for (int i = 0; i < a->nmembers; ++i)
+        if (a->sig[i] == nullptr || a->pe[i] < 0 || a->pe[i] >= MI355_SIG_RSDONE) return MI355_E_INVAL;
+    hipLaunchKernelGGL(device_barrier, dim3(1), dim3(64), 0, (hipStream_t)stream, *a);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
 }

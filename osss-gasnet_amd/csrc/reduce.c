@@ -38,6 +38,8 @@
 #include "shmemx.h"
 #include "shmemi.h"
 
+enum { SHMEMI_CHAN_HOST = 0, SHMEMI_CHAN_STREAM = 1 }; /* signal-region channels */
+
 struct aset {
     int start, stride, size, me; /* me = index of this PE in the set */
 };
@@ -155,6 +157,7 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
 static int fused_eligible (size_t es, size_t dst_off, size_t src_off, size_t n, const struct aset *s)
 {
     return s->size > 1 && s->size <= MI355_FUSED_MAX_MEMBERS && n * es <= shmemi.fused_max &&
+           shmemi.npes <= MI355_SIG_RSDONE &&
            shmemi.sigmem != NULL && ((dst_off | src_off) & 15) == 0 && es <= 256 &&
            (dst_off == src_off || !ranges_overlap (dst_off, src_off, n * es)) &&
            shmemi.algorithm != SHMEMX_REDUCE_EXACT;
@@ -176,11 +179,11 @@ static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t sr
         a.pe[i] = pe;
         a.src[i] = shmemi_peer_ptr (pe, src_off);
         a.dst[i] = shmemi_peer_ptr (pe, dst_off);
-        a.sig[i] = shmemi.peer_sig[pe];
-        a.count[i] = ++shmemi.fused_count[pe];
+        a.sig[i] = shmemi.peer_sig[pe] + SHMEMI_CHAN_HOST * MI355_SIG_CHANNEL_WORDS;
     }
     a.host_flag = shmemi.sig_flag;
     a.epoch = shmemi_next_epoch ();
+    a.err_flag = shmemi.stream_err;
     a.timeout_ticks = (unsigned long long) (shmemi.barrier_timeout * 1e8);
     const int rc = mi355_fused_allreduce (&a, shmemi.stream);
     if (rc != 0)
@@ -419,6 +422,183 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
 }
 
 /* ---------------------------------------------------------------------- */
+/* stream-ordered collectives (shmemx.h)                                   */
+/* ---------------------------------------------------------------------- */
+/* The same P2P schedule, enqueued on the caller's stream with no host wait:
+ * cross-PE ordering is device-side (fused.hip's pair counts), so a caller can
+ * overlap the reduction with its own kernels or capture it into a HIP graph.
+ *   fused-eligible   one launch of the fused kernel
+ *   otherwise        device barrier, fold of shard `me`, device barrier,
+ *                    gather, device barrier -- the host schedule's three
+ *                    barriers, each a one-block kernel instead of a host wait
+ They use their own signal-region channel, so a host-launched fused call may
+ * run while they are in flight; among themselves they must run one at a time
+ * per PE (one stream, or streams the caller orders). Errors of device-side
+ * waits (a peer never arrives within SHMEM_BARRIER_TIMEOUT) surface at the
+ * next library call. */
+
+void shmemi_check_stream_err (const char *fn)
+{
+    if (shmemi.stream_err != NULL && __atomic_load_n (shmemi.stream_err, __ATOMIC_ACQUIRE) != 0)
+        shmemi_fatal ("%s: a stream-ordered collective timed out waiting for another PE", fn);
+}
+
+static void stream_begin (const char *fn)
+{
+    shmemi_init_check (fn);
+    if (shmemi.heap == NULL)
+        shmemi_fatal ("%s: no GPU (SHMEM_BOOTSTRAP_ONLY set?)", fn);
+    shmemi_check_stream_err (fn);
+}
+
+static void stream_members (MI355FusedArgs *a, const struct aset *s)
+{
+    memset (a, 0, sizeof *a);
+    a->nmembers = s->size;
+    a->me = s->me;
+    for (int i = 0; i < s->size; ++i) {
+        a->pe[i] = aset_pe (s, i);
+        a->sig[i] = shmemi.peer_sig[a->pe[i]] + SHMEMI_CHAN_STREAM * MI355_SIG_CHANNEL_WORDS;
+    }
+    a->err_flag = shmemi.stream_err;
+    a->timeout_ticks = (unsigned long long) (shmemi.barrier_timeout * 1e8);
+}
+
+static void stream_aset (const char *fn, struct aset *s, int PE_start, int logPE_stride, int PE_size)
+{
+    if (logPE_stride < 0 || logPE_stride > 30 || PE_size < 1 || PE_start < 0 ||
+        PE_start + (long) (PE_size - 1) * (1L << logPE_stride) >= shmemi.npes)
+        shmemi_fatal ("%s: active set (PE_start %d, logPE_stride %d, PE_size %d) outside the %d PEs",
+                      fn, PE_start, logPE_stride, PE_size, shmemi.npes);
+    s->start = PE_start;
+    s->stride = 1 << logPE_stride;
+    s->size = PE_size;
+    s->me = -1;
+    for (int i = 0; i < PE_size; ++i)
+        if (aset_pe (s, i) == shmemi.mype)
+            s->me = i;
+    if (s->me < 0)
+        shmemi_fatal ("%s: PE %d is not in the active set (PE_start %d, logPE_stride %d, PE_size %d)",
+                      fn, shmemi.mype, PE_start, logPE_stride, PE_size);
+    if (PE_size > MI355_FUSED_MAX_MEMBERS || shmemi.npes > MI355_SIG_RSDONE)
+        shmemi_fatal ("%s: stream-ordered collectives take at most %d PEs per active set (of at most %d)",
+                      fn, MI355_FUSED_MAX_MEMBERS, MI355_SIG_RSDONE);
+    if (PE_size > 1 && (shmemi.sigmem == NULL || shmemi.p2p_broken || shmemi.sig_broken))
+        shmemi_fatal ("%s: peer GPU memory failed the init self-test", fn);
+}
+
+static void stream_barrier (const char *fn, const struct aset *s, hipStream_t st)
+{
+    if (s->size < 2)
+        return;
+    MI355FusedArgs a;
+    stream_members (&a, s);
+    const int rc = mi355_device_barrier (&a, st);
+    if (rc != 0)
+        shmemi_fatal ("%s: device barrier launch failed: %d", fn, rc);
+}
+
+static void stream_copy (const char *fn, void *const *dsts, const void *const *srcs, const size_t *nb, int k,
+                         hipStream_t st)
+{
+    for (int base = 0; base < k; base += 64) {
+        const int m = k - base < 64 ? k - base : 64;
+        const int rc = mi355_copy_segments (dsts + base, srcs + base, nb + base, m, st);
+        if (rc != 0)
+            shmemi_fatal ("%s: copy kernel launch failed: %d", fn, rc);
+    }
+}
+
+static void reduce_on_stream (int op, int dtype, const char *fn, void *target, const void *source, int nreduce,
+                              int PE_start, int logPE_stride, int PE_size, void *stream)
+{
+    hipStream_t st = (hipStream_t) stream;
+    stream_begin (fn);
+    struct aset s;
+    stream_aset (fn, &s, PE_start, logPE_stride, PE_size);
+    if (nreduce < 0)
+        shmemi_fatal ("%s: nreduce %d < 0", fn, nreduce);
+    const size_t es = mi355_dtype_size (dtype);
+    const size_t n = (size_t) nreduce;
+    const size_t nbytes = n * es;
+    if (n > 0 && (target == NULL || source == NULL || !shmemi_in_device_heap (target, nbytes) ||
+                  !shmemi_in_device_heap (source, nbytes)))
+        shmemi_fatal ("%s: target and source must lie in the device symmetric heap (shmemx_malloc_device)", fn);
+    if (n > 0 && target != source && ranges_overlap ((size_t) target, (size_t) source, nbytes))
+        shmemi_fatal ("%s: target and source overlap without being equal", fn);
+
+    if (n == 0) {
+        stream_barrier (fn, &s, st);
+    } else if (s.size == 1) {
+        if (target != source) {
+            void *d = target;
+            const void *sv = source;
+            stream_copy (fn, &d, &sv, &nbytes, 1, st);
+        }
+    } else {
+        const size_t dst_off = shmemi_heap_offset (target), src_off = shmemi_heap_offset (source);
+        MI355FusedArgs a;
+        stream_members (&a, &s);
+        if (n * es <= shmemi.fused_max && ((dst_off | src_off) & 15) == 0 && es <= 256) {
+            a.op = op;
+            a.dtype = dtype;
+            a.n = n;
+            a.shard = shard_chunk (n, es, s.size);
+            for (int i = 0; i < s.size; ++i) {
+                a.src[i] = shmemi_peer_ptr (a.pe[i], src_off);
+                a.dst[i] = shmemi_peer_ptr (a.pe[i], dst_off);
+            }
+            const int rc = mi355_fused_allreduce (&a, st);
+            if (rc != 0)
+                shmemi_fatal ("%s: fused reduction launch failed: %d", fn, rc);
+        } else {
+            const void **sp = (const void **) malloc (sizeof (void *) * (size_t) s.size);
+            void **dsts = (void **) malloc (sizeof (void *) * (size_t) s.size);
+            size_t *nb = (size_t *) malloc (sizeof (size_t) * (size_t) s.size);
+            if (sp == NULL || dsts == NULL || nb == NULL)
+                shmemi_fatal ("out of host memory");
+            size_t lo, hi;
+            mi355_shard_bounds (n, es, s.size, s.me, &lo, &hi);
+            stream_barrier (fn, &s, st); /* every source is ready */
+            if (hi > lo) {
+                for (int i = 0; i < s.size; ++i)
+                    sp[i] = shmemi_peer_ptr (a.pe[i], src_off + lo * es);
+                const int rc = mi355_combine (op, dtype, shmemi_peer_ptr (shmemi.mype, dst_off + lo * es), sp,
+                                              s.size, hi - lo, st);
+                if (rc != 0)
+                    shmemi_fatal ("%s: combine kernel launch failed: %d", fn, rc);
+            }
+            stream_barrier (fn, &s, st); /* every shard is reduced */
+            int k = 0;
+            for (int i = 0; i < s.size; ++i) {
+                size_t l, h;
+                mi355_shard_bounds (n, es, s.size, i, &l, &h);
+                if (i == s.me || h <= l)
+                    continue;
+                dsts[k] = shmemi_peer_ptr (shmemi.mype, dst_off + l * es);
+                sp[k] = shmemi_peer_ptr (a.pe[i], dst_off + l * es);
+                nb[k] = (h - l) * es;
+                ++k;
+            }
+            stream_copy (fn, dsts, sp, nb, k, st);
+            stream_barrier (fn, &s, st); /* peers are done reading this target */
+            free (nb);
+            free (dsts);
+            free (sp);
+        }
+    }
+}
+
+void shmemx_barrier_on_stream (int PE_start, int logPE_stride, int PE_size, void *stream)
+{
+    hipStream_t st = (hipStream_t) stream;
+    stream_begin ("shmemx_barrier_on_stream");
+    struct aset s;
+    stream_aset ("shmemx_barrier_on_stream", &s, PE_start, logPE_stride, PE_size);
+    stream_barrier ("shmemx_barrier_on_stream", &s, st);
+}
+
+/* ---------------------------------------------------------------------- */
 /* the 44 entry points (reduce-op.c:388-448), pshmem_ strong, shmem_ weak  */
 /* ---------------------------------------------------------------------- */
 #define SHMEMI_REDUCE(Name, Op, Type, DT, OPC)                                                      \
@@ -428,6 +608,15 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
         (void) pWrk; /* scratch lives in the device heap; pWrk is not touched */                   \
         reduce_impl (OPC, DT, "shmem_" #Name "_" #Op "_to_all", target, source, nreduce, PE_start,  \
                      logPE_stride, PE_size, pSync);                                                  \
+    }                                                                                                \
+    void shmemx_##Name##_##Op##_to_all_on_stream (Type *target, Type *source, int nreduce,           \
+                                                  int PE_start, int logPE_stride, int PE_size,       \
+                                                  Type *pWrk, long *pSync, void *stream)             \
+    {                                                                                                \
+        (void) pWrk;                                                                                 \
+        (void) pSync;                                                                                \
+        reduce_on_stream (OPC, DT, "shmemx_" #Name "_" #Op "_to_all_on_stream", target, source,     \
+                          nreduce, PE_start, logPE_stride, PE_size, stream);                         \
     }                                                                                                \
     void shmem_##Name##_##Op##_to_all (Type *target, Type *source, int nreduce, int PE_start,        \
                                        int logPE_stride, int PE_size, Type *pWrk, long *pSync)       \

@@ -339,12 +339,14 @@ static void heap_init (void)
 static void signal_init (void)
 {
     void *h = NULL, *d = NULL;
-    SHMEMI_HIP (hipHostMalloc (&h, 64, hipHostMallocCoherent | hipHostMallocMapped));
+    SHMEMI_HIP (hipHostMalloc (&h, 128, hipHostMallocCoherent | hipHostMallocMapped));
     SHMEMI_HIP (hipHostGetDevicePointer (&d, h, 0));
     if (d != h)
         shmemi_fatal ("host-coherent signal word maps to a different device address");
     shmemi.sig_flag = (unsigned *) h;
     *shmemi.sig_flag = 0;
+    shmemi.stream_err = (unsigned *) ((char *) h + 64); /* own cache line */
+    *shmemi.stream_err = 0;
     SHMEMI_HIP (hipMalloc (&d, 64));
     SHMEMI_HIP (hipMemset (d, 0, 64));
     SHMEMI_HIP (hipDeviceSynchronize ());
@@ -405,15 +407,14 @@ unsigned shmemi_wait_flag (unsigned want)
 static void sigmem_init (void)
 {
     void *p = NULL;
-    const size_t bytes = 65536;
-    _Static_assert (MI355_SIG_WORDS * 8 <= 65536, "signal region too small");
+    const size_t bytes = 131072;
+    _Static_assert (MI355_SIG_WORDS * 8 <= 131072, "signal region too small");
     SHMEMI_HIP (hipExtMallocWithFlags (&p, bytes, hipDeviceMallocUncached));
     SHMEMI_HIP (hipMemset (p, 0, bytes));
     SHMEMI_HIP (hipDeviceSynchronize ());
     shmemi.sigmem = (unsigned long long *) p;
     shmemi.peer_sig = (unsigned long long **) calloc ((size_t) shmemi.npes, sizeof (void *));
-    shmemi.fused_count = (unsigned long long *) calloc ((size_t) shmemi.npes, sizeof (unsigned long long));
-    if (shmemi.peer_sig == NULL || shmemi.fused_count == NULL)
+    if (shmemi.peer_sig == NULL)
         shmemi_fatal ("out of host memory");
     shmemi.peer_sig[shmemi.mype] = shmemi.sigmem;
 }
@@ -537,6 +538,7 @@ static void interconnect_selftest (void)
             fprintf (stderr, "[shmem] warning: peer signal-region stores are not visible; "
                              "the fused small-message kernel is disabled\n");
         shmemi.fused_max = 0;
+        shmemi.sig_broken = 1;
     }
     if (!all_heap) {
         if (me == 0)
@@ -785,9 +787,11 @@ void pshmem_finalize (void)
 {
     if (!shmemi.initialized)
         return;
-    shmem_barrier_all ();
-    if (shmemi.device >= 0)
+    /* stream-ordered collectives still queued on the caller's streams finish
+     * first (they only wait on peers' kernels that are already enqueued) */
+    if (shmemi.device >= 0 && shmemi.heap != NULL)
         (void) hipDeviceSynchronize ();
+    shmem_barrier_all ();
     if (shmemi.rccl_comm != NULL) {
         extern void shmemi_rccl_destroy (void);
         shmemi_rccl_destroy ();
@@ -821,9 +825,8 @@ void pshmem_finalize (void)
         (void) hipFree (shmemi.sigmem);
     shmemi.sigmem = NULL;
     free (shmemi.peer_sig);
-    free (shmemi.fused_count);
     shmemi.peer_sig = NULL;
-    shmemi.fused_count = NULL;
+    shmemi.stream_err = NULL;
     if (shmemi.sig_flag != NULL)
         (void) hipHostFree (shmemi.sig_flag);
     if (shmemi.sig_count != NULL)
@@ -877,6 +880,7 @@ int pshmem_n_pes (void) { return shmemi.initialized ? shmemi.npes : 1; }
 void pshmem_barrier_all (void)
 {
     shmemi_init_check ("shmem_barrier_all");
+    shmemi_check_stream_err ("shmem_barrier_all");
     if (shmemi.stream != NULL)
         SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
     shmemi_barrier_set (0, 1, shmemi.npes);
@@ -899,6 +903,8 @@ void pshmem_quiet (void)
 {
     if (shmemi.initialized && shmemi.stream != NULL)
         SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    if (shmemi.initialized)
+        shmemi_check_stream_err ("shmem_quiet");
 }
 
 /* shmem_ names are weak aliases of the pshmem_ ones (PSHMEM, reference

@@ -97,13 +97,16 @@ struct shmemi_state {
     /* signal region for the fused kernel: uncached device memory, mapped by peers */
     unsigned long long *sigmem;
     unsigned long long **peer_sig;  /* [npes] */
-    unsigned long long *fused_count;/* [npes]: fused reductions shared with each PE */
     size_t fused_max;           /* SHMEM_FUSED_MAX_BYTES: largest message on the fused path */
+    int sig_broken;             /* peers' signal-region stores failed the init self-test */
 
     /* completion signal: host-coherent word the last block of a kernel writes */
     unsigned *sig_flag;         /* hipHostMalloc coherent+mapped, same address on both sides */
     unsigned *sig_count;        /* device word, 0 between launches */
     unsigned sig_epoch;
+
+    /* stream-ordered collectives (shmemx_*_on_stream, streamops.c) */
+    unsigned *stream_err;       /* host-coherent: a device-side wait timed out */
 
     /* kernel timing */
     int timing;
@@ -123,6 +126,7 @@ int shmemi_in_device_heap (const void *p, size_t nbytes);
 size_t shmemi_heap_offset (const void *p);
 void *shmemi_peer_ptr (int pe, size_t off);
 void shmemi_order_after_caller (int host_wait);
+void shmemi_check_stream_err (const char *fn);
 void shmemi_arm_signal (void);
 void shmemi_wait_signal (void);
 unsigned shmemi_next_epoch (void);

@@ -42,6 +42,7 @@ def load(path=LIB_PATH):
         "shmem_barrier_all": ([], None),
         "shmem_barrier": ([_i, _i, _i, _vp], None),
         "shmem_global_exit": ([_i], None),
+        "shmemx_barrier_on_stream": ([_i, _i, _i, _vp], None),
         "shmemx_malloc_device": ([_sz], _vp), "shmemx_free_device": ([_vp], None),
         "shmemx_is_device_symmetric": ([_vp], _i),
         "shmemx_set_reduce_algorithm": ([_i], _i), "shmemx_get_reduce_algorithm": ([], _i),
@@ -132,6 +133,58 @@ class Shmem:
         if pSync is None:
             pSync = self._psync_ptr
         self._reduction(op, dtype)(target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync)
+
+    def _stream_reduction(self, op, dtype):
+        key = ("stream", op, dtype)
+        f = self._fns.get(key)
+        if f is None:
+            f = getattr(self.lib, f"shmemx_{dtype}_{op}_to_all_on_stream")
+            f.restype = None
+            f.argtypes = [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp]
+            self._fns[key] = f
+        return f
+
+    # ---- stream-ordered variants (include/shmemx.h)
+    def to_all_on_stream(self, op, dtype, target, source, nreduce, PE_start, logPE_stride, PE_size, stream):
+        self._stream_reduction(op, dtype)(target, source, nreduce, PE_start, logPE_stride, PE_size, None,
+                                          self._psync_ptr, stream)
+
+    def barrier_on_stream(self, PE_start, logPE_stride, PE_size, stream):
+        self.lib.shmemx_barrier_on_stream(PE_start, logPE_stride, PE_size, stream)
+
+    # ---- HIP streams and graphs, for callers of the stream-ordered API
+    #      (resolved through the library's own libamdhip64 dependency)
+    def _hip(self, name, *args):
+        rc = getattr(self.lib, name)(*args)
+        if rc != 0:
+            raise RuntimeError(f"{name} failed: {rc}")
+
+    def stream_create(self):
+        s = _vp()
+        self._hip("hipStreamCreate", ctypes.byref(s))
+        return s.value
+
+    def stream_sync(self, stream):
+        self._hip("hipStreamSynchronize", _vp(stream))
+
+    def stream_destroy(self, stream):
+        self._hip("hipStreamDestroy", _vp(stream))
+
+    def capture_begin(self, stream, mode=2):  # hipStreamCaptureModeRelaxed
+        self._hip("hipStreamBeginCapture", _vp(stream), _i(mode))
+
+    def capture_end(self, stream):
+        g, e = _vp(), _vp()
+        self._hip("hipStreamEndCapture", _vp(stream), ctypes.byref(g))
+        self._hip("hipGraphInstantiate", ctypes.byref(e), g, None, None, _sz(0))
+        return g.value, e.value
+
+    def graph_launch(self, exe, stream):
+        self._hip("hipGraphLaunch", _vp(exe), _vp(stream))
+
+    def graph_destroy(self, graph, exe):
+        self._hip("hipGraphExecDestroy", _vp(exe))
+        self._hip("hipGraphDestroy", _vp(graph))
 
     # ---- the combine layer (include/mi355_reduce.h)
     def combine(self, op, dtype, dst, srcs, n, stream=None):

@@ -96,6 +96,59 @@ def run_datamove(shm, c, me, da, db, ha, hb, results):
     results[str(c["id"])] = got
 
 
+def run_stream(shm, c, me, da, db, results):
+    """kind "stream": a chain of `chain` stream-ordered reductions on one HIP
+    stream, buf[i+1] <- reduce(buf[i]), enqueued back to back with no host
+    wait; or (graph > 0) the same chain captured once into a HIP graph and
+    replayed `graph` times with a fresh input each time."""
+    op, dtype, n, k = c["op"], c["dtype"], c["n"], c["chain"]
+    es = np.dtype(shmem_reduce.NP[dtype]).itemsize
+    off = c.get("offset", 0)                      # elements off 16-byte alignment
+    stride = ((n + off) * es + 255) // 256 * 256 + 256
+    base = shm.malloc_device(stride * (k + 1))    # collective: every PE allocates
+    mine = None
+    for s in c["sets"]:
+        if me in members(*s):
+            mine = s
+    if mine is not None:
+        bufs = [base + i * stride + off * es for i in range(k + 1)]
+        st = shm.stream_create()
+
+        def enqueue():
+            for i in range(k):
+                shm.to_all_on_stream(op, dtype, bufs[i + 1], bufs[i], n, *mine, st)
+                if c.get("barriers"):
+                    shm.barrier_on_stream(*mine, st)
+
+        replays = c.get("graph", 0)
+        if replays:
+            shm.capture_begin(st)
+            enqueue()
+            graph, exe = shm.capture_end(st)
+            for r in range(replays):
+                if n:
+                    shm.put(bufs[0], source(op, dtype, n, c["seed"] + r, me))
+                shm.graph_launch(exe, st)
+                shm.stream_sync(st)
+                results[f"{c['id']}_r{r}"] = shm.get(bufs[k], n, dtype)
+            shm.graph_destroy(graph, exe)
+        else:
+            if n:
+                shm.put(bufs[0], source(op, dtype, n, c["seed"], me))
+                if c.get("mixed"):
+                    shm.put(da, source(op, dtype, n, c["seed"] + 1, me))
+            enqueue()
+            if c.get("mixed"):
+                # a host-side call while the stream chain is in flight
+                shm.to_all(op, dtype, db, da, n, *mine)
+                results[f"{c['id']}_host"] = shm.get(db, n, dtype)
+            shm.stream_sync(st)
+            for i in range(1, k + 1):
+                results[f"{c['id']}_{i}"] = shm.get(bufs[i], n, dtype)
+        shm.stream_destroy(st)
+    shm.free_device(base)
+
+
 def main():
     spec = json.load(open(sys.argv[1]))
     outdir = sys.argv[2]
@@ -107,6 +160,9 @@ def main():
     ha, hb = shm.malloc(maxb), shm.malloc(maxb)
     results = {}
     for c in spec["cases"]:
+        if c.get("kind") == "stream":
+            run_stream(shm, c, me, da, db, results)
+            continue
         if c.get("kind", "reduce") != "reduce":
             run_datamove(shm, c, me, da, db, ha, hb, results)
             continue

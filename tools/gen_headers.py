@@ -32,6 +32,19 @@ def protos(prefix):
     return "\n".join(out)
 
 
+def stream_protos():
+    """shmemx.h: the stream-ordered variants (same arguments, plus the stream)."""
+    out = []
+    for op, names in MATRIX:
+        for n in names:
+            t = TYPES[n]
+            out.append(f"void shmemx_{n}_{op}_to_all_on_stream ({t} *target, {t} *source,\n"
+                       f"        int nreduce, int PE_start, int logPE_stride, int PE_size,\n"
+                       f"        {t} *pWrk, long *pSync, void *stream);")
+    return "\n".join(out)
+
+
 if __name__ == "__main__":
     import sys
-    print(protos(sys.argv[1] if len(sys.argv) > 1 else "shmem"))
+    arg = sys.argv[1] if len(sys.argv) > 1 else "shmem"
+    print(stream_protos() if arg == "stream" else protos(arg))
