@@ -71,9 +71,10 @@ void shmemx_kernel_timing_stats (long *launches, double *total_ms, double *avg_m
  *   - target and source lie in the device symmetric heap, equal or disjoint
  *   - PE_size <= 32; P2P schedule (results identical on all members, equal
  *     to the reference's on PE_start) whatever the reduce algorithm setting
- *   - every member enqueues the same sequence of stream-ordered collectives,
- *     and one PE's run one at a time: issue them on one stream (or order the
- *     streams); host-side calls may run meanwhile (separate device flags)
+ *   - every member issues the same sequence of collectives, host-side and
+ *     stream-ordered interleaved in the same order; one PE's stream-ordered
+ *     calls run one at a time: one stream, or streams the caller orders
+ *     (host-side calls use separate device flags and may overlap them)
  *   - a device-side wait that times out (SHMEM_BARRIER_TIMEOUT) is reported
  *     by the next shmem_barrier_all / shmem_quiet / stream-ordered call
  * pWrk and pSync are accepted for symmetry with shmem_*_to_all and unused. */

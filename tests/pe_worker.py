@@ -149,17 +149,45 @@ def run_stream(shm, c, me, da, db, results):
     shm.free_device(base)
 
 
+def run_config(shm, c, me, results):
+    """kind "config": a BASELINE.json config at its full size with SURVEY
+    §8(d)'s inputs (tests/_configs.py); saves digests, not whole arrays.
+    c5: `calls` back-to-back calls cycling over `slots` source/target pairs."""
+    import _configs
+    op, dtype = _configs.CONFIGS[c["config"]]
+    n, slots, calls = c["n"], c.get("slots", 1), c.get("calls", 1)
+    es = np.dtype(shmem_reduce.NP[dtype]).itemsize
+    stride = (n * es + 255) // 256 * 256
+    src, dst = shm.malloc_device(stride * slots), shm.malloc_device(stride * slots)
+    for k in range(slots):
+        shm.put(src + k * stride, _configs.source(c["config"], n, me, k))
+    shm.barrier_all()
+    for j in range(calls):
+        k = j % slots
+        shm.to_all(op, dtype, dst + k * stride, src + k * stride, n, 0, 0, shm.n_pes())
+    for k in range(slots):
+        h, sample = _configs.digest(shm.get(dst + k * stride, n, dtype))
+        results[f"{c['id']}_{k}_sha"] = np.frombuffer(bytes.fromhex(h), dtype=np.uint8)
+        results[f"{c['id']}_{k}_sample"] = sample
+    shm.free_device(dst)
+    shm.free_device(src)
+
+
 def main():
     spec = json.load(open(sys.argv[1]))
     outdir = sys.argv[2]
     shm = shmem_reduce.Shmem()
     shm.init()
     me = shm.my_pe()
-    maxb = max(max(c["n"] + 16, c.get("cap", 0)) * 16 for c in spec["cases"])
+    maxb = max(max(c["n"] + 16, c.get("cap", 0)) * 16 if c.get("kind") != "config" else 4096
+               for c in spec["cases"])
     da, db = shm.malloc_device(maxb), shm.malloc_device(maxb)
     ha, hb = shm.malloc(maxb), shm.malloc(maxb)
     results = {}
     for c in spec["cases"]:
+        if c.get("kind") == "config":
+            run_config(shm, c, me, results)
+            continue
         if c.get("kind") == "stream":
             run_stream(shm, c, me, da, db, results)
             continue
