@@ -39,7 +39,7 @@ def run_pes(npes, cases, tmp_path, extra_env=None, timeout=600):
         # PEs sharing the one test GPU: keep the job's hardware queues at 16
         # (8 processes x the default 4 oversubscribe the GPU's queue slots and
         # every call then waits ~34 ms for a time slice)
-        env.setdefault("GPU_MAX_HW_QUEUES", str(max(1, 16 // npes)))
+        env["GPU_MAX_HW_QUEUES"] = str(max(1, 16 // npes))
     env.update(extra_env or {})
     procs = []
     for pe in range(npes):
