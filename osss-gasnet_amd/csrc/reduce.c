@@ -111,7 +111,102 @@ void mi355_shard_bounds (size_t n, size_t es, int size, int i, size_t *lo, size_
 /* device-resident schedules on symmetric heap offsets                     */
 /* ---------------------------------------------------------------------- */
 
-/* P2P shard schedule, dst and src disjoint or identical. */
+/* Member list of the active set for the device-flag kernels (fused.hip), on
+ * one signal-region channel. */
+static void member_args (MI355FusedArgs *a, const struct aset *s, int chan)
+{
+    memset (a, 0, sizeof *a);
+    a->nmembers = s->size;
+    a->me = s->me;
+    for (int i = 0; i < s->size; ++i) {
+        a->pe[i] = aset_pe (s, i);
+        a->sig[i] = shmemi.peer_sig[a->pe[i]] + (size_t) chan * MI355_SIG_CHANNEL_WORDS;
+    }
+    a->err_flag = shmemi.stream_err;
+    a->timeout_ticks = (unsigned long long) (shmemi.barrier_timeout * 1e8);
+}
+
+/* The device-flag kernels can carry this active set's synchronization. */
+static int device_flags_ok (const struct aset *s)
+{
+    return s->size <= MI355_FUSED_MAX_MEMBERS && shmemi.npes <= MI355_SIG_RSDONE && shmemi.sigmem != NULL &&
+           !shmemi.sig_broken;
+}
+
+static void device_barrier (const MI355FusedArgs *a, hipStream_t st)
+{
+    const int rc = mi355_device_barrier (a, st);
+    if (rc != 0)
+        shmemi_fatal ("device barrier launch failed: %d", rc);
+}
+
+/* P2P shard schedule, dst and src disjoint or identical, with the three
+ * barriers as one-block device-barrier kernels on the library stream: five
+ * launches queued back to back, one host wait (the last barrier carries the
+ * completion flag). The first barrier also orders the sources: each PE's
+ * arrival is stream-ordered after its caller's work. */
+static void p2p_range_dev (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
+                           const struct aset *s)
+{
+    MI355FusedArgs a;
+    member_args (&a, s, SHMEMI_CHAN_HOST);
+    const void *sp[MI355_FUSED_MAX_MEMBERS];
+    void *dsts[MI355_FUSED_MAX_MEMBERS];
+    size_t nb[MI355_FUSED_MAX_MEMBERS];
+    size_t lo, hi;
+    mi355_shard_bounds (n, es, s->size, s->me, &lo, &hi);
+
+    device_barrier (&a, shmemi.stream); /* every source is ready */
+    if (hi > lo) {
+        for (int i = 0; i < s->size; ++i)
+            sp[i] = shmemi_peer_ptr (a.pe[i], src_off + lo * es);
+        shmemi_timed_begin ();
+        const int rc = mi355_combine (op, dtype, shmemi_peer_ptr (shmemi.mype, dst_off + lo * es), sp, s->size,
+                                      hi - lo, shmemi.stream);
+        shmemi_timed_end ();
+        if (rc != 0)
+            shmemi_fatal ("combine kernel launch failed (op %d, dtype %d, %d sources, %zu elements): %d", op,
+                          dtype, s->size, hi - lo, rc);
+    }
+    device_barrier (&a, shmemi.stream); /* every shard is reduced */
+    int k = 0;
+    for (int i = 0; i < s->size; ++i) {
+        size_t l, h;
+        mi355_shard_bounds (n, es, s->size, i, &l, &h);
+        if (i == s->me || h <= l)
+            continue;
+        dsts[k] = shmemi_peer_ptr (shmemi.mype, dst_off + l * es);
+        sp[k] = shmemi_peer_ptr (a.pe[i], dst_off + l * es);
+        nb[k] = (h - l) * es;
+        ++k;
+    }
+    if (k > 0) {
+        const int rc = mi355_copy_segments (dsts, sp, nb, k, shmemi.stream);
+        if (rc != 0)
+            shmemi_fatal ("copy kernel launch failed: %d", rc);
+    }
+    a.host_flag = shmemi.sig_flag; /* peers are done reading us: the call is over */
+    a.epoch = shmemi_next_epoch ();
+    device_barrier (&a, shmemi.stream);
+    if (shmemi_wait_flag (a.epoch) != a.epoch)
+        shmemi_fatal ("device barrier timed out waiting for the other PEs of the active set");
+}
+
+/* Before a host barrier lets peers read this PE's caller-written buffers,
+ * the host must know the caller's queued work is done (one signal kernel,
+ * shmemi_order_after_caller). Set per call by reduce_impl; the device-flag
+ * schedules never need it. */
+static int caller_order_pending;
+
+static void host_order (void)
+{
+    if (caller_order_pending) {
+        shmemi_order_after_caller (1);
+        caller_order_pending = 0;
+    }
+}
+
+/* P2P shard schedule (host barriers), dst and src disjoint or identical. */
 static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
                        const struct aset *s)
 {
@@ -123,6 +218,7 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
     size_t lo, hi;
     mi355_shard_bounds (n, es, s->size, s->me, &lo, &hi);
 
+    host_order ();
     shmemi_barrier_set (s->start, s->stride, s->size); /* every source is ready */
     if (hi > lo) {
         for (int i = 0; i < s->size; ++i)
@@ -150,6 +246,14 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
     free (nb);
     free (dsts);
     free (sp);
+}
+
+static void p2p_any (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n, const struct aset *s)
+{
+    if (device_flags_ok (s))
+        p2p_range_dev (op, dtype, es, dst_off, src_off, n, s);
+    else
+        p2p_range (op, dtype, es, dst_off, src_off, n, s);
 }
 
 /* The fused one-launch schedule (fused.hip) applies: small enough, few
@@ -244,9 +348,10 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
         if (fused_eligible (es, dst_off, src_off, n, s))
             fused_range (op, dtype, es, dst_off, src_off, n, s);
         else
-            p2p_range (op, dtype, es, dst_off, src_off, n, s);
+            p2p_any (op, dtype, es, dst_off, src_off, n, s);
         return;
     } else if (exact && !overlap) {
+        host_order ();
         shmemi_barrier_set (s->start, s->stride, s->size);
         exact_into (op, dtype, dst_off, src_off, n, s);
         shmemi_barrier_set (s->start, s->stride, s->size);
@@ -266,8 +371,9 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
         if (s->size == 1) {
             copy_local (tmp_off, src_off + b * es, cn * es, 0);
         } else if (!exact) {
-            p2p_range (op, dtype, es, tmp_off, src_off + b * es, cn, s);
+            p2p_any (op, dtype, es, tmp_off, src_off + b * es, cn, s);
         } else {
+            host_order ();
             shmemi_barrier_set (s->start, s->stride, s->size);
             exact_into (op, dtype, tmp_off, src_off + b * es, cn, s);
             shmemi_barrier_set (s->start, s->stride, s->size);
@@ -399,11 +505,13 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
         shmemi_fatal ("%s: NULL target or source", fn);
     const size_t nbytes = n * es;
     const int kt = ptr_kind (target, nbytes), ks = ptr_kind (source, nbytes);
-    /* the fused kernel learns on the device that peers' sources are ready */
-    const int fused = kt == PK_DEV_SYM && ks == PK_DEV_SYM &&
-                      fused_eligible (es, shmemi_heap_offset (target), shmemi_heap_offset (source), n, &s);
+    /* Device buffers: the library stream is ordered after the caller's
+     * null-stream work. The device-flag schedules (fused kernel, device
+     * barriers) then learn on the GPU that peers' sources are ready; a
+     * schedule with host barriers first waits for that point on the host. */
     if (kt != PK_HOST || ks != PK_HOST)
-        shmemi_order_after_caller (s.size > 1 && !fused);
+        shmemi_order_after_caller (0); /* SHMEM_ENTRY_SYNC */
+    caller_order_pending = s.size > 1 && kt == PK_DEV_SYM && ks == PK_DEV_SYM;
 
     const int overlap = target != source && ranges_overlap ((size_t) target, (size_t) source, nbytes);
     const int use_rccl = shmemi.algorithm == SHMEMX_REDUCE_RCCL && s.size == shmemi.npes && s.size > 1 &&
@@ -451,19 +559,6 @@ static void stream_begin (const char *fn)
     shmemi_check_stream_err (fn);
 }
 
-static void stream_members (MI355FusedArgs *a, const struct aset *s)
-{
-    memset (a, 0, sizeof *a);
-    a->nmembers = s->size;
-    a->me = s->me;
-    for (int i = 0; i < s->size; ++i) {
-        a->pe[i] = aset_pe (s, i);
-        a->sig[i] = shmemi.peer_sig[a->pe[i]] + SHMEMI_CHAN_STREAM * MI355_SIG_CHANNEL_WORDS;
-    }
-    a->err_flag = shmemi.stream_err;
-    a->timeout_ticks = (unsigned long long) (shmemi.barrier_timeout * 1e8);
-}
-
 static void stream_aset (const char *fn, struct aset *s, int PE_start, int logPE_stride, int PE_size)
 {
     if (logPE_stride < 0 || logPE_stride > 30 || PE_size < 1 || PE_start < 0 ||
@@ -492,7 +587,7 @@ static void stream_barrier (const char *fn, const struct aset *s, hipStream_t st
     if (s->size < 2)
         return;
     MI355FusedArgs a;
-    stream_members (&a, s);
+    member_args (&a, s, SHMEMI_CHAN_STREAM);
     const int rc = mi355_device_barrier (&a, st);
     if (rc != 0)
         shmemi_fatal ("%s: device barrier launch failed: %d", fn, rc);
@@ -538,7 +633,7 @@ static void reduce_on_stream (int op, int dtype, const char *fn, void *target, c
     } else {
         const size_t dst_off = shmemi_heap_offset (target), src_off = shmemi_heap_offset (source);
         MI355FusedArgs a;
-        stream_members (&a, &s);
+        member_args (&a, &s, SHMEMI_CHAN_STREAM);
         if (n * es <= shmemi.fused_max && ((dst_off | src_off) & 15) == 0 && es <= 256) {
             a.op = op;
             a.dtype = dtype;
