@@ -67,6 +67,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--no-small", action="store_true",
+                    help="skip the 64 KiB small-call leg (profiling runs: keeps the dominant kernel's rocprof "
+                         "average to the 256 MiB calls)")
     ap.add_argument("--host", action="store_true",
                     help="source/target in host memory (shmem_malloc, page-locked): the rate includes the "
                          "H2D/D2H staging copies (DESIGN.md); not the headline metric")
@@ -134,14 +137,16 @@ def main():
     shm.kernel_timing(False)
 
     # the many-small-bucket regime (BASELINE config 5 shape: 64 KiB per call)
-    small_n, small_calls = 8192, 1000
-    for _ in range(20):
-        shm.to_all("sum", "double", dst, src, small_n, 0, 0, npes)
-    shm.barrier_all()
-    ts0 = time.perf_counter()
-    for _ in range(small_calls):
-        shm.to_all("sum", "double", dst, src, small_n, 0, 0, npes)
-    t_small = (time.perf_counter() - ts0) / small_calls
+    small_n, small_calls = 8192, 0 if args.no_small else 1000
+    t_small = None
+    if small_calls:
+        for _ in range(20):
+            shm.to_all("sum", "double", dst, src, small_n, 0, 0, npes)
+        shm.barrier_all()
+        ts0 = time.perf_counter()
+        for _ in range(small_calls):
+            shm.to_all("sum", "double", dst, src, small_n, 0, 0, npes)
+        t_small = (time.perf_counter() - ts0) / small_calls
 
     # max over PEs, through the library's own host-staged double max reduction
     tbuf = np.array([t_local], dtype=np.float64)
@@ -214,8 +219,9 @@ def main():
             "per_pe_gib_s": round(S / t_step / GIB, 2),
             "roofline": roofline,
             "cpu_baseline": cpu,
-            "small_call": {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small * 1e6, 2),
-                           "calls": small_calls, "note": "64 KiB shmem_double_sum_to_all back-to-back (PE 0 clock)"},
+            "small_call": None if t_small is None else
+            {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small * 1e6, 2), "calls": small_calls,
+             "note": "64 KiB shmem_double_sum_to_all back-to-back (PE 0 clock)"},
             "check": check,
         }
         print(json.dumps(out), flush=True)
