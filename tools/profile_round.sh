@@ -26,5 +26,5 @@ cp "$(find "$OUT/trace" -name '*kernel_stats.csv' -print -quit)" "$DST/rocprof_k
 cp "$(find "$OUT/trace" -name '*kernel_trace.csv' -print -quit)" "$DST/rocprof_kernel_trace_bench_n1.csv"
 cp "$(find "$OUT/fetch" -name '*counter_collection.csv' -print -quit)" "$DST/pmc/fetch_size_counter_collection.csv"
 cp "$(find "$OUT/write" -name '*counter_collection.csv' -print -quit)" "$DST/pmc/write_size_counter_collection.csv"
-tail -n 1 "$OUT/bench_trace.log" > "$DST/bench_n1_under_rocprof.json"
+grep "^{\"metric\"" "$OUT/bench_trace.log" > "$DST/bench_n1_under_rocprof.json"
 head -n 3 "$DST/rocprof_kernel_stats_bench_n1.csv"
