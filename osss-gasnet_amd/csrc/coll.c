@@ -29,9 +29,10 @@
  * memory, and every collective, PULLS with the streaming copy kernel: every
  * PE reads the members' sources over xGMI into its own target, between two
  * barriers -- the same producer/consumer pattern as the reduction's
- * all-gather leg. Host-memory local sides use hipMemcpy. The collectives: every PE reads the members' sources over xGMI into its
- * own target, between two barriers -- the same producer/consumer pattern as
- * the reduction's all-gather leg.
+ * all-gather leg. Host-memory local sides use hipMemcpy. Broadcast and
+ * fcollect queue barrier, copies and barrier on the library stream (device
+ * barriers, one host wait); collect exchanges its counts through the host
+ * bootstrap segment and keeps host barriers.
  */
 #define _GNU_SOURCE
 #include <complex.h>
@@ -202,10 +203,11 @@ static int is_device_ptr (const void *p)
     return e == hipSuccess && (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged);
 }
 
-/* Pull nseg byte ranges from peers into local memory: one copy kernel (with
- * the completion signal) when the destination is device memory, DMA copies
- * otherwise. */
-static void pull (void **dsts, const void **srcs, size_t *nbytes, int nseg)
+/* Pull nseg byte ranges from peers into local memory: one copy kernel when
+ * the destination is device memory, DMA copies otherwise. wait: block until
+ * done (the copy kernel's completion signal, or a stream synchronize);
+ * otherwise only queue them on the library stream. */
+static void pull_impl (void **dsts, const void **srcs, size_t *nbytes, int nseg, int wait)
 {
     int dev = 1;
     for (int i = 0; i < nseg; ++i)
@@ -214,28 +216,54 @@ static void pull (void **dsts, const void **srcs, size_t *nbytes, int nseg)
         for (int base = 0; base < nseg; base += 64) {
             const int k = nseg - base < 64 ? nseg - base : 64;
             const int last = base + k == nseg;
-            if (last)
+            if (last && wait)
                 shmemi_arm_signal ();
             int rc = mi355_copy_segments (dsts + base, srcs + base, nbytes + base, k, shmemi.stream);
             if (rc != 0)
                 shmemi_fatal ("copy kernel launch failed: %d", rc);
         }
-        shmemi_wait_signal ();
+        if (wait)
+            shmemi_wait_signal ();
     } else {
         for (int i = 0; i < nseg; ++i)
             if (nbytes[i] != 0)
                 SHMEMI_HIP (hipMemcpyAsync (dsts[i], srcs[i], nbytes[i], hipMemcpyDefault, shmemi.stream));
-        SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+        if (wait)
+            SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
     }
 }
 
-static void collective_entry (const char *fn, const void *source, size_t nbytes, const struct cset *s)
+static void pull (void **dsts, const void **srcs, size_t *nbytes, int nseg)
+{
+    pull_impl (dsts, srcs, nbytes, nseg, 1);
+}
+
+/* Opening barrier: every source is ready. With device barriers the rest of
+ * the collective is queued behind it (dev = 1); else a host barrier after the
+ * host has seen the caller's work done. */
+static int collective_entry (const char *fn, const void *source, size_t nbytes, const struct cset *s,
+                             int allow_dev)
 {
     if (nbytes != 0 && !shmemi_in_device_heap (source, nbytes))
         shmemi_fatal ("%s: source %p is not in the device symmetric heap (allocate it with "
                       "shmemx_malloc_device)", fn, source);
+    if (allow_dev && shmemi_dev_barrier_ok (s->start, s->stride, s->size)) {
+        shmemi_order_after_caller (0); /* SHMEM_ENTRY_SYNC */
+        shmemi_dev_barrier (s->start, s->stride, s->size, s->me, 0);
+        return 1;
+    }
     shmemi_order_after_caller (1);
-    shmemi_barrier_set (s->start, s->stride, s->size); /* every source is ready */
+    shmemi_barrier_set (s->start, s->stride, s->size);
+    return 0;
+}
+
+/* Closing barrier: nobody reads this PE's source any more. */
+static void collective_exit (const struct cset *s, int dev)
+{
+    if (dev)
+        shmemi_dev_barrier (s->start, s->stride, s->size, s->me, 1);
+    else
+        shmemi_barrier_set (s->start, s->stride, s->size);
 }
 
 static void broadcast_bytes (const char *fn, void *target, const void *source, size_t nbytes, int PE_root,
@@ -245,13 +273,13 @@ static void broadcast_bytes (const char *fn, void *target, const void *source, s
     if (PE_root < 0 || PE_root >= PE_size)
         shmemi_fatal ("%s: PE_root %d outside the active set of %d PEs", fn, PE_root, PE_size);
     const int root = PE_start + PE_root * s.stride;
-    collective_entry (fn, source, nbytes, &s);
+    const int dev = collective_entry (fn, source, nbytes, &s, 1);
     if (shmemi.mype != root && nbytes != 0) {
         void *d = target;
         const void *src = shmemi_peer_ptr (root, shmemi_heap_offset (source));
-        pull (&d, &src, &nbytes, 1);
+        pull_impl (&d, &src, &nbytes, 1, !dev);
     }
-    shmemi_barrier_set (s.start, s.stride, s.size); /* nobody reads the root's source any more */
+    collective_exit (&s, dev); /* nobody reads the root's source any more */
 }
 
 void pshmem_broadcast32 (void *target, const void *source, size_t nelems, int PE_root, int PE_start,
@@ -269,7 +297,7 @@ void pshmem_broadcast64 (void *target, const void *source, size_t nelems, int PE
 }
 
 /* counts[i] bytes from member i land at the running offset in target */
-static void gather_bytes (void *target, const void *source, const size_t *counts, const struct cset *s)
+static void gather_bytes (void *target, const void *source, const size_t *counts, const struct cset *s, int wait)
 {
     void **dsts = (void **) malloc (sizeof (void *) * (size_t) s->size);
     const void **srcs = (const void **) malloc (sizeof (void *) * (size_t) s->size);
@@ -289,7 +317,7 @@ static void gather_bytes (void *target, const void *source, const size_t *counts
         off += counts[i];
     }
     if (k > 0)
-        pull (dsts, srcs, nb, k);
+        pull_impl (dsts, srcs, nb, k, wait);
     free (nb);
     free (srcs);
     free (dsts);
@@ -299,15 +327,15 @@ static void fcollect_bytes (const char *fn, void *target, const void *source, si
                             int logPE_stride, int PE_size)
 {
     struct cset s = make_set (fn, PE_start, logPE_stride, PE_size);
-    collective_entry (fn, source, nbytes, &s);
+    const int dev = collective_entry (fn, source, nbytes, &s, 1);
     size_t *counts = (size_t *) malloc (sizeof (size_t) * (size_t) s.size);
     if (counts == NULL)
         shmemi_fatal ("out of host memory");
     for (int i = 0; i < s.size; ++i)
         counts[i] = nbytes;
-    gather_bytes (target, source, counts, &s);
+    gather_bytes (target, source, counts, &s, !dev);
     free (counts);
-    shmemi_barrier_set (s.start, s.stride, s.size); /* nobody reads our source any more */
+    collective_exit (&s, dev); /* nobody reads our source any more */
 }
 
 void pshmem_fcollect32 (void *target, const void *source, size_t nelems, int PE_start, int logPE_stride,
@@ -331,13 +359,13 @@ static void collect_bytes (const char *fn, void *target, const void *source, siz
 {
     struct cset s = make_set (fn, PE_start, logPE_stride, PE_size);
     shmemi_publish_count (nbytes);
-    collective_entry (fn, source, nbytes, &s);
+    (void) collective_entry (fn, source, nbytes, &s, 0);
     size_t *counts = (size_t *) malloc (sizeof (size_t) * (size_t) s.size);
     if (counts == NULL)
         shmemi_fatal ("out of host memory");
     for (int i = 0; i < s.size; ++i)
         counts[i] = shmemi_peer_count (s.start + i * s.stride);
-    gather_bytes (target, source, counts, &s);
+    gather_bytes (target, source, counts, &s, 1);
     free (counts);
     shmemi_barrier_set (s.start, s.stride, s.size);
 }

@@ -140,6 +140,28 @@ static void device_barrier (const MI355FusedArgs *a, hipStream_t st)
         shmemi_fatal ("device barrier launch failed: %d", rc);
 }
 
+/* For coll.c: a device barrier over an active set on the library stream
+ * (host channel); `last` makes it carry the completion flag and waits. */
+int shmemi_dev_barrier_ok (int PE_start, int stride, int PE_size)
+{
+    struct aset s = {PE_start, stride, PE_size, 0};
+    return device_flags_ok (&s);
+}
+
+void shmemi_dev_barrier (int PE_start, int stride, int PE_size, int me, int last)
+{
+    struct aset s = {PE_start, stride, PE_size, me};
+    MI355FusedArgs a;
+    member_args (&a, &s, SHMEMI_CHAN_HOST);
+    if (last) {
+        a.host_flag = shmemi.sig_flag;
+        a.epoch = shmemi_next_epoch ();
+    }
+    device_barrier (&a, shmemi.stream);
+    if (last && shmemi_wait_flag (a.epoch) != a.epoch)
+        shmemi_fatal ("device barrier timed out waiting for the other PEs of the active set");
+}
+
 /* P2P shard schedule, dst and src disjoint or identical, with the three
  * barriers as one-block device-barrier kernels on the library stream: five
  * launches queued back to back, one host wait (the last barrier carries the

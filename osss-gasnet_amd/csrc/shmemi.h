@@ -127,6 +127,10 @@ size_t shmemi_heap_offset (const void *p);
 void *shmemi_peer_ptr (int pe, size_t off);
 void shmemi_order_after_caller (int host_wait);
 void shmemi_check_stream_err (const char *fn);
+
+/* reduce.c: device-flag barrier on the library stream (host channel) */
+int shmemi_dev_barrier_ok (int PE_start, int stride, int PE_size);
+void shmemi_dev_barrier (int PE_start, int stride, int PE_size, int me, int last);
 void shmemi_arm_signal (void);
 void shmemi_wait_signal (void);
 unsigned shmemi_next_epoch (void);

@@ -14,9 +14,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "osss-gasnet_amd"))
 import shmem_reduce  # noqa: E402
 
-mib = int(sys.argv[1]) if len(sys.argv) > 1 else 64
+mib = float(sys.argv[1]) if len(sys.argv) > 1 else 64.0
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 20
-S = mib << 20
+S = int(mib * (1 << 20)) // 256 * 256
 shm = shmem_reduce.Shmem()
 npes_env = int(os.environ.get("SHMEM_NPES", os.environ.get("WORLD_SIZE", "1")))
 os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str((npes_env + 2) * S + (64 << 20)))
