@@ -1,5 +1,6 @@
-"""A C program written against the reference's API builds and links against
-libshmem_reduce.so (CPU), and runs on 1 and 3 PEs (GPU)."""
+"""C programs build and link against libshmem_reduce.so (CPU) and run on 1
+and 3 PEs (GPU): one written against the reference's API, and one using the
+stream-ordered extension with HIP streams and graphs."""
 import os
 import subprocess
 import sys
@@ -18,6 +19,22 @@ def build(tmp_path):
     return exe
 
 
+def build_stream(tmp_path):
+    exe = str(tmp_path / "stream_example")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-D__HIP_PLATFORM_AMD__", "-I",
+                    os.path.join(ROOT, "include"), "-I", "/opt/rocm/include",
+                    os.path.join(ROOT, "examples", "stream_example.c"), "-L", LIBDIR, "-lshmem_reduce",
+                    "-L", "/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{LIBDIR}", "-Wl,-rpath,/opt/rocm/lib",
+                    "-o", exe], check=True)
+    return exe
+
+
+def test_c_stream_program_compiles_and_links(tmp_path):
+    exe = build_stream(tmp_path)
+    out = subprocess.check_output(["nm", "-u", exe], text=True)
+    assert "shmemx_long_sum_to_all_on_stream" in out
+
+
 def test_c_program_compiles_and_links(tmp_path):
     exe = build(tmp_path)
     out = subprocess.check_output(["nm", "-u", exe], text=True)
@@ -29,6 +46,18 @@ def test_c_program_compiles_and_links(tmp_path):
 @pytest.mark.parametrize("npes", [1, 3])
 def test_c_program_runs(tmp_path, npes):
     exe = build(tmp_path)
+    env = dict(os.environ, SHMEM_DEVICE_HEAP_SIZE="16M", SHMEM_DEVICE_SCRATCH_SIZE="3M")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "oshrun"), "-np", str(npes), "--same-device",
+                        exe], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count(": ok") == npes, r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.multipe
+@pytest.mark.parametrize("npes", [1, 3])
+def test_c_stream_program_runs(tmp_path, npes):
+    exe = build_stream(tmp_path)
     env = dict(os.environ, SHMEM_DEVICE_HEAP_SIZE="16M", SHMEM_DEVICE_SCRATCH_SIZE="3M")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "oshrun"), "-np", str(npes), "--same-device",
                         exe], env=env, capture_output=True, text=True, timeout=300)
