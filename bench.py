@@ -198,6 +198,19 @@ def main():
         except (ValueError, KeyError):
             pass
 
+    # N > 1: bus bandwidth of the reduce-scatter + all-gather exchange against
+    # the full-mesh xGMI bound: each PE moves 2(N-1)/N * S
+    # over its N-1 links, t >= 2 S / (N * 153 GB/s)
+    xgmi = None
+    if npes > 1:
+        busbw = 2.0 * (npes - 1) / npes * S / t_step / 1e9
+        bound = (npes - 1) * XGMI_LINK_GBS
+        rs_remote = (npes - 1) / npes * S / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else None
+        xgmi = {"busbw_GB_s_per_pe": round(busbw, 1), "mesh_bound_GB_s_per_pe": bound,
+                "frac": round(busbw / bound, 4),
+                "rs_kernel_remote_read_GB_s": None if rs_remote is None else round(rs_remote, 1),
+                "note": "busbw = 2(N-1)/N * S / t_step; bound = (N-1) links x 153 GB/s"}
+
     if me == 0:
         out = {
             "metric": ("GiB/s reduced (host-staged incl. H2D/D2H), shmem_double_sum_to_all @256MiB" if args.host else
@@ -218,6 +231,7 @@ def main():
                        "algorithm": args.algorithm, "parallelism": f"pe{npes}"},
             "per_pe_gib_s": round(S / t_step / GIB, 2),
             "roofline": roofline,
+            "xgmi": xgmi,
             "cpu_baseline": cpu,
             "small_call": None if t_small is None else
             {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small * 1e6, 2), "calls": small_calls,
