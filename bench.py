@@ -107,17 +107,20 @@ def main():
         dst = shm.malloc_device(S)
         shm.put(src, synth(me, np.arange(n, dtype=np.uint64)))
 
-    def step():
-        shm.to_all("sum", "double", dst, src, n, 0, 0, npes)
+    # The K calls run in a C loop (osss-gasnet_amd/csrc/bench_loop.c): each is
+    # shmem_double_sum_to_all called as a C program calls it, so the step time
+    # is the library's entry-to-return time without ctypes marshalling.
+    loop = shmem_reduce.bench_loop()
 
-    for _ in range(args.warmup):
-        step()
+    def steps(k, nred=n):
+        loop(dst, src, nred, 0, 0, npes, None, shm._psync_ptr, k)
+
+    steps(args.warmup)
     # timed region: K steps, barrier + device synchronize on both sides
     shm.barrier_all()
     shm.sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    steps(args.steps)
     shm.sync()
     t_local = time.perf_counter() - t0
     shm.barrier_all()
@@ -128,8 +131,7 @@ def main():
     # host-side latency per call (tools/overhead.py), not kernel time.
     shm.kernel_timing(True)
     t1 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    steps(args.steps)
     shm.sync()
     t_local_ev = time.perf_counter() - t1
     shm.barrier_all()
@@ -140,12 +142,10 @@ def main():
     small_n, small_calls = 8192, 0 if args.no_small else 1000
     t_small = None
     if small_calls:
-        for _ in range(20):
-            shm.to_all("sum", "double", dst, src, small_n, 0, 0, npes)
+        steps(20, small_n)
         shm.barrier_all()
         ts0 = time.perf_counter()
-        for _ in range(small_calls):
-            shm.to_all("sum", "double", dst, src, small_n, 0, 0, npes)
+        steps(small_calls, small_n)
         t_small = (time.perf_counter() - ts0) / small_calls
 
     # max over PEs, through the library's own host-staged double max reduction

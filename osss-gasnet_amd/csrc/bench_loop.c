@@ -1,0 +1,23 @@
+/* bench_loop.c -- the timed loop of bench.py, in C.
+ *
+ * Not part of libshmem_reduce.so: a separate libshmem_bench.so that calls the
+ * public entry point exactly as an OpenSHMEM C program does (the reference's
+ * callers are C programs), so the per-call time bench.py reports is the
+ * library's entry-to-return time with no Python/ctypes marshalling in it
+ * (~2 us per call through ctypes, profiles/r01/overhead*.txt).
+ *
+ * The caller (bench.py) still brackets the loop with shmem_barrier_all and a
+ * device synchronize on both sides and takes its own wall clock around it.
+ */
+#include <stddef.h>
+
+#include <shmem.h>
+
+/* K back-to-back shmem_double_sum_to_all calls with identical arguments;
+ * pWrk/pSync as a conforming caller passes them. */
+void shmemb_double_sum_loop (double *target, double *source, int nreduce, int PE_start, int logPE_stride,
+                             int PE_size, double *pWrk, long *pSync, int iters)
+{
+    for (int i = 0; i < iters; ++i)
+        shmem_double_sum_to_all (target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync);
+}

@@ -200,6 +200,20 @@ class Shmem:
         return n.value, tot.value, avg.value
 
 
+BENCH_LIB_PATH = os.path.join(HERE, "lib", "libshmem_bench.so")
+
+
+def bench_loop(path=BENCH_LIB_PATH):
+    """bench.py's timed loop in C (csrc/bench_loop.c): K back-to-back
+    shmem_double_sum_to_all calls. Load after the main library."""
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    f = ctypes.CDLL(path).shmemb_double_sum_loop
+    f.argtypes = [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i]
+    f.restype = None
+    return f
+
+
 def shard_bounds(lib, n, elem_size, nshards, i):
     lo, hi = _sz(), _sz()
     lib.mi355_shard_bounds(n, elem_size, nshards, i, ctypes.byref(lo), ctypes.byref(hi))

@@ -173,6 +173,23 @@ def run_config(shm, c, me, results):
     shm.free_device(src)
 
 
+FORTRAN_KIND = {"short": "int2", "int": "int4", "long": "int8", "float": "real4", "double": "real8",
+                "longdouble": "real16", "complexf": "comp4", "complexd": "comp8"}
+
+
+def fortran_to_all(shm, op, dtype, dst, src, n, start, logstride, size):
+    """The Fortran binding (csrc/fortran.c): every argument by reference and an
+    INTEGER (4-byte) pSync, as a Fortran program passes them."""
+    import ctypes
+    f = getattr(shm.lib, f"shmem_{FORTRAN_KIND[dtype]}_{op}_to_all_")
+    f.restype = None
+    psync = np.full(shmem_reduce.SHMEM_REDUCE_SYNC_SIZE, -1, dtype=np.int32)
+    ints = [ctypes.c_int(v) for v in (n, start, logstride, size)]
+    f(ctypes.c_void_p(dst), ctypes.c_void_p(src), *[ctypes.byref(v) for v in ints], None,
+      ctypes.c_void_p(psync.ctypes.data))
+    assert (psync == -1).all(), "pSync modified"
+
+
 def main():
     spec = json.load(open(sys.argv[1]))
     outdir = sys.argv[2]
@@ -221,7 +238,10 @@ def main():
         if n:
             shm.put(src, x)
         shm.set_algorithm(c.get("algorithm", "auto"))
-        shm.to_all(op, dtype, dst, src, n, *mine)
+        if c.get("api") == "fortran":
+            fortran_to_all(shm, op, dtype, dst, src, n, *mine)
+        else:
+            shm.to_all(op, dtype, dst, src, n, *mine)
         results[str(c["id"])] = shm.get(dst, n, dtype) if n else np.zeros(0, dtype=shmem_reduce.NP[dtype])
     shm.free(hb)
     shm.free(ha)

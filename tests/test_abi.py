@@ -13,7 +13,7 @@ import pytest
 import shmem_reduce
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-HEADERS = ["shmem.h", "pshmem.h", "shmemx.h", "mi355_reduce.h"]
+HEADERS = ["shmem.h", "pshmem.h", "shmemx.h", "mi355_reduce.h", "shmem_fortran.h"]
 
 
 def declared_functions(header):

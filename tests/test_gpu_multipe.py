@@ -141,6 +141,23 @@ def test_eight_pes_one_gpu(tmp_path):
     check(results, cases)
 
 
+FORTRAN_PAIRS = [(op, dt) for op, dt in oracle.PAIRS if dt != "longlong"]
+
+
+def test_fortran_binding_three_pes(tmp_path):
+    """The 37 Fortran-callable reductions (csrc/fortran.c, reference
+    fortran.c:1218-1256) on 3 PEs: by-reference arguments, INTEGER pSync,
+    fused and multi-launch schedules, a strided set; same parity bar as C."""
+    assert len(FORTRAN_PAIRS) == 37
+    cases = make_cases(FORTRAN_PAIRS, 300, [[0, 0, 3]], "dev", "p2p", 0)
+    cases += make_cases(FORTRAN_PAIRS, 70000, [[0, 0, 3]], "inplace", "p2p", 100)
+    cases += make_cases([p for p in SOME if p[1] != "longlong"], 515, [[0, 1, 2]], "host", "exact", 200)
+    for c in cases:
+        c["api"] = "fortran"
+    results = run_pes(3, cases, tmp_path, extra_env={"SHMEM_FUSED_MAX_BYTES": "256K"})
+    check(results, cases)
+
+
 def test_bad_active_set_aborts_every_pe(tmp_path):
     """A PE outside the active set fails loudly and its peers do not hang."""
     cases = [{"id": 0, "op": "sum", "dtype": "double", "n": 10, "sets": [[0, 0, 2]], "mode": "dev",
