@@ -272,10 +272,15 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
 
 static void p2p_any (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n, const struct aset *s)
 {
-    if (device_flags_ok (s))
+    if (device_flags_ok (s)) {
+        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: P2P shards, device barriers (%zu elements, %d members)", n,
+                      s->size);
         p2p_range_dev (op, dtype, es, dst_off, src_off, n, s);
-    else
+    } else {
+        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: P2P shards, host barriers (%zu elements, %d members)", n,
+                      s->size);
         p2p_range (op, dtype, es, dst_off, src_off, n, s);
+    }
 }
 
 /* The fused one-launch schedule (fused.hip) applies: small enough, few
@@ -292,6 +297,7 @@ static int fused_eligible (size_t es, size_t dst_off, size_t src_off, size_t n, 
 static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
                          const struct aset *s)
 {
+    SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: fused one-launch P2P (%zu elements, %d members)", n, s->size);
     MI355FusedArgs a;
     memset (&a, 0, sizeof a);
     a.op = op;
@@ -360,9 +366,12 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
 
     if (s->size == 1) {
         /* a one-PE fold is the identity: target = source (reduce-op.c:226-229) */
-        if (same)
+        if (same) {
+            SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: 1-PE identity in place, nothing to move");
             return;
+        }
         if (!overlap) {
+            SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: 1-PE identity, one copy of %zu bytes", nbytes);
             copy_local (dst_off, src_off, nbytes, 1);
             return;
         }
@@ -373,6 +382,7 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
             p2p_any (op, dtype, es, dst_off, src_off, n, s);
         return;
     } else if (exact && !overlap) {
+        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: EXACT reference order, host barriers");
         host_order ();
         shmemi_barrier_set (s->start, s->stride, s->size);
         exact_into (op, dtype, dst_off, src_off, n, s);
@@ -386,6 +396,8 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
     const size_t per = shmemi.scratch_chunk / es;
     const size_t nchunks = (n + per - 1) / per;
     const int down = dst_off > src_off;
+    SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: overlapping target, %zu chunk(s) through scratch, %s", nchunks,
+                  down ? "top down" : "bottom up");
     for (size_t c = 0; c < nchunks; ++c) {
         const size_t idx = down ? nchunks - 1 - c : c;
         const size_t b = idx * per;
@@ -536,9 +548,20 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
     caller_order_pending = s.size > 1 && kt == PK_DEV_SYM && ks == PK_DEV_SYM;
 
     const int overlap = target != source && ranges_overlap ((size_t) target, (size_t) source, nbytes);
+    if (shmemi_trace_mask & (1u << SHMEMI_LOG_REDUCTION)) {
+        static const char *const kind[] = {"host", "device heap", "device, not symmetric"};
+        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION,
+                      "%s: nreduce %d, PE_start %d, logPE_stride %d, PE_size %d; target %p (%s), source %p (%s)", fn,
+                      nreduce, PE_start, logPE_stride, PE_size, target, kind[kt], source, kind[ks]);
+        /* the reference's overlap trace (reduce-op.c:210-223) */
+        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "target (%p) and source (%p, size %zu) %s", target, source, nbytes,
+                      target == source ? "are the same buffer" : overlap ? "overlap, using temporary target"
+                                                                          : "do not overlap");
+    }
     const int use_rccl = shmemi.algorithm == SHMEMX_REDUCE_RCCL && s.size == shmemi.npes && s.size > 1 &&
                          shmemi_rccl_supported (op, dtype);
     if (use_rccl && kt != PK_HOST && ks != PK_HOST && !overlap) {
+        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: RCCL allreduce");
         if (shmemi_rccl_allreduce (op, dtype, source, target, n) != 0)
             shmemi_fatal ("%s: ncclAllReduce failed", fn);
         return;
@@ -548,6 +571,7 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
         return;
     }
 
+    SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "staged through the scratch buffers (%s)", use_rccl ? "RCCL" : "P2P");
     staged (op, dtype, fn, target, source, n, &s, ks, kt, use_rccl);
 }
 

@@ -593,7 +593,11 @@ void *shmemx_malloc_device (size_t size)
             ret = shmemi.heap + b->off;
             break;
         }
+        if (ret == NULL)
+            SHMEMI_TRACE (SHMEMI_LOG_NOTICE, "shmemx_malloc_device(%zu): device heap exhausted", size);
     }
+    SHMEMI_TRACE (SHMEMI_LOG_MEMORY, "shmemx_malloc_device(%zu) = %p (heap offset %zu)", size, ret,
+                  ret != NULL ? (size_t) ((char *) ret - shmemi.heap) : (size_t) 0);
     shmem_barrier_all ();
     return ret;
 }
@@ -627,6 +631,7 @@ static int device_free (void *ptr)
 void shmemx_free_device (void *ptr)
 {
     shmemi_init_check ("shmemx_free_device");
+    SHMEMI_TRACE (SHMEMI_LOG_MEMORY, "shmemx_free_device(%p)", ptr);
     shmem_barrier_all ();
     if (ptr != NULL && !device_free (ptr))
         shmemi_fatal ("shmemx_free_device(%p): not in the device symmetric heap", ptr);
@@ -665,6 +670,7 @@ void *pshmem_malloc (size_t size)
         h->next = shmemi.host_blocks;
         shmemi.host_blocks = h;
     }
+    SHMEMI_TRACE (SHMEMI_LOG_MEMORY, "shmem_malloc(%zu) = %p (host)", size, p);
     shmem_barrier_all ();
     return p;
 }
@@ -716,6 +722,7 @@ void pshmem_init (void)
     if (shmemi.npes < 1 || shmemi.npes > SHMEMI_MAX_PES || shmemi.mype < 0 || shmemi.mype >= shmemi.npes)
         shmemi_fatal ("invalid PE identity %d of %d (SHMEM_PE/SHMEM_NPES or RANK/WORLD_SIZE)",
                       shmemi.mype, shmemi.npes);
+    shmemi_trace_init ();
     shmemi.barrier_timeout = (double) env_long (to_env, 600);
     shmemi.debug = (int) env_long (dbg_env, 0);
     static const char *es_env[] = {"SHMEM_ENTRY_SYNC", NULL};
@@ -736,6 +743,8 @@ void pshmem_init (void)
             }
         }
         shmemi.initialized = 1;
+        shmemi_trace_show_levels ();
+        shmemi_trace_show_info ();
         return;
     }
 
@@ -770,6 +779,20 @@ void pshmem_init (void)
         }
     }
     shmemi.initialized = 1;
+    shmemi_trace_show_levels ();
+    if (shmemi_trace_mask & (1u << SHMEMI_LOG_INIT)) {
+        char bus[64] = "";
+        (void) hipDeviceGetPCIBusId (bus, (int) sizeof bus, shmemi.device);
+        static const char *const alg[] = {"auto", "p2p", "exact", "rccl"};
+        SHMEMI_TRACE (SHMEMI_LOG_INIT, "%s: PE %d of %d on GPU %d (%s)", SHMEMX_VERSION_STRING, shmemi.mype,
+                      shmemi.npes, shmemi.device, bus);
+        SHMEMI_TRACE (SHMEMI_LOG_INIT, "device heap %zu bytes (user %zu, scratch 3 x %zu), signal region %s",
+                      shmemi.heap_size, shmemi.user_size, shmemi.scratch_chunk,
+                      shmemi.sig_broken ? "off (self-test failed)" : "on");
+        SHMEMI_TRACE (SHMEMI_LOG_INIT, "reduce algorithm %s, fused path up to %zu bytes, peer heap reads %s",
+                      alg[shmemi.algorithm & 3], shmemi.fused_max, shmemi.p2p_broken ? "FAILED (RCCL)" : "ok");
+    }
+    shmemi_trace_show_info ();
     static int registered = 0;
     if (!registered) {
         atexit (finalize_atexit);
@@ -787,6 +810,7 @@ void pshmem_finalize (void)
 {
     if (!shmemi.initialized)
         return;
+    SHMEMI_TRACE (SHMEMI_LOG_FINALIZE, "finalizing (PE %d of %d)", shmemi.mype, shmemi.npes);
     /* stream-ordered collectives still queued on the caller's streams finish
      * first (they only wait on peers' kernels that are already enqueued) */
     if (shmemi.device >= 0 && shmemi.heap != NULL)
@@ -857,6 +881,7 @@ void pshmem_finalize (void)
     free (shmemi.bar_count);
     shmemi.bar_count = NULL;
     shmemi.initialized = 0;
+    shmemi_trace_fini ();
 }
 
 void pshmem_global_exit (int status)
@@ -881,6 +906,7 @@ void pshmem_barrier_all (void)
 {
     shmemi_init_check ("shmem_barrier_all");
     shmemi_check_stream_err ("shmem_barrier_all");
+    SHMEMI_TRACE (SHMEMI_LOG_BARRIER, "shmem_barrier_all");
     if (shmemi.stream != NULL)
         SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
     shmemi_barrier_set (0, 1, shmemi.npes);
@@ -894,6 +920,8 @@ void pshmem_barrier (int PE_start, int logPE_stride, int PE_size, long *pSync)
         PE_start + (long) (PE_size - 1) * (1L << logPE_stride) >= shmemi.npes)
         shmemi_fatal ("shmem_barrier: active set (%d, %d, %d) outside the %d PEs", PE_start,
                       logPE_stride, PE_size, shmemi.npes);
+    SHMEMI_TRACE (SHMEMI_LOG_BARRIER, "shmem_barrier(PE_start %d, logPE_stride %d, PE_size %d)", PE_start,
+                  logPE_stride, PE_size);
     if (shmemi.stream != NULL)
         SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
     shmemi_barrier_set (PE_start, 1 << logPE_stride, PE_size);

@@ -144,4 +144,24 @@ size_t shmemi_peer_count (int pe);
 
 #define SHMEMI_HIP(call) shmemi_hip_check ((call), #call)
 
+/* trace.c: env-gated trace lines (SHMEM_LOG_LEVELS, SHMEM_LOG_FILE);
+ * levels follow the reference's enum (src/utils/trace.h:59-83) */
+enum shmemi_log_level {
+    SHMEMI_LOG_DEBUG = 1, SHMEMI_LOG_INFO, SHMEMI_LOG_VERSION, SHMEMI_LOG_INIT, SHMEMI_LOG_FINALIZE,
+    SHMEMI_LOG_BARRIER, SHMEMI_LOG_BROADCAST, SHMEMI_LOG_REDUCTION, SHMEMI_LOG_COLLECT, SHMEMI_LOG_QUIET,
+    SHMEMI_LOG_MEMORY, SHMEMI_LOG_NOTICE, SHMEMI_LOG_NLEVELS
+};
+#define SHMEMX_VERSION_STRING "osss-gasnet MI355X reduction path (OpenSHMEM 1.3 API, gfx950)"
+extern unsigned shmemi_trace_mask;
+void shmemi_trace_init (void);
+void shmemi_trace_fini (void);
+void shmemi_trace_show_info (void);
+void shmemi_trace_show_levels (void);
+void shmemi_trace_emit (int level, const char *fmt, ...) __attribute__ ((format (printf, 2, 3)));
+#define SHMEMI_TRACE(level, ...)                                                                            \
+    do {                                                                                                    \
+        if (__builtin_expect (shmemi_trace_mask & (1u << (level)), 0))                                      \
+            shmemi_trace_emit ((level), __VA_ARGS__);                                                       \
+    } while (0)
+
 #endif /* SHMEMI_H */
