@@ -30,7 +30,8 @@ sys.path.insert(0, os.path.join(ROOT, "oracle"))
 import shmem_reduce  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
-XGMI_LINK_GBS = 153.0      # per link, 7 links per GPU
+XGMI_LINK_GBS = 153.0      # per link, 7 links per GPU (AMD's per-link figure)
+XGMI_LINK_DIR_GBS = 76.8   # one direction of a link, if 153.6 counts both directions (as MI300X's 128 = 2 x 64)
 GIB = float(1 << 30)
 
 
@@ -206,10 +207,14 @@ def main():
         busbw = 2.0 * (npes - 1) / npes * S / t_step / 1e9
         bound = (npes - 1) * XGMI_LINK_GBS
         rs_remote = (npes - 1) / npes * S / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else None
+        bound_dir = (npes - 1) * XGMI_LINK_DIR_GBS
         xgmi = {"busbw_GB_s_per_pe": round(busbw, 1), "mesh_bound_GB_s_per_pe": bound,
                 "frac": round(busbw / bound, 4),
+                "mesh_bound_one_direction_GB_s_per_pe": round(bound_dir, 1),
+                "frac_one_direction": round(busbw / bound_dir, 4),
                 "rs_kernel_remote_read_GB_s": None if rs_remote is None else round(rs_remote, 1),
-                "note": "busbw = 2(N-1)/N * S / t_step; bound = (N-1) links x 153 GB/s"}
+                "note": "busbw = 2(N-1)/N * S / t_step = bytes each PE receives over xGMI per second; "
+                        "bound = (N-1) links x 153 GB/s (SURVEY 8d), or x 76.8 GB/s if 153.6 is both directions"}
 
     if me == 0:
         out = {

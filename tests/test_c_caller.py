@@ -1,6 +1,7 @@
 """C programs build and link against libshmem_reduce.so (CPU) and run on 1
-and 3 PEs (GPU): one written against the reference's API, and one using the
-stream-ordered extension with HIP streams and graphs."""
+and 3 PEs (GPU): one written against the reference's API, one using the
+stream-ordered extension with HIP streams and graphs, and a C++ caller
+(std::complex through COMPLEXIFY, long double)."""
 import os
 import subprocess
 import sys
@@ -27,6 +28,20 @@ def build_stream(tmp_path):
                     "-L", "/opt/rocm/lib", "-lamdhip64", f"-Wl,-rpath,{LIBDIR}", "-Wl,-rpath,/opt/rocm/lib",
                     "-o", exe], check=True)
     return exe
+
+
+def build_cpp(tmp_path):
+    exe = str(tmp_path / "reduce_example_cpp")
+    subprocess.run(["g++", "-std=c++17", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "examples", "reduce_example.cpp"), "-L", LIBDIR, "-lshmem_reduce",
+                    f"-Wl,-rpath,{LIBDIR}", "-o", exe], check=True)
+    return exe
+
+
+def test_cpp_program_compiles_and_links(tmp_path):
+    exe = build_cpp(tmp_path)
+    out = subprocess.check_output(["nm", "-u", exe], text=True)
+    assert "shmem_complexd_prod_to_all" in out and "shmem_longdouble_sum_to_all" in out
 
 
 def test_c_stream_program_compiles_and_links(tmp_path):
@@ -58,6 +73,18 @@ def test_c_program_runs(tmp_path, npes):
 @pytest.mark.parametrize("npes", [1, 3])
 def test_c_stream_program_runs(tmp_path, npes):
     exe = build_stream(tmp_path)
+    env = dict(os.environ, SHMEM_DEVICE_HEAP_SIZE="16M", SHMEM_DEVICE_SCRATCH_SIZE="3M")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "oshrun"), "-np", str(npes), "--same-device",
+                        exe], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.count(": ok") == npes, r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.multipe
+@pytest.mark.parametrize("npes", [1, 3])
+def test_cpp_program_runs(tmp_path, npes):
+    exe = build_cpp(tmp_path)
     env = dict(os.environ, SHMEM_DEVICE_HEAP_SIZE="16M", SHMEM_DEVICE_SCRATCH_SIZE="3M")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "oshrun"), "-np", str(npes), "--same-device",
                         exe], env=env, capture_output=True, text=True, timeout=300)
