@@ -71,6 +71,9 @@ def main():
     ap.add_argument("--no-small", action="store_true",
                     help="skip the 64 KiB small-call leg (profiling runs: keeps the dominant kernel's rocprof "
                          "average to the 256 MiB calls)")
+    ap.add_argument("--no-rccl-compare", action="store_true",
+                    help="N > 1: skip timing the same K calls through RCCL's ncclAllReduce (SHMEM_REDUCE_ALGORITHM"
+                         "=rccl) beside the default P2P schedule")
     ap.add_argument("--host", action="store_true",
                     help="source/target in host memory (shmem_malloc, page-locked): the rate includes the "
                          "H2D/D2H staging copies (DESIGN.md); not the headline metric")
@@ -149,12 +152,46 @@ def main():
         steps(small_calls, small_n)
         t_small = (time.perf_counter() - ts0) / small_calls
 
+    # N > 1: the same K calls through RCCL (ncclAllReduce on the whole job,
+    # SHMEM_REDUCE_ALGORITHM=rccl) for comparison with the P2P schedule; the
+    # headline value stays the default schedule's
+    t_rccl_local = None
+    distinct_gpus = False
+    if npes > 1:
+        # RCCL refuses two ranks on one device: compare only with one GPU per PE
+        dev = np.array([shm.lib.shmemx_device_id()], dtype=np.int32)
+        lo, hi = np.zeros(1, dtype=np.int32), np.zeros(1, dtype=np.int32)
+        shm.to_all("min", "int", lo.ctypes.data, dev.ctypes.data, 1, 0, 0, npes)
+        shm.to_all("max", "int", hi.ctypes.data, dev.ctypes.data, 1, 0, 0, npes)
+        distinct_gpus = int(lo[0]) != int(hi[0])
+    if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host:
+        shm.set_algorithm("rccl")
+        steps(3)
+        shm.barrier_all()
+        shm.sync()
+        tr0 = time.perf_counter()
+        steps(args.steps)
+        shm.sync()
+        t_rccl_local = time.perf_counter() - tr0
+        shm.barrier_all()
+        shm.set_algorithm(args.algorithm)
+
     # max over PEs, through the library's own host-staged double max reduction
     tbuf = np.array([t_local], dtype=np.float64)
     tout = np.zeros(1, dtype=np.float64)
     shm.to_all("max", "double", tout.ctypes.data, tbuf.ctypes.data, 1, 0, 0, npes)
     t_max = float(tout[0])
     t_step = t_max / args.steps
+    rccl = None
+    if t_rccl_local is not None:
+        tbuf[0] = t_rccl_local
+        shm.to_all("max", "double", tout.ctypes.data, tbuf.ctypes.data, 1, 0, 0, npes)
+        tr_step = float(tout[0]) / args.steps
+        rccl = {"ms_per_step": round(tr_step * 1e3, 4), "value": round(npes * S / tr_step / GIB, 2),
+                "busbw_GB_s_per_pe": round(2.0 * (npes - 1) / npes * S / tr_step / 1e9, 1),
+                "p2p_speedup": round(tr_step / t_step, 3),
+                "note": "same K calls with SHMEM_REDUCE_ALGORITHM=rccl (ncclAllReduce, RCCL's order: "
+                        "FP results within tolerance, not bit-exact); comparison only, not the headline"}
 
     # correctness of the last result on a sample: the P2P schedule's result is
     # the reference's result on PE_start (own-first = ascending order)
@@ -215,6 +252,9 @@ def main():
                 "rs_kernel_remote_read_GB_s": None if rs_remote is None else round(rs_remote, 1),
                 "note": "busbw = 2(N-1)/N * S / t_step = bytes each PE receives over xGMI per second; "
                         "bound = (N-1) links x 153 GB/s (SURVEY 8d), or x 76.8 GB/s if 153.6 is both directions"}
+        if not distinct_gpus:
+            xgmi["note"] = ("the PEs share ONE GPU (test layout): peer 'xGMI' reads are local HBM reads, so "
+                            "these figures are not xGMI rates")
 
     if me == 0:
         out = {
@@ -237,6 +277,7 @@ def main():
             "per_pe_gib_s": round(S / t_step / GIB, 2),
             "roofline": roofline,
             "xgmi": xgmi,
+            "rccl_compare": rccl,
             "cpu_baseline": cpu,
             "small_call": None if t_small is None else
             {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small * 1e6, 2), "calls": small_calls,

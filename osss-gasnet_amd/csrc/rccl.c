@@ -38,13 +38,14 @@ int shmemi_rccl_comm (void **comm)
     if (shmemi.rccl_comm == NULL) {
         ncclUniqueId id;
         _Static_assert (sizeof id <= sizeof shmemi.seg->rccl_id, "ncclUniqueId too large");
-        if (shmemi.mype == 0) {
-            if (ncclGetUniqueId (&id) != ncclSuccess)
-                shmemi_fatal ("ncclGetUniqueId failed");
-            memcpy (shmemi.seg->rccl_id, &id, sizeof id);
+        if (shmemi.mype == 0 && ncclGetUniqueId (&id) != ncclSuccess)
+            shmemi_fatal ("ncclGetUniqueId failed");
+        if (shmemi.seg != NULL) { /* one PE has no bootstrap segment */
+            if (shmemi.mype == 0)
+                memcpy (shmemi.seg->rccl_id, &id, sizeof id);
+            shmemi_barrier_set (0, 1, shmemi.npes);
+            memcpy (&id, shmemi.seg->rccl_id, sizeof id);
         }
-        shmemi_barrier_set (0, 1, shmemi.npes);
-        memcpy (&id, shmemi.seg->rccl_id, sizeof id);
         ncclComm_t c;
         ncclResult_t r = ncclCommInitRank (&c, shmemi.npes, id, shmemi.mype);
         if (r != ncclSuccess)

@@ -124,3 +124,25 @@ def test_psync_is_left_at_sync_value(shm):
     t = np.zeros(100)
     shm.to_all("sum", "double", t.ctypes.data, x.ctypes.data, 100, 0, 0, 1, pSync=psync.ctypes.data)
     assert (psync == -1).all()
+
+
+@pytest.mark.parametrize("op,dtype", [("sum", "double"), ("max", "float"), ("min", "int"), ("prod", "long"),
+                                      ("sum", "complexd"), ("sum", "complexf")])
+def test_rccl_glue_one_rank(shm, op, dtype):
+    """The RCCL schedule's glue (csrc/rccl.c: communicator setup, type/op
+    mapping, complex sum as 2n reals) on a 1-rank communicator, where
+    ncclAllReduce is the identity. Multi-rank RCCL needs one GPU per rank (RCCL
+    refuses two ranks on one device), so this is what the one-GPU box can run."""
+    f = shm.lib.shmemi_rccl_allreduce
+    f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+    f.restype = ctypes.c_int
+    assert shm.lib.shmemi_rccl_supported(shmem_reduce.OPS.index(op), shmem_reduce.DTYPES.index(dtype))
+    n = 4099
+    es = np.dtype(oracle.NP[dtype]).itemsize
+    x = gen_golden.values(np.random.default_rng(9), op, dtype, n)
+    ds, dt = shm.malloc_device(n * es), shm.malloc_device(n * es)
+    shm.put(ds, x)
+    assert f(shmem_reduce.OPS.index(op), shmem_reduce.DTYPES.index(dtype), ds, dt, n) == 0
+    assert same_bits(shm.get(dt, n, dtype), x, dtype)
+    shm.free_device(dt)
+    shm.free_device(ds)
