@@ -215,7 +215,7 @@ def main():
 
     # dominant kernel and its algorithmic bytes per launch
     if npes == 1:
-        kname = "copy_segments<8> (identity fold, PE_size=1)"
+        kname = "copy_segments<4> (identity fold, PE_size=1)"
         alg_bytes = 2 * S
     else:
         kname = f"combine_vec<sum,double,{npes}> (reduce-scatter leg, {npes - 1} sources over xGMI)"

@@ -101,7 +101,7 @@ __device__ __forceinline__ u32x4 ld16(const u32x4 *p) {
     else return *p;
 }
 __device__ __forceinline__ void st16(u32x4 *p, u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(p), "v"(v) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 // Vector path: every pointer 16-byte aligned. Each lane owns UNROLL vectors
@@ -196,19 +196,32 @@ __global__ __launch_bounds__(kBlock) void copy_segments(SegParams p) {
         u32x4 *d = (u32x4 *)dst;
         const uint64_t nvec = nb / 16;
         const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
-        for (uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x; base < nvec;
-             base += step) {
-            u32x4 x[UNROLL];
+        // software-pipelined: the loads of pass k+1 are in flight while the
+        // stores of pass k issue (tools/copy_variants.hip: 78.3 vs 80.0 us for
+        // 256 MiB at UNROLL 4, one block per CU, over all-loads-then-stores)
+        uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
+        u32x4 x[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = base + (uint64_t)u * kBlock;
+            if (i < nvec) x[u] = ld16<POL_PLAIN>(s + i);
+        }
+        while (base < nvec) {
+            const uint64_t next = base + step;
+            u32x4 y[UNROLL];
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) {
-                const uint64_t i = base + (uint64_t)u * kBlock;
-                if (i < nvec) x[u] = ld16<POL_PLAIN>(s + i);
+                const uint64_t i = next + (uint64_t)u * kBlock;
+                if (i < nvec) y[u] = ld16<POL_PLAIN>(s + i);
             }
 #pragma unroll
             for (int u = 0; u < UNROLL; ++u) {
                 const uint64_t i = base + (uint64_t)u * kBlock;
                 if (i < nvec) st16(d + i, x[u]);
             }
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) x[u] = y[u];
+            base = next;
         }
         done = nvec * 16;
     }
@@ -492,12 +505,13 @@ static int copy_segments_impl(void *const *dsts, const void *const *srcs, const 
         fire_on_host((hipStream_t)stream);
         return 0;
     }
-    // 2 blocks per CU: as fast as 8 for 256 MiB (tools/overhead_c.c, 84.3 vs
-    // 84.4 us per call) with a quarter of the completion-counter atomics
-    constexpr int U = 8;
-    unsigned gx = grid_for((uint64_t)kBlock * U, maxv, 2);
+    // pipelined UNROLL 4, one block per CU (tools/copy_variants.hip,
+    // profiles/r01/copy_variants.txt: 78.2-78.5 us for 256 MiB, the best of
+    // grid-stride / per-block partition / 1-4 blocks per CU / UNROLL 4-16)
+    constexpr int U = 4;
+    unsigned gx = grid_for((uint64_t)kBlock * U, maxv, 1);
     // keep total blocks ~ cap when many segments share the chip
-    unsigned cap = (unsigned)device_cus() * 2;
+    unsigned cap = (unsigned)device_cus();
     if ((uint64_t)gx * used > cap) gx = cap / used > 0 ? cap / used : 1;
     return launch(copy_segments<U>, dim3(gx, used), (hipStream_t)stream, p);
 }

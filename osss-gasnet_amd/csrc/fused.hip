@@ -54,7 +54,7 @@ __device__ __forceinline__ unsigned long long ld_sys_u64(const unsigned long lon
 // 16-byte store, write-through to memory at system scope: a peer reads it
 // over xGMI after the flag that follows it
 __device__ __forceinline__ void st16_sys(u32x4 *p, u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 // This call's pair count with every member (lanes of wave 0, into LDS).

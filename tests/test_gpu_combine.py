@@ -160,3 +160,38 @@ def test_full_size_256mib_properties(shm, dev):
     assert shm.combine("sum", "double", out, [pb], n) == 0
     shm.sync()
     assert (shm.get(out, n, "double").view(np.uint64) == b.view(np.uint64)).all()
+
+
+def test_copy_segments_sizes_offsets_and_many_segments(shm, dev):
+    """mi355_copy_segments (the 1-PE identity and the all-gather leg): every
+    byte lands for sizes around the vector/pass boundaries, 16-byte aligned and
+    not, one segment and 7 / 64 segments per launch (the launch shape divides
+    the grid between segments). Regression for a store-data hazard: an
+    inline-asm store whose data VGPRs the next VALU overwrote corrupted the
+    upper lanes of small copies (fixed by the wait states in st16)."""
+    import ctypes
+    rng = np.random.default_rng(17)
+    sizes = [1, 15, 16, 17, 255, 4096, 8000, 16383, 16384, 16400, 65536 + 48, 1 << 20, (1 << 22) + 16]
+    for nb in sizes:
+        for off in (0, 16, 3):
+            x = rng.integers(0, 256, nb + off, dtype=np.uint8)
+            s = dev.upload(x)
+            d = dev.empty(nb + off)
+            dsts = (ctypes.c_void_p * 1)(d + off)
+            srcs = (ctypes.c_void_p * 1)(s + off)
+            nbs = (ctypes.c_size_t * 1)(nb)
+            assert shm.lib.mi355_copy_segments(dsts, srcs, nbs, 1, None) == 0
+            shm.sync()
+            got = shm.get(d + off, nb, np.uint8)
+            assert (got == x[off:]).all(), (nb, off, int(np.argmax(got != x[off:])))
+    for k, seg in ((7, 33333), (64, 4112)):
+        xs = [rng.integers(0, 256, seg, dtype=np.uint8) for _ in range(k)]
+        sp = [dev.upload(x) for x in xs]
+        dp = [dev.empty(seg) for _ in range(k)]
+        dsts = (ctypes.c_void_p * k)(*dp)
+        srcs = (ctypes.c_void_p * k)(*sp)
+        nbs = (ctypes.c_size_t * k)(*([seg] * k))
+        assert shm.lib.mi355_copy_segments(dsts, srcs, nbs, k, None) == 0
+        shm.sync()
+        for i in range(k):
+            assert (shm.get(dp[i], seg, np.uint8) == xs[i]).all(), (k, i)

@@ -26,9 +26,9 @@ __device__ __forceinline__ u32x4 ld(const u32x4 *p) {
 }
 template <int POL>
 __device__ __forceinline__ void st(u32x4 *p, u32x4 v) {
-    if constexpr (POL == 4) asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(p), "v"(v) : "memory");
-    else if constexpr (POL == 5) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" :: "v"(p), "v"(v) : "memory");
-    else if constexpr (POL == 6 || POL == 7) asm volatile("global_store_dwordx4 %0, %1, off nt sc1" :: "v"(p), "v"(v) : "memory");
+    if constexpr (POL == 4) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 5) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 6 || POL == 7) asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" :: "v"(p), "v"(v) : "memory");
     else if constexpr (POL & 2) __builtin_nontemporal_store(v, p);
     else *p = v;
 }
