@@ -140,6 +140,7 @@ def main():
     t_local_ev = time.perf_counter() - t1
     shm.barrier_all()
     nk, k_total_ms, k_avg_ms = shm.kernel_timing_stats()
+    nag, _, ag_avg_ms = shm.kernel_timing_phase_stats(1)   # N > 1: the all-gather copy
     shm.kernel_timing(False)
 
     # the many-small-bucket regime (BASELINE config 5 shape: 64 KiB per call)
@@ -250,6 +251,9 @@ def main():
                 "mesh_bound_one_direction_GB_s_per_pe": round(bound_dir, 1),
                 "frac_one_direction": round(busbw / bound_dir, 4),
                 "rs_kernel_remote_read_GB_s": None if rs_remote is None else round(rs_remote, 1),
+                "ag_kernel_avg_us": round(ag_avg_ms * 1e3, 2) if nag else None,
+                "ag_kernel_remote_read_GB_s": round((npes - 1) / npes * S / (ag_avg_ms * 1e-3) / 1e9, 1)
+                if nag and ag_avg_ms > 0 else None,
                 "note": "busbw = 2(N-1)/N * S / t_step = bytes each PE receives over xGMI per second; "
                         "bound = (N-1) links x 153 GB/s (SURVEY 8d), or x 76.8 GB/s if 153.6 is both directions"}
         if not distinct_gpus:

@@ -60,6 +60,9 @@ void shmemx_kernel_timing (int enable);        /* enable resets the counters */
 /* Number of timed launches, total and per-launch average duration (ms) of the
  * launches timed since the last enable. Synchronizes the stream. */
 void shmemx_kernel_timing_stats (long *launches, double *total_ms, double *avg_ms);
+/* the same for one phase: 0 = each call's dominant kernel (the fold, or a 1-PE call's copy; what
+ * shmemx_kernel_timing_stats reports), 1 = the all-gather copy of the P2P schedule */
+void shmemx_kernel_timing_phase_stats (int phase, long *launches, double *total_ms, double *avg_ms);
 
 /* Stream-ordered collectives. Enqueued on `stream` (a hipStream_t; NULL =
  * the null stream) and return at once: the reduction runs after the work

@@ -62,9 +62,12 @@ static void combine_wait (int op, int dtype, void *dst, const void *const *srcs,
     shmemi_wait_signal ();
 }
 
-/* Byte copies, 64 segments per launch; the last launch carries the signal. */
-static void copy_wait (void *const *dsts, const void *const *srcs, const size_t *nbytes, int nseg, int timed)
+/* Byte copies, 64 segments per launch; the last launch carries the signal
+ * (and, when kernel timing is on, the event pair of timing phase `phase`;
+ * phase < 0: not timed). */
+static void copy_wait (void *const *dsts, const void *const *srcs, const size_t *nbytes, int nseg, int phase)
 {
+    const int timed = phase >= 0;
     if (nseg <= 0)
         return;
     for (int base = 0; base < nseg; base += 64) {
@@ -72,7 +75,7 @@ static void copy_wait (void *const *dsts, const void *const *srcs, const size_t 
         const int last = base + k == nseg;
         if (last) {
             if (timed)
-                shmemi_timed_begin ();
+                shmemi_timed_begin_phase (phase);
             shmemi_arm_signal ();
         }
         int rc = mi355_copy_segments (dsts + base, srcs + base, nbytes + base, k, shmemi.stream);
@@ -203,7 +206,9 @@ static void p2p_range_dev (int op, int dtype, size_t es, size_t dst_off, size_t 
         ++k;
     }
     if (k > 0) {
+        shmemi_timed_begin_phase (1);
         const int rc = mi355_copy_segments (dsts, sp, nb, k, shmemi.stream);
+        shmemi_timed_end ();
         if (rc != 0)
             shmemi_fatal ("copy kernel launch failed: %d", rc);
     }
@@ -263,7 +268,7 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
         nb[k] = (h - l) * es;
         ++k;
     }
-    copy_wait (dsts, sp, nb, k, 0);
+    copy_wait (dsts, sp, nb, k, 1);
     shmemi_barrier_set (s->start, s->stride, s->size); /* peers are done reading us */
     free (nb);
     free (dsts);
@@ -347,7 +352,7 @@ static void copy_local (size_t dst_off, size_t src_off, size_t nbytes, int timed
     void *d = shmemi_peer_ptr (shmemi.mype, dst_off);
     const void *sv = shmemi_peer_ptr (shmemi.mype, src_off);
     size_t nb = nbytes;
-    copy_wait (&d, &sv, &nb, 1, timed);
+    copy_wait (&d, &sv, &nb, 1, timed ? 0 : -1);
 }
 
 /* Reduce n elements at symmetric offsets. Handles aliasing like the

@@ -862,6 +862,8 @@ void pshmem_finalize (void)
             (void) hipEventDestroy (shmemi.ev[i]);
         free (shmemi.ev);
         shmemi.ev = NULL;
+        free (shmemi.timed_phase);
+        shmemi.timed_phase = NULL;
         shmemi.timed_cap = 0;
     }
     if (shmemi.stream != NULL) {
@@ -1014,23 +1016,30 @@ void shmemi_order_after_caller (int host_wait)
 }
 
 /* Kernel timing without marker packets: the next kernel the combine layer
- * launches carries the event pair itself (hipExtLaunchKernel stamps). */
-void shmemi_timed_begin (void)
+ * launches carries the event pair itself (hipExtLaunchKernel stamps). Each
+ * timed launch has a phase: 0 = the call's dominant kernel (the fold, or the
+ * copy of a 1-PE call), 1 = the all-gather copy of the P2P schedule. */
+void shmemi_timed_begin_phase (int phase)
 {
     if (!shmemi.timing)
         return;
     if (shmemi.ntimed == shmemi.timed_cap) {
         int cap = shmemi.timed_cap ? 2 * shmemi.timed_cap : 256;
         hipEvent_t *ev = (hipEvent_t *) realloc (shmemi.ev, sizeof (hipEvent_t) * 2 * (size_t) cap);
-        if (ev == NULL)
+        int *ph = (int *) realloc (shmemi.timed_phase, sizeof (int) * (size_t) cap);
+        if (ev == NULL || ph == NULL)
             shmemi_fatal ("out of host memory");
+        shmemi.ev = ev;
+        shmemi.timed_phase = ph;
         for (int i = 2 * shmemi.timed_cap; i < 2 * cap; ++i)
             SHMEMI_HIP (hipEventCreate (&ev[i]));
-        shmemi.ev = ev;
         shmemi.timed_cap = cap;
     }
+    shmemi.timed_phase[shmemi.ntimed] = phase;
     mi355_time_next_launch (shmemi.ev[2 * shmemi.ntimed], shmemi.ev[2 * shmemi.ntimed + 1]);
 }
+
+void shmemi_timed_begin (void) { shmemi_timed_begin_phase (0); }
 
 void shmemi_timed_end (void)
 {
@@ -1055,17 +1064,26 @@ void shmemi_timed_marker (int end)
     }
 }
 
-void shmemx_kernel_timing_stats (long *launches, double *total_ms, double *avg_ms)
+void shmemx_kernel_timing_phase_stats (int phase, long *launches, double *total_ms, double *avg_ms)
 {
     double tot = 0.0;
+    long k = 0;
     if (shmemi.ntimed > 0)
         SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
     for (int i = 0; i < shmemi.ntimed; ++i) {
+        if (shmemi.timed_phase[i] != phase)
+            continue;
         float ms = 0.f;
         SHMEMI_HIP (hipEventElapsedTime (&ms, shmemi.ev[2 * i], shmemi.ev[2 * i + 1]));
         tot += ms;
+        ++k;
     }
-    if (launches) *launches = shmemi.ntimed;
+    if (launches) *launches = k;
     if (total_ms) *total_ms = tot;
-    if (avg_ms) *avg_ms = shmemi.ntimed ? tot / shmemi.ntimed : 0.0;
+    if (avg_ms) *avg_ms = k ? tot / (double) k : 0.0;
+}
+
+void shmemx_kernel_timing_stats (long *launches, double *total_ms, double *avg_ms)
+{
+    shmemx_kernel_timing_phase_stats (0, launches, total_ms, avg_ms);
 }

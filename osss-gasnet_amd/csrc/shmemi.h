@@ -113,6 +113,7 @@ struct shmemi_state {
     int ntimed;
     int timed_cap;
     hipEvent_t *ev;             /* 2 per timed launch */
+    int *timed_phase;           /* per timed launch: 0 dominant kernel, 1 all-gather copy */
 };
 
 extern struct shmemi_state shmemi;
@@ -136,6 +137,7 @@ void shmemi_wait_signal (void);
 unsigned shmemi_next_epoch (void);
 unsigned shmemi_wait_flag (unsigned epoch);
 void shmemi_timed_begin (void);
+void shmemi_timed_begin_phase (int phase);
 void shmemi_timed_end (void);
 void shmemi_timed_marker (int end);
 int shmemi_rccl_comm (void **comm);

@@ -51,6 +51,8 @@ def load(path=LIB_PATH):
         "shmemx_kernel_timing": ([_i], None),
         "shmemx_kernel_timing_stats": ([ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_double)], None),
+        "shmemx_kernel_timing_phase_stats": ([_i, ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double),
+                                              ctypes.POINTER(ctypes.c_double)], None),
         "mi355_dtype_size": ([_i], _sz), "mi355_op_supported": ([_i, _i], _i),
         "mi355_combine": ([_i, _i, _vp, ctypes.POINTER(_vp), _i, _sz, _vp], _i),
         "mi355_copy_segments": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_sz), _i, _vp], _i),
@@ -197,6 +199,12 @@ class Shmem:
     def kernel_timing_stats(self):
         n, tot, avg = ctypes.c_long(), ctypes.c_double(), ctypes.c_double()
         self.lib.shmemx_kernel_timing_stats(ctypes.byref(n), ctypes.byref(tot), ctypes.byref(avg))
+        return n.value, tot.value, avg.value
+
+    def kernel_timing_phase_stats(self, phase):
+        """phase 0: each call's dominant kernel; 1: the P2P all-gather copy"""
+        n, tot, avg = ctypes.c_long(), ctypes.c_double(), ctypes.c_double()
+        self.lib.shmemx_kernel_timing_phase_stats(phase, ctypes.byref(n), ctypes.byref(tot), ctypes.byref(avg))
         return n.value, tot.value, avg.value
 
 

@@ -112,8 +112,9 @@ def test_kernel_timing_counts_launches(shm):
     for _ in range(3):
         shm.to_all("sum", "double", b, a, n, 0, 0, 1)
     k, tot, avg = shm.kernel_timing_stats()
+    k1, _, _ = shm.kernel_timing_phase_stats(1)   # no all-gather leg on one PE
     shm.kernel_timing(False)
-    assert k == 3 and tot > 0 and avg > 0
+    assert k == 3 and tot > 0 and avg > 0 and k1 == 0
     shm.free_device(b)
     shm.free_device(a)
 
