@@ -91,6 +91,12 @@ void mi355_signal_next_launch (unsigned *count, unsigned *flag, unsigned epoch);
  * the host learns that everything queued on `stream` before it is done. */
 int mi355_signal_launch (void *stream);
 
+/* Queue a system-scope acquire on every XCD of the current GPU (one small
+ * kernel): afterwards kernels on `stream` do not see L2 copies of peer-GPU
+ * memory older than this point. The P2P schedules queue it after each barrier
+ * that precedes reads of other PEs' buffers. */
+int mi355_acquire_system (void *stream);
+
 /* ---- one-launch P2P reduction for small messages (fused.hip) ----
  * Signal region: per PE, MI355_SIG_WORDS 8-byte words of uncached device
  * memory mapped into every peer; all zero before first use. It holds

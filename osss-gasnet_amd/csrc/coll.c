@@ -213,6 +213,7 @@ static void pull_impl (void **dsts, const void **srcs, size_t *nbytes, int nseg,
     for (int i = 0; i < nseg; ++i)
         dev &= is_device_ptr (dsts[i]);
     if (dev) {
+        shmemi_peer_acquire (shmemi.stream); /* the sources are other PEs' memory */
         for (int base = 0; base < nseg; base += 64) {
             const int k = nseg - base < 64 ? nseg - base : 64;
             const int last = base + k == nseg;

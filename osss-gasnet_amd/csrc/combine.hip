@@ -516,6 +516,29 @@ static int copy_segments_impl(void *const *dsts, const void *const *srcs, const 
     return launch(copy_segments<U>, dim3(gx, used), (hipStream_t)stream, p);
 }
 
+// System-scope acquire on every XCD of this GPU (`buffer_inv sc0 sc1`): drops
+// L2 copies of lines another agent may have rewritten since they were read.
+// Peer GPUs' memory reached through IPC mappings is cached in this GPU's L2
+// without coherence (non-coherent MTYPE), and a kernel boundary on the same
+// stream only acquires at agent scope, so a fold or copy that reads peers'
+// buffers a second time (the next call on the same buffers) could otherwise
+// hit the first call's lines. 32 one-wave blocks: blocks are dealt
+// round-robin over the 8 XCDs, so every XCD's L2 gets invalidated (4 times);
+// the next kernel on the stream starts after all of them. (One block per CU
+// cost ~8 us per call at 4 PEs on one GPU: the invalidates queue up.)
+__global__ __launch_bounds__(64) void acquire_system_k() {
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+}
+
+extern "C" int mi355_acquire_system(void *stream) {
+    hipLaunchKernelGGL(acquire_system_k, dim3(32), dim3(64), 0, (hipStream_t)stream);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
 extern "C" int mi355_signal_launch(void *stream) {
     if (t_sig.flag == nullptr) return MI355_E_INVAL;
     return launch(signal_only, dim3(1), (hipStream_t)stream, EmptyParams{});

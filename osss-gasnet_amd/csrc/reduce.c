@@ -183,6 +183,7 @@ static void p2p_range_dev (int op, int dtype, size_t es, size_t dst_off, size_t 
 
     device_barrier (&a, shmemi.stream); /* every source is ready */
     if (hi > lo) {
+        shmemi_peer_acquire (shmemi.stream);
         for (int i = 0; i < s->size; ++i)
             sp[i] = shmemi_peer_ptr (a.pe[i], src_off + lo * es);
         shmemi_timed_begin ();
@@ -194,6 +195,7 @@ static void p2p_range_dev (int op, int dtype, size_t es, size_t dst_off, size_t 
                           dtype, s->size, hi - lo, rc);
     }
     device_barrier (&a, shmemi.stream); /* every shard is reduced */
+    shmemi_peer_acquire (shmemi.stream);
     int k = 0;
     for (int i = 0; i < s->size; ++i) {
         size_t l, h;
@@ -248,11 +250,13 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
     host_order ();
     shmemi_barrier_set (s->start, s->stride, s->size); /* every source is ready */
     if (hi > lo) {
+        shmemi_peer_acquire (shmemi.stream);
         for (int i = 0; i < s->size; ++i)
             sp[i] = shmemi_peer_ptr (aset_pe (s, i), src_off + lo * es);
         combine_wait (op, dtype, shmemi_peer_ptr (shmemi.mype, dst_off + lo * es), sp, s->size, hi - lo, 1);
     }
     shmemi_barrier_set (s->start, s->stride, s->size); /* every shard is reduced */
+    shmemi_peer_acquire (shmemi.stream);
 
     /* gather the other members' shards from their targets: one launch */
     int k = 0;
@@ -337,6 +341,7 @@ static void exact_into (int op, int dtype, size_t dst_off, size_t src_off, size_
     const void **sp = (const void **) malloc (sizeof (void *) * (size_t) s->size);
     if (sp == NULL)
         shmemi_fatal ("out of host memory");
+    shmemi_peer_acquire (shmemi.stream);
     sp[0] = shmemi_peer_ptr (shmemi.mype, src_off);
     int k = 1;
     for (int i = 0; i < s->size; ++i)
@@ -707,6 +712,7 @@ static void reduce_on_stream (int op, int dtype, const char *fn, void *target, c
             mi355_shard_bounds (n, es, s.size, s.me, &lo, &hi);
             stream_barrier (fn, &s, st); /* every source is ready */
             if (hi > lo) {
+                shmemi_peer_acquire (st);
                 for (int i = 0; i < s.size; ++i)
                     sp[i] = shmemi_peer_ptr (a.pe[i], src_off + lo * es);
                 const int rc = mi355_combine (op, dtype, shmemi_peer_ptr (shmemi.mype, dst_off + lo * es), sp,
@@ -715,6 +721,7 @@ static void reduce_on_stream (int op, int dtype, const char *fn, void *target, c
                     shmemi_fatal ("%s: combine kernel launch failed: %d", fn, rc);
             }
             stream_barrier (fn, &s, st); /* every shard is reduced */
+            shmemi_peer_acquire (st);
             int k = 0;
             for (int i = 0; i < s.size; ++i) {
                 size_t l, h;

@@ -456,6 +456,8 @@ static void heap_exchange (void)
                 (void) hipGetLastError ();
             }
         }
+        if (peer_dev != shmemi.device)
+            shmemi.peer_acquire = 1; /* a peer on another GPU (or one this process cannot see) */
         void *p = NULL;
         hipError_t e = hipIpcOpenMemHandle (&p, pi->heap_handle, hipIpcMemLazyEnablePeerAccess);
         if (e != hipSuccess)
@@ -772,6 +774,9 @@ void pshmem_init (void)
     if (shmemi.npes > 1) {
         bootstrap_attach ();
         heap_exchange ();
+        /* SHMEM_PEER_ACQUIRE=0|1 overrides the choice made from the peers' devices */
+        static const char *pa_env[] = {"SHMEM_PEER_ACQUIRE", NULL};
+        shmemi.peer_acquire = (int) env_long (pa_env, shmemi.peer_acquire) != 0;
         interconnect_selftest ();
         if (shmemi.mype == 0 && !shmemi.seg_unlinked) {
             shm_unlink (shmemi.seg_name); /* every PE is attached: drop the name */
@@ -1013,6 +1018,20 @@ void shmemi_order_after_caller (int host_wait)
     if (rc != 0)
         shmemi_fatal ("signal kernel launch failed: %d", rc);
     shmemi_wait_signal ();
+}
+
+/* Before a kernel reads buffers that other PEs wrote since this GPU last read
+ * them: their GPUs' memory is cached in this GPU's L2 without coherence, so
+ * queue a system-scope acquire on every XCD first (mi355_acquire_system).
+ * Only when some peer is on another GPU (PEs sharing one GPU read their own
+ * device's memory, coherent in its L2), or SHMEM_PEER_ACQUIRE=1. */
+void shmemi_peer_acquire (hipStream_t st)
+{
+    if (!shmemi.peer_acquire)
+        return;
+    const int rc = mi355_acquire_system (st);
+    if (rc != 0)
+        shmemi_fatal ("acquire kernel launch failed: %d", rc);
 }
 
 /* Kernel timing without marker packets: the next kernel the combine layer

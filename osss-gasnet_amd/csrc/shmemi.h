@@ -71,6 +71,7 @@ struct shmemi_state {
     int debug;
     int entry_sync;             /* SHMEM_ENTRY_SYNC: hipDeviceSynchronize on entry */
     int p2p_broken;             /* init self-test: peer heap reads failed */
+    int peer_acquire;           /* queue mi355_acquire_system before reads of peers' buffers */
 
     /* bootstrap */
     struct shmemi_seg *seg;
@@ -128,6 +129,7 @@ size_t shmemi_heap_offset (const void *p);
 void *shmemi_peer_ptr (int pe, size_t off);
 void shmemi_order_after_caller (int host_wait);
 void shmemi_check_stream_err (const char *fn);
+void shmemi_peer_acquire (hipStream_t st);
 
 /* reduce.c: device-flag barrier on the library stream (host channel) */
 int shmemi_dev_barrier_ok (int PE_start, int stride, int PE_size);

@@ -131,6 +131,7 @@ void shmemi_trace_show_info (void)
         {"SHMEM_FUSED_MAX_BYTES", "largest message for the one-launch fused reduction (default 1M)"},
         {"SHMEM_BARRIER_TIMEOUT", "seconds before a barrier wait aborts the job (default 600)"},
         {"SHMEM_ENTRY_SYNC", "1: every call starts with hipDeviceSynchronize"},
+        {"SHMEM_PEER_ACQUIRE", "1/0: system-scope L2 acquire before reading peers' buffers (default: on if a peer is on another GPU)"},
     };
     shmemi_trace_emit (SHMEMI_LOG_INFO, "environment variables understood by this build:");
     for (size_t i = 0; i < sizeof vars / sizeof vars[0]; ++i)

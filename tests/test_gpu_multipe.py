@@ -34,7 +34,10 @@ def run_pes(npes, cases, tmp_path, extra_env=None, timeout=600):
     env = dict(os.environ)
     env.update({"SHMEM_NPES": str(npes), "SHMEM_JOB_ID": uuid.uuid4().hex[:12], "SHMEM_DEVICE": "0",
                 "SHMEM_DEVICE_HEAP_SIZE": "96M", "SHMEM_DEVICE_SCRATCH_SIZE": "384K",
-                "SHMEM_BARRIER_TIMEOUT": "120"})
+                "SHMEM_BARRIER_TIMEOUT": "120",
+                # the multi-GPU layout queues a system-scope acquire before every read of peers'
+                # buffers (peers on other GPUs); the PEs here share one GPU, so force it on
+                "SHMEM_PEER_ACQUIRE": "1"})
     if npes > 4:
         # PEs sharing the one test GPU: keep the job's hardware queues at 16
         # (8 processes x the default 4 oversubscribe the GPU's queue slots and
