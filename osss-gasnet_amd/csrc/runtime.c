@@ -794,8 +794,10 @@ void pshmem_init (void)
         SHMEMI_TRACE (SHMEMI_LOG_INIT, "device heap %zu bytes (user %zu, scratch 3 x %zu), signal region %s",
                       shmemi.heap_size, shmemi.user_size, shmemi.scratch_chunk,
                       shmemi.sig_broken ? "off (self-test failed)" : "on");
-        SHMEMI_TRACE (SHMEMI_LOG_INIT, "reduce algorithm %s, fused path up to %zu bytes, peer heap reads %s",
-                      alg[shmemi.algorithm & 3], shmemi.fused_max, shmemi.p2p_broken ? "FAILED (RCCL)" : "ok");
+        SHMEMI_TRACE (SHMEMI_LOG_INIT,
+                      "reduce algorithm %s, fused path up to %zu bytes, peer heap reads %s, peer L2 acquire %s",
+                      alg[shmemi.algorithm & 3], shmemi.fused_max, shmemi.p2p_broken ? "FAILED (RCCL)" : "ok",
+                      shmemi.peer_acquire ? "on" : "off");
     }
     shmemi_trace_show_info ();
     static int registered = 0;
