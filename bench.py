@@ -61,8 +61,8 @@ def cpu_baseline(n, budget_s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--mib", type=int, default=256, help="MiB per PE")
     ap.add_argument("--algorithm", default=os.environ.get("SHMEM_REDUCE_ALGORITHM", "auto"))
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
