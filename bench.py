@@ -165,7 +165,14 @@ def main():
         shm.to_all("min", "int", lo.ctypes.data, dev.ctypes.data, 1, 0, 0, npes)
         shm.to_all("max", "int", hi.ctypes.data, dev.ctypes.data, 1, 0, 0, npes)
         distinct_gpus = int(lo[0]) != int(hi[0])
+    rccl_ok = False
     if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host:
+        # non-blocking RCCL bring-up with a deadline; every PE must have it
+        mine = np.array([1 if shm.lib.shmemx_rccl_init(60.0) == 0 else 0], dtype=np.int32)
+        allok = np.zeros(1, dtype=np.int32)
+        shm.to_all("min", "int", allok.ctypes.data, mine.ctypes.data, 1, 0, 0, npes)
+        rccl_ok = bool(allok[0])
+    if rccl_ok:
         shm.set_algorithm("rccl")
         steps(3)
         shm.barrier_all()
@@ -184,6 +191,8 @@ def main():
     t_max = float(tout[0])
     t_step = t_max / args.steps
     rccl = None
+    if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host and not rccl_ok:
+        rccl = {"error": "RCCL communicator did not come up within 60 s on every PE; comparison skipped"}
     if t_rccl_local is not None:
         tbuf[0] = t_rccl_local
         shm.to_all("max", "double", tout.ctypes.data, tbuf.ctypes.data, 1, 0, 0, npes)

@@ -64,6 +64,11 @@ void shmemx_kernel_timing_stats (long *launches, double *total_ms, double *avg_m
  * shmemx_kernel_timing_stats reports), 1 = the all-gather copy of the P2P schedule */
 void shmemx_kernel_timing_phase_stats (int phase, long *launches, double *total_ms, double *avg_ms);
 
+/* Bring up the RCCL communicator of the whole job (what SHMEM_REDUCE_ALGORITHM=rccl uses) without
+ * aborting when RCCL cannot come up within timeout_s seconds: 0 = ready on this PE, -1 = not. Every PE
+ * must call it; agree on the outcome (e.g. a min reduction) before selecting the RCCL schedule. */
+int shmemx_rccl_init (double timeout_s);
+
 /* Stream-ordered collectives. Enqueued on `stream` (a hipStream_t; NULL =
  * the null stream) and return at once: the reduction runs after the work
  * queued on that stream before it, and the work queued after it sees the

@@ -7,7 +7,11 @@
  * from the reference's, so floating-point results on this path are within
  * the tolerance stated in DESIGN.md, not bit-exact.
  */
+#define _DEFAULT_SOURCE
+#include <stdio.h>
 #include <string.h>
+#include <time.h>
+#include <unistd.h>
 
 #include <rccl/rccl.h>
 
@@ -33,28 +37,88 @@ int shmemi_rccl_supported (int op, int dtype)
     }
 }
 
+static double mono_s (void)
+{
+    struct timespec ts;
+    clock_gettime (CLOCK_MONOTONIC, &ts);
+    return (double) ts.tv_sec + 1e-9 * (double) ts.tv_nsec;
+}
+
+/* Wait for a non-blocking communicator's pending work (init or an enqueue)
+ * with a deadline; ncclSuccess, an error, or ncclInProgress on timeout. */
+static ncclResult_t rccl_settle (ncclComm_t c, ncclResult_t r, double timeout_s)
+{
+    const double t0 = mono_s ();
+    while (r == ncclInProgress) {
+        if (mono_s () - t0 > timeout_s)
+            return ncclInProgress;
+        usleep (50);
+        if (ncclCommGetAsyncError (c, &r) != ncclSuccess)
+            return ncclSystemError;
+    }
+    return r;
+}
+
+/* The whole job's communicator, created non-blocking so a peer that never
+ * arrives cannot hang this PE: 0, or -1 (nothing kept) when RCCL did not come
+ * up within timeout_s. The unique id travels through the bootstrap segment. */
+static int rccl_comm_create (double timeout_s, char *why, size_t why_len)
+{
+    ncclUniqueId id;
+    _Static_assert (sizeof id <= sizeof shmemi.seg->rccl_id, "ncclUniqueId too large");
+    memset (&id, 0, sizeof id);
+    if (shmemi.mype == 0 && ncclGetUniqueId (&id) != ncclSuccess) {
+        snprintf (why, why_len, "ncclGetUniqueId failed");
+        return -1; /* the other PEs time out below */
+    }
+    if (shmemi.seg != NULL) { /* one PE has no bootstrap segment */
+        if (shmemi.mype == 0)
+            memcpy (shmemi.seg->rccl_id, &id, sizeof id);
+        shmemi_barrier_set (0, 1, shmemi.npes);
+        memcpy (&id, shmemi.seg->rccl_id, sizeof id);
+    }
+    ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+    cfg.blocking = 0;
+    ncclComm_t c = NULL;
+    ncclResult_t r = ncclCommInitRankConfig (&c, shmemi.npes, id, shmemi.mype, &cfg);
+    if (c != NULL)
+        r = rccl_settle (c, r, timeout_s);
+    if (r != ncclSuccess) {
+        snprintf (why, why_len, "ncclCommInitRankConfig: %s",
+                  r == ncclInProgress ? "timed out" : ncclGetErrorString (r));
+        if (c != NULL)
+            ncclCommAbort (c);
+        return -1;
+    }
+    shmemi.rccl_comm = (void *) c;
+    return 0;
+}
+
 int shmemi_rccl_comm (void **comm)
 {
     if (shmemi.rccl_comm == NULL) {
-        ncclUniqueId id;
-        _Static_assert (sizeof id <= sizeof shmemi.seg->rccl_id, "ncclUniqueId too large");
-        if (shmemi.mype == 0 && ncclGetUniqueId (&id) != ncclSuccess)
-            shmemi_fatal ("ncclGetUniqueId failed");
-        if (shmemi.seg != NULL) { /* one PE has no bootstrap segment */
-            if (shmemi.mype == 0)
-                memcpy (shmemi.seg->rccl_id, &id, sizeof id);
-            shmemi_barrier_set (0, 1, shmemi.npes);
-            memcpy (&id, shmemi.seg->rccl_id, sizeof id);
-        }
-        ncclComm_t c;
-        ncclResult_t r = ncclCommInitRank (&c, shmemi.npes, id, shmemi.mype);
-        if (r != ncclSuccess)
-            shmemi_fatal ("ncclCommInitRank: %s", ncclGetErrorString (r));
-        shmemi.rccl_comm = (void *) c;
+        char why[160] = "";
+        if (rccl_comm_create (shmemi.barrier_timeout, why, sizeof why) != 0)
+            shmemi_fatal ("RCCL communicator: %s", why);
         shmemi_barrier_set (0, 1, shmemi.npes);
     }
     *comm = shmemi.rccl_comm;
     return 0;
+}
+
+/* Bring RCCL up without aborting the job when it cannot: 0 when the
+ * communicator exists on this PE, -1 otherwise (callers agree among
+ * themselves before relying on it, e.g. with a min reduction). */
+int shmemx_rccl_init (double timeout_s)
+{
+    shmemi_init_check ("shmemx_rccl_init");
+    if (shmemi.rccl_comm != NULL)
+        return 0;
+    char why[160] = "";
+    const int rc = rccl_comm_create (timeout_s, why, sizeof why);
+    if (rc != 0)
+        fprintf (stderr, "[shmem PE %d] RCCL unavailable: %s\n", shmemi.mype, why);
+    return rc;
 }
 
 void shmemi_rccl_destroy (void)
@@ -92,6 +156,7 @@ int shmemi_rccl_allreduce (int op, int dtype, const void *src, void *dst, size_t
     shmemi_timed_marker (0);
     ncclResult_t r = ncclAllReduce (src, dst, count, t, o, (ncclComm_t) comm, shmemi.stream);
     shmemi_timed_marker (1);
+    r = rccl_settle ((ncclComm_t) comm, r, shmemi.barrier_timeout); /* non-blocking communicator */
     if (r != ncclSuccess)
         return -1;
     SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));

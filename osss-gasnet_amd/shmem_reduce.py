@@ -49,6 +49,7 @@ def load(path=LIB_PATH):
         "shmemx_device_id": ([], _i), "shmemx_device_synchronize": ([], None),
         "shmemx_memcpy": ([_vp, _vp, _sz], None), "shmemx_wtime": ([], ctypes.c_double),
         "shmemx_kernel_timing": ([_i], None),
+        "shmemx_rccl_init": ([ctypes.c_double], _i),
         "shmemx_kernel_timing_stats": ([ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_double)], None),
         "shmemx_kernel_timing_phase_stats": ([_i, ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double),

@@ -130,10 +130,12 @@ def test_psync_is_left_at_sync_value(shm):
 @pytest.mark.parametrize("op,dtype", [("sum", "double"), ("max", "float"), ("min", "int"), ("prod", "long"),
                                       ("sum", "complexd"), ("sum", "complexf")])
 def test_rccl_glue_one_rank(shm, op, dtype):
-    """The RCCL schedule's glue (csrc/rccl.c: communicator setup, type/op
-    mapping, complex sum as 2n reals) on a 1-rank communicator, where
-    ncclAllReduce is the identity. Multi-rank RCCL needs one GPU per rank (RCCL
-    refuses two ranks on one device), so this is what the one-GPU box can run."""
+    """The RCCL schedule's glue (csrc/rccl.c: non-blocking communicator
+    bring-up with a deadline, type/op mapping, complex sum as 2n reals) on a
+    1-rank communicator, where ncclAllReduce is the identity. Multi-rank RCCL
+    needs one GPU per rank (RCCL refuses two ranks on one device), so this is
+    what the one-GPU box can run."""
+    assert shm.lib.shmemx_rccl_init(30.0) == 0
     f = shm.lib.shmemi_rccl_allreduce
     f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
     f.restype = ctypes.c_int

@@ -188,6 +188,31 @@ def test_bad_active_set_aborts_every_pe(tmp_path):
     assert procs[0].returncode != 0 and "aborting" in outs[0][0]
 
 
+def test_rccl_init_is_bounded_on_a_shared_gpu(tmp_path):
+    """shmemx_rccl_init (non-blocking RCCL bring-up with a deadline): with two
+    PEs on ONE GPU, which RCCL does not support, it must come back on both PEs
+    (ready or not, the same answer) instead of hanging or aborting the job, and
+    the P2P schedule must still work afterwards. bench.py relies on this before
+    timing its RCCL comparison leg."""
+    env = dict(os.environ, SHMEM_NPES="2", SHMEM_JOB_ID=uuid.uuid4().hex[:12], SHMEM_DEVICE="0",
+               SHMEM_DEVICE_HEAP_SIZE="32M", SHMEM_DEVICE_SCRATCH_SIZE="384K", SHMEM_BARRIER_TIMEOUT="60")
+    code = ("import sys,os,time; sys.path[:0]=[%r,%r]\n" % (HERE, os.path.join(os.path.dirname(HERE), "osss-gasnet_amd")) +
+            "import numpy as np, shmem_reduce\nshm=shmem_reduce.Shmem(); shm.init()\n"
+            "t0=time.time(); rc=shm.lib.shmemx_rccl_init(15.0); dt=time.time()-t0\n"
+            "d=shm.malloc_device(1024); shm.put(d, np.full(16, 1.0 + shm.my_pe()))\n"
+            "shm.to_all('sum','double',d,d,16,0,0,2)\n"
+            "ok=(shm.get(d,16,'double')==3.0).all()\n"
+            "print('rc', rc, 'dt %.1f' % dt, 'p2p', ok, flush=True)\nshm.finalize()\n")
+    procs = [subprocess.Popen([sys.executable, "-c", code], env=dict(env, SHMEM_PE=str(pe)),
+                              stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for pe in range(2)]
+    outs = [p.communicate(timeout=100)[0] for p in procs]
+    for p, out in zip(procs, outs):
+        assert p.returncode == 0, out[-2000:]
+        assert "p2p True" in out, out[-2000:]
+    rcs = [int(o.split("rc ")[1].split()[0]) for o in outs]
+    assert rcs[0] == rcs[1], outs
+
+
 def test_random_sequence_stress(tmp_path):
     """300 back-to-back reductions with random op/type, size (0 .. 300k elements,
     across the fused/multi-launch threshold), buffer mode, schedule and active
