@@ -213,6 +213,16 @@ def test_rccl_init_is_bounded_on_a_shared_gpu(tmp_path):
     assert rcs[0] == rcs[1], outs
 
 
+def test_signal_region_mapping_failure_falls_back(tmp_path):
+    """One PE cannot map the peers' signal regions (SHMEM_TEST_IPC_FAIL=sig
+    on PE 1): init must not abort; every PE agrees to run without device-side
+    flags (no fused kernel, host barriers) and the results stay exact."""
+    cases = make_cases(SOME, 1000, [[0, 0, 3]], "dev", "p2p", 0)
+    cases += make_cases(SOME[:3], 200000, [[0, 0, 3]], "dev", "p2p", 100)
+    results = run_pes(3, cases, tmp_path, extra_env={"SHMEM_TEST_IPC_FAIL": "sig"})
+    check(results, cases)
+
+
 def test_random_sequence_stress(tmp_path):
     """300 back-to-back reductions with random op/type, size (0 .. 300k elements,
     across the fused/multi-launch threshold), buffer mode, schedule and active
