@@ -144,7 +144,7 @@ def main():
     shm.kernel_timing(False)
 
     # the many-small-bucket regime (BASELINE config 5 shape: 64 KiB per call)
-    small_n, small_calls = 8192, 0 if args.no_small else 1000
+    small_n, small_calls = 8192, 0 if args.no_small else 4096   # BASELINE config 5: 4096 x 64 KiB
     t_small = None
     if small_calls:
         steps(20, small_n)
@@ -294,7 +294,7 @@ def main():
             "cpu_baseline": cpu,
             "small_call": None if t_small is None else
             {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small * 1e6, 2), "calls": small_calls,
-             "note": "64 KiB shmem_double_sum_to_all back-to-back (PE 0 clock)"},
+             "note": "BASELINE config 5 shape: 4096 back-to-back 64 KiB shmem_double_sum_to_all calls, PE 0 clock"},
             "check": check,
         }
         print(json.dumps(out), flush=True)
