@@ -14,7 +14,7 @@ OUT=gpurun_out/prof_$R
 DST=gpurun_out/profiles/$R
 mkdir -p "$OUT" "$DST/pmc"
 export TMPDIR=/tmp
-BENCH=(bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-small)
+BENCH=(bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-small)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "${BENCH[@]}" \
     > "$OUT/bench_trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 "${BENCH[@]}" --no-check \
