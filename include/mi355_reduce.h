@@ -113,6 +113,7 @@ int mi355_acquire_system (void *stream);
 #define MI355_SIG_RS_COUNT 4096  /* local block counters (own 128-byte lines)          */
 #define MI355_SIG_AG_COUNT 4112
 #define MI355_SIG_ERROR 4128
+#define MI355_SIG_STAGE_COUNT 4144
 #define MI355_SIG_CHANNEL_WORDS 4160
 #define MI355_SIG_CHANNELS 2
 #define MI355_SIG_SELFTEST (MI355_SIG_CHANNELS * MI355_SIG_CHANNEL_WORDS) /* [PE]: init-time check */
@@ -131,6 +132,11 @@ typedef struct MI355FusedArgs {
     unsigned epoch;                   /* stored there when done (| 1u<<31: timeout) */
     unsigned *err_flag;               /* host-coherent; set to 1 on a timeout, or NULL */
     unsigned long long timeout_ticks; /* bound on every wait, 100 MHz ticks       */
+    /* Host-staged form (or NULL): device-accessible pointers to this PE's page-locked HOST source and
+     * target. The kernel first copies host_src into src[me], and at the end dst[me] into host_dst, so
+     * a small reduction of host arrays is one launch (src/dst are then this PE's staging scratch). */
+    const void *host_src;
+    void *host_dst;
 } MI355FusedArgs;
 
 /* Reduce-scatter + all-gather of n elements over the members in ONE launch:

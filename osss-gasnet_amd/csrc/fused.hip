@@ -126,6 +126,26 @@ __device__ void finish(const MI355FusedArgs &a, unsigned long long *mine, const 
     }
 }
 
+// Byte copy shared by `nblocks` blocks, this one being number `bi` of them:
+// 16-byte vectors when both ends allow it, then the byte tail; stores
+// write-through at system scope (the destination is read by peers or by the
+// host next). A block that stored the byte tail (plain stores) releases at
+// system scope.
+__device__ void block_copy(void *dst, const void *src, uint64_t nbytes, unsigned bi, unsigned nblocks) {
+    const bool vec = ((((uintptr_t)dst) | ((uintptr_t)src)) & 15) == 0;
+    const uint64_t nv = vec ? nbytes / 16 : 0;
+    for (uint64_t v = (uint64_t)bi * kBlock + threadIdx.x; v < nv; v += (uint64_t)nblocks * kBlock)
+        st16_sys((u32x4 *)dst + v, ((const u32x4 *)src)[v]);
+    bool plain = false;
+    for (uint64_t b = nv * 16 + (uint64_t)bi * kBlock + threadIdx.x; b < nbytes;
+         b += (uint64_t)nblocks * kBlock) {
+        ((char *)dst)[b] = ((const char *)src)[b];
+        plain = true;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (__syncthreads_or(plain) && threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
 template <int OP, typename T>
 __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
     constexpr int V = 16 / sizeof(T);
@@ -135,13 +155,27 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
     if (threadIdx.x == 0) ok_all = 1;
     load_counts(a, mine, cnt);
 
-    // ---- arrive
-    if (blockIdx.x == 0) {
+    const bool staged = a.host_src != nullptr;
+    if (staged) {
+        // ---- stage in: this PE's host source -> its staging source (every
+        // block; the host may have rewritten the source since the last call,
+        // so drop stale cached copies first). The grid's last block then
+        // announces arrival to every member, this PE included: the blocks
+        // that read src[me] below wait for it like for the peers.
+        if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        __syncthreads();
+        block_copy((void *)a.src[a.me], a.host_src, a.n * sizeof(T), blockIdx.x, gridDim.x);
+        if (last_block(mine + MI355_SIG_STAGE_COUNT)) {
+            if (threadIdx.x < a.nmembers)
+                st_sys_u64(a.sig[threadIdx.x] + MI355_SIG_ARRIVE + a.pe[a.me], cnt[threadIdx.x]);
+        }
+    } else if (blockIdx.x == 0) {
+        // ---- arrive (the source was written before the kernel started)
         if (threadIdx.x < a.nmembers && threadIdx.x != a.me)
             st_sys_u64(a.sig[threadIdx.x] + MI355_SIG_ARRIVE + a.pe[a.me], cnt[threadIdx.x]);
     }
     __syncthreads();
-    if (!wait_members(a, mine, cnt, MI355_SIG_ARRIVE, false)) ok_all = 0;
+    if (!wait_members(a, mine, cnt, MI355_SIG_ARRIVE, staged)) ok_all = 0;
     __syncthreads();
     if (!ok_all) goto fail;
 
@@ -207,6 +241,35 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the element tail went through L2
         if (last_block(mine + MI355_SIG_AG_COUNT)) {
             publish(a, cnt, MI355_SIG_AGDONE);
+            if (!staged) {
+                __syncthreads();
+                if (!wait_members(a, mine, cnt, MI355_SIG_AGDONE, true)) ok_all = 0;
+                __syncthreads();
+                finish(a, mine, cnt, ok_all != 0);
+                return;
+            }
+        }
+        if (!staged) return;
+        // ---- stage out (every block): dst[me] is complete once this PE's own
+        // AGDONE slot shows this call (published above by the gather's last
+        // block, after every block's write-through stores drained); acquire,
+        // copy this block's part to the host target, count the blocks out;
+        // the last one waits for every member's AGDONE and reports
+        if (threadIdx.x == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (ld_sys_u64(mine + MI355_SIG_AGDONE + a.pe[a.me]) < cnt[a.me]) {
+                if (__builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks) {
+                    ok_all = 0;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+        }
+        __syncthreads();
+        if (ok_all) block_copy(a.host_dst, a.dst[a.me], a.n * sizeof(T), blockIdx.x, gridDim.x);
+        if (last_block(mine + MI355_SIG_STAGE_COUNT)) {
+            if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             __syncthreads();
             if (!wait_members(a, mine, cnt, MI355_SIG_AGDONE, true)) ok_all = 0;
             __syncthreads();

@@ -46,6 +46,7 @@ struct shmemi_hostblk {
     void *p;
     size_t size;
     int registered;
+    char *dev; /* device-accessible address of p (registered blocks), else NULL */
     struct shmemi_hostblk *next;
 };
 
@@ -700,6 +701,9 @@ void *pshmem_malloc (size_t size)
         /* page-locked so the staging copies run at full PCIe rate */
         if (shmemi.device >= 0) {
             h->registered = hipHostRegister (p, round_up (size, 4096), hipHostRegisterDefault) == hipSuccess;
+            void *d = NULL;
+            if (h->registered && hipHostGetDevicePointer (&d, p, 0) == hipSuccess)
+                h->dev = (char *) d;
             (void) hipGetLastError ();
         }
         h->next = shmemi.host_blocks;
@@ -708,6 +712,18 @@ void *pshmem_malloc (size_t size)
     SHMEMI_TRACE (SHMEMI_LOG_MEMORY, "shmem_malloc(%zu) = %p (host)", size, p);
     shmem_barrier_all ();
     return p;
+}
+
+/* Device-accessible address of [p, p + nbytes) when it lies inside one
+ * page-locked shmem_malloc block (kernels can then read and write it over
+ * PCIe directly), else NULL. */
+void *shmemi_host_dev_ptr (const void *p, size_t nbytes)
+{
+    const char *c = (const char *) p;
+    for (const struct shmemi_hostblk *h = shmemi.host_blocks; h != NULL; h = h->next)
+        if (h->dev != NULL && c >= (const char *) h->p && c + nbytes <= (const char *) h->p + h->size)
+            return h->dev + (c - (const char *) h->p);
+    return NULL;
 }
 
 static void host_free_one (struct shmemi_hostblk *h)

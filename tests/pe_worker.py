@@ -191,6 +191,7 @@ def fortran_to_all(shm, op, dtype, dst, src, n, start, logstride, size):
 
 
 def main():
+    import ctypes
     spec = json.load(open(sys.argv[1]))
     outdir = sys.argv[2]
     shm = shmem_reduce.Shmem()
@@ -231,18 +232,36 @@ def main():
             src, dst = da + 5 * es, da
         elif mode == "host":
             src, dst = ha, hb
+        elif mode == "host_mixed":
+            # even PEs: page-locked shmem_malloc arrays (one-launch in-kernel
+            # staging for small n); odd PEs: plain numpy arrays (staged copies)
+            if me % 2 == 0:
+                src, dst = ha, hb
+            else:
+                np_src = np.zeros(max(n, 1), dtype=shmem_reduce.NP[dtype])
+                np_dst = np.zeros(max(n, 1), dtype=shmem_reduce.NP[dtype])
+                src, dst = np_src.ctypes.data, np_dst.ctypes.data
         elif mode == "unaligned":        # device, both one element off 16-byte alignment
             src, dst = da + es, db + es
         else:
             raise ValueError(mode)
         if n:
-            shm.put(src, x)
+            if mode.startswith("host"):
+                ctypes.memmove(src, x.ctypes.data, x.nbytes)
+            else:
+                shm.put(src, x)
         shm.set_algorithm(c.get("algorithm", "auto"))
         if c.get("api") == "fortran":
             fortran_to_all(shm, op, dtype, dst, src, n, *mine)
         else:
             shm.to_all(op, dtype, dst, src, n, *mine)
-        results[str(c["id"])] = shm.get(dst, n, dtype) if n else np.zeros(0, dtype=shmem_reduce.NP[dtype])
+        if mode.startswith("host"):
+            out = np.empty(n, dtype=shmem_reduce.NP[dtype])
+            if n:
+                ctypes.memmove(out.ctypes.data, dst, out.nbytes)
+            results[str(c["id"])] = out
+        else:
+            results[str(c["id"])] = shm.get(dst, n, dtype) if n else np.zeros(0, dtype=shmem_reduce.NP[dtype])
     shm.free(hb)
     shm.free(ha)
     shm.free_device(db)

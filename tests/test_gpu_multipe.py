@@ -213,6 +213,23 @@ def test_rccl_init_is_bounded_on_a_shared_gpu(tmp_path):
     assert rcs[0] == rcs[1], outs
 
 
+def test_small_host_arrays_one_launch_and_mixed(tmp_path):
+    """Host arrays (shmem_malloc, page-locked) up to 64 KiB take the one-launch
+    path with in-kernel staging; odd PEs use plain numpy arrays (staged
+    copies) in the same collectives: both forms must meet and agree. Sizes
+    around the 64 KiB limit and the multi-chunk path above it."""
+    cases = []
+    cid = 0
+    for mode in ("host", "host_mixed"):
+        for n in (1, 3, 515, 8191, 8192, 8193, 100000):
+            cases += make_cases([("sum", "double"), ("max", "int"), ("xor", "short"), ("prod", "complexf")],
+                                n, [[0, 0, 4]], mode, "p2p", cid)
+            cid += 100
+    cases += make_cases(SOME, 515, [[0, 1, 2], [1, 1, 2]], "host_mixed", "p2p", cid)
+    results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_DEVICE_SCRATCH_SIZE": "3M"})
+    check(results, cases)
+
+
 def test_signal_region_mapping_failure_falls_back(tmp_path):
     """One PE cannot map the peers' signal regions (SHMEM_TEST_IPC_FAIL=sig
     on PE 1): init must not abort; every PE agrees to run without device-side

@@ -6,9 +6,11 @@
  *   gcc -O2 -Iinclude tools/size_sweep.c -Losss-gasnet_amd/lib -lshmem_reduce \
  *       -Wl,-rpath,$PWD/osss-gasnet_amd/lib -o tools/size_sweep
  *   tools/oshrun -np 4 --same-device tools/size_sweep      (or run directly: 1 PE)
+ *   tools/size_sweep host [max_bytes]    source/target from shmem_malloc (host memory, staged)
  */
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
 
 #include <shmem.h>
 #include <shmemx.h>
@@ -21,15 +23,19 @@ static int cmp (const void *a, const void *b)
     return x < y ? -1 : x > y;
 }
 
-int main (void)
+int main (int argc, char **argv)
 {
+    const int host = argc > 1 && strcmp (argv[1], "host") == 0;
+    const size_t max_bytes = argc > 2 ? (size_t) strtoull (argv[2], NULL, 10) : ((size_t) 1 << 28);
     for (int i = 0; i < SHMEM_REDUCE_SYNC_SIZE; ++i)
         psync[i] = SHMEM_SYNC_VALUE;
     shmem_init ();
     const int me = shmem_my_pe (), npes = shmem_n_pes ();
-    const size_t nmax = (size_t) 1 << 25; /* 256 MiB of doubles */
-    double *src = (double *) shmemx_malloc_device (nmax * sizeof (double));
-    double *dst = (double *) shmemx_malloc_device (nmax * sizeof (double));
+    const size_t nmax = max_bytes / sizeof (double); /* default 256 MiB of doubles */
+    double *src = (double *) (host ? shmem_malloc (nmax * sizeof (double))
+                                   : shmemx_malloc_device (nmax * sizeof (double)));
+    double *dst = (double *) (host ? shmem_malloc (nmax * sizeof (double))
+                                   : shmemx_malloc_device (nmax * sizeof (double)));
     double *h = (double *) malloc (nmax * sizeof (double));
     for (size_t i = 0; i < nmax; ++i)
         h[i] = (double) (i % 1000) * 0.5 + me;
@@ -55,12 +61,18 @@ int main (void)
         }
         qsort (t, reps, sizeof t[0], cmp);
         if (me == 0)
-            printf ("{\"npes\": %d, \"bytes_per_pe\": %zu, \"us_per_call\": %.2f, \"gib_s_reduced_per_pe\": %.2f}\n",
-                    npes, bytes, t[reps / 2] * 1e6, (double) bytes / t[reps / 2] / (double) (1 << 30));
+            printf ("{\"npes\": %d, \"memory\": \"%s\", \"bytes_per_pe\": %zu, \"us_per_call\": %.2f, "
+                    "\"gib_s_reduced_per_pe\": %.2f}\n", npes, host ? "host" : "device", bytes, t[reps / 2] * 1e6,
+                    (double) bytes / t[reps / 2] / (double) (1 << 30));
         fflush (stdout);
     }
-    shmemx_free_device (dst);
-    shmemx_free_device (src);
+    if (host) {
+        shmem_free (dst);
+        shmem_free (src);
+    } else {
+        shmemx_free_device (dst);
+        shmemx_free_device (src);
+    }
     shmem_finalize ();
     return 0;
 }
