@@ -251,7 +251,7 @@ def test_random_sequence_stress(tmp_path):
     for cid in range(300):
         op, dtype = oracle.PAIRS[rng.integers(len(oracle.PAIRS))]
         n = int(rng.choice([0, 1, 7, 64, 1000, 8191, 40000, 150000, 300000]))
-        mode = str(rng.choice(["dev", "dev", "inplace", "host"]))
+        mode = str(rng.choice(["dev", "dev", "inplace", "host", "host_mixed"]))
         alg = str(rng.choice(["p2p", "p2p", "p2p", "exact"]))
         sets = sets_choices[rng.integers(len(sets_choices))]
         cases.append({"id": cid, "op": op, "dtype": dtype, "n": n, "sets": sets, "mode": mode,
