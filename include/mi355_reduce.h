@@ -137,6 +137,9 @@ typedef struct MI355FusedArgs {
      * a small reduction of host arrays is one launch (src/dst are then this PE's staging scratch). */
     const void *host_src;
     void *host_dst;
+    /* 1: one-shot -- every member folds the whole array from all members' sources (one flag exchange
+     * fewer than reduce-scatter + all-gather; for small messages). Needs dst != src. */
+    int oneshot;
 } MI355FusedArgs;
 
 /* Reduce-scatter + all-gather of n elements over the members in ONE launch:

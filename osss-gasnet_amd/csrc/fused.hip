@@ -180,9 +180,13 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
     if (!ok_all) goto fail;
 
     {
-        // ---- reduce shard `me`
-        const uint64_t lo = (uint64_t)a.me * a.shard;
-        const uint64_t hi = lo + a.shard < a.n ? lo + a.shard : a.n;
+        // ---- fold: one-shot = the whole array from every member's source
+        // (no reduce-scatter/all-gather split, one flag exchange fewer);
+        // otherwise shard `me` (the reduce-scatter leg)
+        const bool oneshot = a.oneshot != 0;
+        bool tail_plain = false;
+        const uint64_t lo = oneshot ? 0 : (uint64_t)a.me * a.shard;
+        const uint64_t hi = oneshot ? a.n : (lo + a.shard < a.n ? lo + a.shard : a.n);
         if (hi > lo) {
             const uint64_t nv = (hi - lo) / V;
             const int nm = a.nmembers;
@@ -211,31 +215,35 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
                 if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // plain tail stores
             }
         }
-        if (last_block(mine + MI355_SIG_RS_COUNT)) publish(a, cnt, MI355_SIG_RSDONE);
+        if (!oneshot) {
+            if (last_block(mine + MI355_SIG_RS_COUNT)) publish(a, cnt, MI355_SIG_RSDONE);
 
-        // ---- every shard is reduced
-        if (!wait_members(a, mine, cnt, MI355_SIG_RSDONE, true)) ok_all = 0;
-        __syncthreads();
-        if (!ok_all) goto fail;
+            // ---- every shard is reduced
+            if (!wait_members(a, mine, cnt, MI355_SIG_RSDONE, true)) ok_all = 0;
+            __syncthreads();
+            if (!ok_all) goto fail;
 
-        // ---- gather the other shards: one grid-stride loop over all of them
-        const uint64_t shard_v = a.shard / V;  // a.shard is a multiple of V
-        const uint64_t total_v = shard_v * (uint64_t)a.nmembers;
-        bool tail_plain = false;
-        for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < total_v;
-             g += (uint64_t)gridDim.x * kBlock) {
-            const int j = (int)(g / shard_v);
-            if (j == a.me) continue;
-            const uint64_t e0 = (uint64_t)j * a.shard + (g - (uint64_t)j * shard_v) * V;
-            if (e0 >= a.n) continue;
-            if (e0 + V <= a.n) {
-                const u32x4 v = *(const u32x4 *)((const char *)a.dst[j] + e0 * sizeof(T));
-                st16_sys((u32x4 *)((char *)a.dst[a.me] + e0 * sizeof(T)), v);
-            } else {
-                for (uint64_t e = e0; e < a.n; ++e) ((T *)a.dst[a.me])[e] = ((const T *)a.dst[j])[e];
-                tail_plain = true;
+            // ---- gather the other shards: one grid-stride loop over all of them
+            const uint64_t shard_v = a.shard / V;  // a.shard is a multiple of V
+            const uint64_t total_v = shard_v * (uint64_t)a.nmembers;
+            for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < total_v;
+                 g += (uint64_t)gridDim.x * kBlock) {
+                const int j = (int)(g / shard_v);
+                if (j == a.me) continue;
+                const uint64_t e0 = (uint64_t)j * a.shard + (g - (uint64_t)j * shard_v) * V;
+                if (e0 >= a.n) continue;
+                if (e0 + V <= a.n) {
+                    const u32x4 v = *(const u32x4 *)((const char *)a.dst[j] + e0 * sizeof(T));
+                    st16_sys((u32x4 *)((char *)a.dst[a.me] + e0 * sizeof(T)), v);
+                } else {
+                    for (uint64_t e = e0; e < a.n; ++e) ((T *)a.dst[a.me])[e] = ((const T *)a.dst[j])[e];
+                    tail_plain = true;
+                }
             }
         }
+        // one-shot: AGDONE below means "this PE has finished reading the
+        // members' sources" -- every member waits for all of them before it
+        // returns, as after the gather
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (__syncthreads_or(tail_plain) && threadIdx.x == 0)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the element tail went through L2
@@ -374,8 +382,10 @@ extern "C" int mi355_fused_allreduce(const MI355FusedArgs *a, void *stream) {
             (((uintptr_t)a->src[i] | (uintptr_t)a->dst[i]) & 15) != 0 || a->pe[i] < 0 ||
             a->pe[i] >= MI355_SIG_RSDONE)
             return MI355_E_INVAL;
-    // enough blocks for the larger of the two legs, all of them co-resident
-    const uint64_t vecs = (a->shard * es / 16) * (uint64_t)(a->nmembers - 1);
+    if (a->oneshot && a->src[a->me] == a->dst[a->me]) return MI355_E_INVAL;  // it overwrites dst while peers read src
+    // enough blocks for the larger of the two legs (one-shot: the whole
+    // array), all of them co-resident
+    const uint64_t vecs = a->oneshot ? (a->n * es + 15) / 16 : (a->shard * es / 16) * (uint64_t)(a->nmembers - 1);
     uint64_t grid = (vecs + kBlock - 1) / kBlock;
     if (grid < 1) grid = 1;
     if (grid > MI355_FUSED_MAX_BLOCKS) grid = MI355_FUSED_MAX_BLOCKS;

@@ -308,8 +308,9 @@ static int fused_eligible (size_t es, size_t dst_off, size_t src_off, size_t n, 
 static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
                          const struct aset *s, const void *host_src, void *host_dst)
 {
-    SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: fused one-launch P2P (%zu elements, %d members)%s", n, s->size,
-                  host_src != NULL ? ", staging host buffers in-kernel" : "");
+    SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: fused one-launch P2P, %s (%zu elements, %d members)%s",
+                  n * es <= shmemi.oneshot_max && dst_off != src_off ? "one-shot" : "reduce-scatter + all-gather", n,
+                  s->size, host_src != NULL ? ", staging host buffers in-kernel" : "");
     MI355FusedArgs a;
     memset (&a, 0, sizeof a);
     a.op = op;
@@ -331,6 +332,7 @@ static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t sr
     a.timeout_ticks = (unsigned long long) (shmemi.barrier_timeout * 1e8);
     a.host_src = host_src;
     a.host_dst = host_dst;
+    a.oneshot = n * es <= shmemi.oneshot_max && dst_off != src_off;
     const int rc = mi355_fused_allreduce (&a, shmemi.stream);
     if (rc != 0)
         shmemi_fatal ("fused reduction launch failed (op %d, dtype %d, %d PEs, %zu elements): %d", op, dtype,
@@ -745,6 +747,7 @@ static void reduce_on_stream (int op, int dtype, const char *fn, void *target, c
                 a.src[i] = shmemi_peer_ptr (a.pe[i], src_off);
                 a.dst[i] = shmemi_peer_ptr (a.pe[i], dst_off);
             }
+            a.oneshot = n * es <= shmemi.oneshot_max && dst_off != src_off;
             const int rc = mi355_fused_allreduce (&a, st);
             if (rc != 0)
                 shmemi_fatal ("%s: fused reduction launch failed: %d", fn, rc);

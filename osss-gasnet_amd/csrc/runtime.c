@@ -819,6 +819,7 @@ void pshmem_init (void)
     signal_init ();
     sigmem_init ();
     shmemi.fused_max = env_size ("SHMEM_FUSED_MAX_BYTES", (size_t) 1 << 20);
+    shmemi.oneshot_max = env_size ("SHMEM_ONESHOT_MAX_BYTES", (size_t) 64 << 10);
 
     if (shmemi.npes > 1) {
         bootstrap_attach ();

@@ -99,6 +99,7 @@ struct shmemi_state {
     unsigned long long *sigmem;
     unsigned long long **peer_sig;  /* [npes] */
     size_t fused_max;           /* SHMEM_FUSED_MAX_BYTES: largest message on the fused path */
+    size_t oneshot_max;         /* SHMEM_ONESHOT_MAX_BYTES: largest fused message folded one-shot */
     int sig_broken;             /* peers' signal-region stores failed the init self-test */
 
     /* completion signal: host-coherent word the last block of a kernel writes */

@@ -129,6 +129,7 @@ void shmemi_trace_show_info (void)
         {"SHMEM_SYMMETRIC_HEAP_KIND", "\"device\": shmem_malloc returns device memory"},
         {"SHMEM_REDUCE_ALGORITHM", "auto | p2p | exact | rccl"},
         {"SHMEM_FUSED_MAX_BYTES", "largest message for the one-launch fused reduction (default 1M)"},
+        {"SHMEM_ONESHOT_MAX_BYTES", "largest fused message folded one-shot, not reduce-scatter + all-gather (default 64K)"},
         {"SHMEM_BARRIER_TIMEOUT", "seconds before a barrier wait aborts the job (default 600)"},
         {"SHMEM_ENTRY_SYNC", "1: every call starts with hipDeviceSynchronize"},
         {"SHMEM_PEER_ACQUIRE", "1/0: system-scope L2 acquire before reading peers' buffers (default: on if a peer is on another GPU)"},

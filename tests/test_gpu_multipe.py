@@ -93,14 +93,18 @@ SOME = [("sum", "double"), ("sum", "float"), ("xor", "int"), ("and", "longlong")
         ("min", "short"), ("prod", "complexd"), ("sum", "longdouble")]
 
 
-@pytest.mark.parametrize("fused_max", ["1M", "0"], ids=["fused", "multi-launch"])
-def test_four_pes_all_44_pairs_p2p_and_exact(tmp_path, fused_max):
+@pytest.mark.parametrize("fused_max,oneshot_max", [("1M", "64K"), ("1M", "0"), ("0", "0")],
+                         ids=["fused-oneshot", "fused-twoshot", "multi-launch"])
+def test_four_pes_all_44_pairs_p2p_and_exact(tmp_path, fused_max, oneshot_max):
     """Every pair on 4 PEs, through the one-launch fused kernel (messages up to
-    1 MiB) and through the multi-launch shard schedule (fused path disabled)."""
+    1 MiB; one-shot fold up to 64 KiB, reduce-scatter + all-gather above) and
+    through the multi-launch shard schedule (fused path disabled)."""
     cases = []
     cases += make_cases(oracle.PAIRS, 1000, [[0, 0, 4]], "dev", "p2p", 0)
     cases += make_cases(oracle.PAIRS, 257, [[0, 0, 4]], "dev", "exact", 100)
-    results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_FUSED_MAX_BYTES": fused_max})
+    cases += make_cases(oracle.PAIRS, 1000, [[0, 0, 4]], "inplace", "p2p", 200)  # in place: never one-shot
+    results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_FUSED_MAX_BYTES": fused_max,
+                                                     "SHMEM_ONESHOT_MAX_BYTES": oneshot_max})
     check(results, cases)
 
 
