@@ -174,17 +174,20 @@ __global__ __launch_bounds__(kBlock) void combine_scalar(CombineParams p) {
     signal_done(p.sig, true);
 }
 
-// Byte copy of up to kMaxSeg segments in one launch; blockIdx.y = segment.
+// Byte copy of up to NS segments in one launch; blockIdx.y = segment. NS = 1
+// (the 1-PE identity, the bench's call) keeps the kernel arguments at 48
+// bytes instead of 1.5 KiB for the 64-segment form (the all-gather leg).
 constexpr int kMaxSeg = 64;
+template <int NS>
 struct SegParams {
-    void *dst[kMaxSeg];
-    const void *src[kMaxSeg];
-    uint64_t nbytes[kMaxSeg];
+    void *dst[NS];
+    const void *src[NS];
+    uint64_t nbytes[NS];
     Signal sig;
 };
 
-template <int UNROLL>
-__global__ __launch_bounds__(kBlock) void copy_segments(SegParams p) {
+template <int UNROLL, int NS>
+__global__ __launch_bounds__(kBlock) void copy_segments(SegParams<NS> p) {
     const int sg = blockIdx.y;
     const uint64_t nb = p.nbytes[sg];
     const char *src = (const char *)p.src[sg];
@@ -488,7 +491,7 @@ static int copy_segments_impl(void *const *dsts, const void *const *srcs, const 
         return 0;
     }
     if (dsts == nullptr || srcs == nullptr || nbytes == nullptr) return MI355_E_INVAL;
-    SegParams p{};
+    SegParams<kMaxSeg> p{};
     uint64_t maxv = 0;
     int used = 0;
     for (int k = 0; k < nseg; ++k) {
@@ -513,7 +516,14 @@ static int copy_segments_impl(void *const *dsts, const void *const *srcs, const 
     // keep total blocks ~ cap when many segments share the chip
     unsigned cap = (unsigned)device_cus();
     if ((uint64_t)gx * used > cap) gx = cap / used > 0 ? cap / used : 1;
-    return launch(copy_segments<U>, dim3(gx, used), (hipStream_t)stream, p);
+    if (used == 1) {
+        SegParams<1> p1{};
+        p1.dst[0] = p.dst[0];
+        p1.src[0] = p.src[0];
+        p1.nbytes[0] = p.nbytes[0];
+        return launch(copy_segments<U, 1>, dim3(gx, 1), (hipStream_t)stream, p1);
+    }
+    return launch(copy_segments<U, kMaxSeg>, dim3(gx, used), (hipStream_t)stream, p);
 }
 
 // System-scope acquire on every XCD of this GPU (`buffer_inv sc0 sc1`): drops

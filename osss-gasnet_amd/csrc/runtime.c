@@ -383,28 +383,36 @@ void shmemi_wait_signal (void)
 }
 
 /* Wait until the host-coherent flag carries `want` (in its low 31 bits) and
- * return it. A kernel that faults never signals: the stream is polled now and
- * then so its error surfaces. */
+ * return it. A kernel that faults never signals: after the first millisecond
+ * the stream is polled every millisecond so its error surfaces. (Polling it
+ * from the start cost up to a microsecond per call: hipStreamQuery takes
+ * runtime locks and could run just as the flag arrived.) */
 unsigned shmemi_wait_flag (unsigned want)
 {
     unsigned spins = 0;
-    double t0 = 0.0;
+    double t0 = 0.0, next_query = 0.0;
     unsigned v;
     while (((v = __atomic_load_n (shmemi.sig_flag, __ATOMIC_ACQUIRE)) & 0x7fffffffu) != want) {
-        if ((++spins & 4095u) == 0) {
-            hipError_t e = hipStreamQuery (shmemi.stream);
-            if (e != hipSuccess && e != hipErrorNotReady)
-                shmemi_fatal ("kernel failed: %s", hipGetErrorString (e));
-            if (e == hipSuccess && (__atomic_load_n (shmemi.sig_flag, __ATOMIC_ACQUIRE) & 0x7fffffffu) != want)
-                shmemi_fatal ("stream drained but the completion signal %u never arrived", want);
-            if (t0 == 0.0)
-                t0 = now_s ();
-            else if (now_s () - t0 > shmemi.barrier_timeout)
-                shmemi_fatal ("kernel did not complete within %.0f s", shmemi.barrier_timeout);
-            check_abort ();
-        } else {
-            __builtin_ia32_pause ();
+        __builtin_ia32_pause ();
+        if ((++spins & 255u) != 0)
+            continue;
+        const double t = now_s (); /* vDSO clock: tens of ns */
+        if (t0 == 0.0) {
+            t0 = t;
+            next_query = t + 1e-3;
+            continue;
         }
+        if (t < next_query)
+            continue;
+        next_query = t + 1e-3;
+        hipError_t e = hipStreamQuery (shmemi.stream);
+        if (e != hipSuccess && e != hipErrorNotReady)
+            shmemi_fatal ("kernel failed: %s", hipGetErrorString (e));
+        if (e == hipSuccess && (__atomic_load_n (shmemi.sig_flag, __ATOMIC_ACQUIRE) & 0x7fffffffu) != want)
+            shmemi_fatal ("stream drained but the completion signal %u never arrived", want);
+        if (t - t0 > shmemi.barrier_timeout)
+            shmemi_fatal ("kernel did not complete within %.0f s", shmemi.barrier_timeout);
+        check_abort ();
     }
     return v;
 }
