@@ -82,6 +82,7 @@ struct CombineParams {
     const void *src[kMaxSrc];
     uint64_t nvec;   // vector kernel: whole 16-byte vectors; scalar kernel: elements
     uint32_t tail;   // vector kernel: elements after nvec*V (< V)
+    uint32_t head;   // vector kernel: elements just BEFORE dst/src (pointers advanced to 16-byte alignment)
     Signal sig;
 };
 
@@ -149,7 +150,15 @@ __global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
         for (int k = 1; k < NSRC; ++k) acc = apply<OP>(acc, ((const T *)p.src[k])[i]);
         ((T *)p.dst)[i] = acc;
     }
-    signal_done(p.sig, tail_block);
+    const bool head_block = V > 1 && p.head != 0 && blockIdx.x == 0;
+    if (head_block && threadIdx.x < p.head) {
+        const int64_t i = (int64_t)threadIdx.x - (int64_t)p.head;
+        T acc = ((const T *)p.src[0])[i];
+#pragma unroll
+        for (int k = 1; k < NSRC; ++k) acc = apply<OP>(acc, ((const T *)p.src[k])[i]);
+        ((T *)p.dst)[i] = acc;
+    }
+    signal_done(p.sig, tail_block || head_block);
 }
 
 // Scalar path for pointers that are not 16-byte aligned (user offsets into
@@ -192,12 +201,22 @@ __global__ __launch_bounds__(kBlock) void copy_segments(SegParams<NS> p) {
     const uint64_t nb = p.nbytes[sg];
     const char *src = (const char *)p.src[sg];
     char *dst = (char *)p.dst[sg];
-    const bool aligned = ((((uintptr_t)src) | ((uintptr_t)dst)) & 15) == 0;
-    uint64_t done = 0;
-    if (aligned) {
-        const u32x4 *s = (const u32x4 *)src;
-        u32x4 *d = (u32x4 *)dst;
-        const uint64_t nvec = nb / 16;
+    // 16-byte vectors where both ends are aligned: pointers with the same
+    // misalignment (a user offset into two arrays) peel a head so that both
+    // start on a 128-byte line (or at least on 16 bytes); different
+    // misalignments take the narrow path below
+    const unsigned mis128 = (unsigned)((uintptr_t)dst & 127);
+    const unsigned mis = mis128 & 15u;
+    const bool coaligned = mis == (unsigned)((uintptr_t)src & 15);
+    uint64_t head = !coaligned ? nb
+                    : mis128 == (unsigned)((uintptr_t)src & 127) ? (128u - mis128) & 127u
+                                                                  : (16u - mis) & 15u;
+    if (head > nb) head = nb;
+    uint64_t vec_end = head;  // bytes [head, vec_end) go as vectors
+    if (coaligned) {
+        const u32x4 *s = (const u32x4 *)(src + head);
+        u32x4 *d = (u32x4 *)(dst + head);
+        const uint64_t nvec = (nb - head) / 16;
         const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
         // software-pipelined: the loads of pass k+1 are in flight while the
         // stores of pass k issue (tools/copy_variants.hip: 78.3 vs 80.0 us for
@@ -226,13 +245,39 @@ __global__ __launch_bounds__(kBlock) void copy_segments(SegParams<NS> p) {
             for (int u = 0; u < UNROLL; ++u) x[u] = y[u];
             base = next;
         }
-        done = nvec * 16;
+        vec_end = head + nvec * 16;
     }
     bool plain = false;
-    for (uint64_t i = done + (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nb;
-         i += (uint64_t)gridDim.x * kBlock) {
-        dst[i] = src[i];
-        plain = true;
+    if (!coaligned) {
+        // narrow path: the widest unit both ends are aligned to (8, 4, 2 or 1 bytes)
+        const unsigned both = (unsigned)(((uintptr_t)dst | (uintptr_t)src) & 7);
+        const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+        const uint64_t t0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+        uint64_t done = 0;
+        if ((both & 7) == 0) {
+            const uint64_t nw = nb / 8;
+            for (uint64_t i = t0; i < nw; i += stride) ((uint64_t *)dst)[i] = ((const uint64_t *)src)[i];
+            done = nw * 8;
+        } else if ((both & 3) == 0) {
+            const uint64_t nw = nb / 4;
+            for (uint64_t i = t0; i < nw; i += stride) ((uint32_t *)dst)[i] = ((const uint32_t *)src)[i];
+            done = nw * 4;
+        } else if ((both & 1) == 0) {
+            const uint64_t nw = nb / 2;
+            for (uint64_t i = t0; i < nw; i += stride) ((uint16_t *)dst)[i] = ((const uint16_t *)src)[i];
+            done = nw * 2;
+        }
+        for (uint64_t i = done + t0; i < nb; i += stride) dst[i] = src[i];
+        plain = nb > 0;
+    } else {
+        // the bytes outside the vector part: [0, head) and [vec_end, nb)
+        const uint64_t nrest = head + (nb - vec_end);
+        for (uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x; r < nrest;
+             r += (uint64_t)gridDim.x * kBlock) {
+            const uint64_t i = r < head ? r : vec_end + (r - head);
+            dst[i] = src[i];
+            plain = true;
+        }
     }
     signal_done(p.sig, __syncthreads_or(plain));
 }
@@ -336,6 +381,27 @@ int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, b
         orbits |= (uintptr_t)srcs[k];
     }
     constexpr int V = 16 / sizeof(T);
+    // every pointer equally misaligned by whole elements (a user offset into
+    // the arrays): the first `head` elements are folded element-wise and the
+    // rest as 16-byte vectors from the advanced, aligned pointers
+    if ((orbits & 15) != 0 && V > 1) {
+        // all equally misaligned within a 128-byte line: peel to the line
+        // (whole-line accesses); else within 16 bytes: peel to 16
+        uintptr_t mis = (uintptr_t)dst & 127;
+        bool line = true;
+        for (int k = 0; k < NSRC; ++k) line = line && ((uintptr_t)srcs[k] & 127) == mis;
+        if (!line) mis &= 15;
+        bool same = mis % sizeof(T) == 0;
+        for (int k = 0; k < NSRC; ++k) same = same && ((uintptr_t)srcs[k] & (line ? 127 : 15)) == mis;
+        const size_t head = ((line ? 128 : 16) - mis) / sizeof(T);
+        if (same && n > head) {
+            p.head = (uint32_t)head;
+            p.dst = (char *)dst + head * sizeof(T);
+            for (int k = 0; k < NSRC; ++k) p.src[k] = (const char *)srcs[k] + head * sizeof(T);
+            n -= head;
+            orbits = 0;
+        }
+    }
     if ((orbits & 15) == 0) {
         using S = Shape<NSRC, T>;
         p.nvec = n / V;

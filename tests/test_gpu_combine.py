@@ -93,8 +93,9 @@ def test_combine_sizes_and_tails(shm, dev, n, dtype):
     assert_match(got, oracle.reduce_pe("sum", dtype, srcs, 0), "sum", dtype)
 
 
-@pytest.mark.parametrize("off", [1, 3])
-@pytest.mark.parametrize("op,dtype", [("sum", "double"), ("and", "short"), ("min", "float"), ("prod", "int")])
+@pytest.mark.parametrize("off", [1, 3, 5])
+@pytest.mark.parametrize("op,dtype", [("sum", "double"), ("and", "short"), ("min", "float"), ("prod", "int"),
+                                      ("xor", "longlong"), ("sum", "complexf")])
 def test_combine_unaligned_pointers(shm, dev, op, dtype, off):
     import gen_golden
     rng = np.random.default_rng(off)
@@ -173,17 +174,19 @@ def test_copy_segments_sizes_offsets_and_many_segments(shm, dev):
     rng = np.random.default_rng(17)
     sizes = [1, 15, 16, 17, 255, 4096, 8000, 16383, 16384, 16400, 65536 + 48, 1 << 20, (1 << 22) + 16]
     for nb in sizes:
-        for off in (0, 16, 3):
-            x = rng.integers(0, 256, nb + off, dtype=np.uint8)
+        # (target offset, source offset): aligned, equally misaligned (head
+        # peeled, then vectors), differently misaligned (byte copy)
+        for doff, soff in ((0, 0), (16, 16), (3, 3), (8, 8), (3, 5)):
+            x = rng.integers(0, 256, nb + soff, dtype=np.uint8)
             s = dev.upload(x)
-            d = dev.empty(nb + off)
-            dsts = (ctypes.c_void_p * 1)(d + off)
-            srcs = (ctypes.c_void_p * 1)(s + off)
+            d = dev.empty(nb + doff)
+            dsts = (ctypes.c_void_p * 1)(d + doff)
+            srcs = (ctypes.c_void_p * 1)(s + soff)
             nbs = (ctypes.c_size_t * 1)(nb)
             assert shm.lib.mi355_copy_segments(dsts, srcs, nbs, 1, None) == 0
             shm.sync()
-            got = shm.get(d + off, nb, np.uint8)
-            assert (got == x[off:]).all(), (nb, off, int(np.argmax(got != x[off:])))
+            got = shm.get(d + doff, nb, np.uint8)
+            assert (got == x[soff:]).all(), (nb, doff, soff, int(np.argmax(got != x[soff:])))
     for k, seg in ((7, 33333), (64, 4112)):
         xs = [rng.integers(0, 256, seg, dtype=np.uint8) for _ in range(k)]
         sp = [dev.upload(x) for x in xs]
@@ -195,3 +198,18 @@ def test_copy_segments_sizes_offsets_and_many_segments(shm, dev):
         shm.sync()
         for i in range(k):
             assert (shm.get(dp[i], seg, np.uint8) == xs[i]).all(), (k, i)
+
+
+def test_combine_target_and_sources_misaligned_differently(shm, dev):
+    """Target one element off, sources three off: no common alignment, so the
+    element-wise kernel runs; results as the oracle's."""
+    import ctypes
+    import gen_golden
+    n, es = 3001, 8
+    rng = np.random.default_rng(77)
+    srcs = [gen_golden.values(rng, "sum", "double", n) for _ in range(3)]
+    ptrs = [dev.upload(np.concatenate([np.zeros(3), s])) + 3 * es for s in srcs]
+    out = dev.empty((n + 1) * es) + es
+    assert shm.combine("sum", "double", out, ptrs, n) == 0
+    shm.sync()
+    assert_match(shm.get(out, n, "double"), oracle.reduce_pe("sum", "double", srcs, 0), "sum", "double")
