@@ -522,30 +522,41 @@ static void staged (int op, int dtype, const char *fn, void *target, const void 
     SHMEMI_HIP (hipStreamSynchronize (shmemi.stream_in));
 }
 
-/* Small reductions of page-locked host arrays (shmem_malloc's default heap)
- * in ONE launch: the kernels read the host source and write the host target
- * over PCIe themselves instead of separate H2D/D2H copies around the
- * reduction (~30 -> ~11 us at 1 PE, ~58 -> ~19 us at 2 PEs for 8 B - 8 KiB).
- * Up to 1 MiB (and the fused path's own limit, SHMEM_FUSED_MAX_BYTES).
- * 1 PE: one copy kernel host -> host. More PEs: the fused kernel with
- * in-kernel staging through this PE's scratch A/B -- the same scratch
- * offsets and the same single collective as staged()'s one-chunk case, so a
- * PE whose buffers are not page-locked (staged() instead) still matches it.
- * Returns 0 when it does not apply. */
-#define SHMEMI_SMALL_HOST_MAX ((size_t) 1 << 20)
-static int small_host (int op, int dtype, void *target, const void *source, size_t n, int overlap,
-                       const struct aset *s)
+/* Buffers outside the device symmetric heap that this GPU can still reach:
+ * plain device memory (hipMalloc, e.g. a framework's tensors) and page-locked
+ * host arrays (shmem_malloc's default heap). Instead of separate H2D/D2D/D2H
+ * copies around the reduction:
+ *   1 PE          one copy kernel straight from source to target (device to
+ *                 device at any size; with a host side up to 1 MiB -- above,
+ *                 the DMA double buffering of staged() is faster);
+ *   N PEs, small  the fused kernel stages this PE's source into its scratch A
+ *                 and the result out of scratch B itself (one launch) -- the
+ *                 same scratch offsets and the same single collective as
+ *                 staged()'s one-chunk case, so PEs that take staged() (pageable
+ *                 host arrays) still meet it.
+ * Host arrays: ~30 -> ~11 us at 1 PE and ~58 -> ~19 us at 2 PEs for 8 B -
+ * 8 KiB. Returns 0 when it does not apply. */
+#define SHMEMI_SMALL_LOCAL_MAX ((size_t) 1 << 20)
+static const void *reachable (const void *p, size_t nbytes, int kind)
+{
+    return kind == PK_HOST ? shmemi_host_dev_ptr (p, nbytes) : p;
+}
+
+static int local_direct (int op, int dtype, void *target, const void *source, size_t n, int overlap, int kt,
+                         int ks, const struct aset *s)
 {
     const size_t es = mi355_dtype_size (dtype), nbytes = n * es;
-    const size_t half = shmemi.scratch_chunk / 2 / SHMEMI_ALIGN * SHMEMI_ALIGN;
-    if (nbytes > SHMEMI_SMALL_HOST_MAX || nbytes > half || (overlap && target != source))
+    if (overlap && target != source)
         return 0;
-    void *ht = shmemi_host_dev_ptr (target, nbytes);
-    const void *hs = shmemi_host_dev_ptr (source, nbytes);
+    void *ht = (void *) reachable (target, nbytes, kt);
+    const void *hs = reachable (source, nbytes, ks);
     if (ht == NULL || hs == NULL)
         return 0;
+    const int any_host = kt == PK_HOST || ks == PK_HOST;
     if (s->size == 1) {
-        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: 1-PE identity, one copy kernel host -> host (%zu bytes)",
+        if (any_host && nbytes > SHMEMI_SMALL_LOCAL_MAX)
+            return 0;
+        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: 1-PE identity, one copy kernel source -> target (%zu bytes)",
                       nbytes);
         if (target != source) {
             void *d = ht;
@@ -554,6 +565,9 @@ static int small_host (int op, int dtype, void *target, const void *source, size
         }
         return 1;
     }
+    const size_t half = shmemi.scratch_chunk / 2 / SHMEMI_ALIGN * SHMEMI_ALIGN;
+    if (nbytes > SHMEMI_SMALL_LOCAL_MAX || nbytes > half)
+        return 0;
     const size_t a_off = shmemi.scratch_off, b_off = shmemi.scratch_off + shmemi.scratch_chunk;
     if (!fused_eligible (es, b_off, a_off, n, s))
         return 0;
@@ -627,7 +641,7 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
         return;
     }
 
-    if (kt == PK_HOST && ks == PK_HOST && !use_rccl && small_host (op, dtype, target, source, n, overlap, &s))
+    if (!use_rccl && local_direct (op, dtype, target, source, n, overlap, kt, ks, &s))
         return;
     SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "staged through the scratch buffers (%s)", use_rccl ? "RCCL" : "P2P");
     staged (op, dtype, fn, target, source, n, &s, ks, kt, use_rccl);

@@ -201,6 +201,11 @@ def main():
                for c in spec["cases"])
     da, db = shm.malloc_device(maxb), shm.malloc_device(maxb)
     ha, hb = shm.malloc(maxb), shm.malloc(maxb)
+    hip = ctypes.CDLL("libamdhip64.so")
+    pa, pb = ctypes.c_void_p(), ctypes.c_void_p()
+    assert hip.hipMalloc(ctypes.byref(pa), ctypes.c_size_t(maxb)) == 0
+    assert hip.hipMalloc(ctypes.byref(pb), ctypes.c_size_t(maxb)) == 0
+    priv_a, priv_b = pa.value, pb.value
     results = {}
     for c in spec["cases"]:
         if c.get("kind") == "config":
@@ -232,6 +237,14 @@ def main():
             src, dst = da + 5 * es, da
         elif mode == "host":
             src, dst = ha, hb
+        elif mode in ("devother", "devother_mixed"):
+            # plain hipMalloc buffers (outside the symmetric heap, like a
+            # framework's tensors); _mixed: odd PEs pass page-locked host
+            # arrays instead (both kinds are staged through the scratch)
+            if mode == "devother" or me % 2 == 0:
+                src, dst = priv_a, priv_b
+            else:
+                src, dst = ha, hb
         elif mode == "host_mixed":
             # even PEs: page-locked shmem_malloc arrays (one-launch in-kernel
             # staging for small n); odd PEs: plain numpy arrays (staged copies)
@@ -262,6 +275,8 @@ def main():
             results[str(c["id"])] = out
         else:
             results[str(c["id"])] = shm.get(dst, n, dtype) if n else np.zeros(0, dtype=shmem_reduce.NP[dtype])
+    hip.hipFree(pa)
+    hip.hipFree(pb)
     shm.free(hb)
     shm.free(ha)
     shm.free_device(db)

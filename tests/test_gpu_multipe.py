@@ -234,6 +234,22 @@ def test_small_host_arrays_one_launch_and_mixed(tmp_path):
     check(results, cases)
 
 
+def test_non_symmetric_device_buffers(tmp_path):
+    """Plain hipMalloc buffers (a framework's tensors): small messages go
+    through the fused kernel staging them itself, larger ones through the
+    scratch staging path; odd PEs passing page-locked host arrays in the same
+    calls (_mixed) must meet them."""
+    cases = []
+    cid = 0
+    for mode in ("devother", "devother_mixed"):
+        for n in (1, 515, 8192, 100000, 300000):
+            cases += make_cases([("sum", "double"), ("min", "int"), ("and", "longlong")], n, [[0, 0, 4]], mode,
+                                "p2p", cid)
+            cid += 100
+    results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_DEVICE_SCRATCH_SIZE": "3M"})
+    check(results, cases)
+
+
 def test_signal_region_mapping_failure_falls_back(tmp_path):
     """One PE cannot map the peers' signal regions (SHMEM_TEST_IPC_FAIL=sig
     on PE 1): init must not abort; every PE agrees to run without device-side
