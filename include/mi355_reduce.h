@@ -154,6 +154,22 @@ typedef struct MI355FusedArgs {
  * run one at a time, in the same order on every member. */
 int mi355_fused_allreduce (const MI355FusedArgs *args, void *stream);
 
+/* One-launch pull collective (small broadcast / fcollect): after every
+ * member has arrived (its sources are ready), each member copies nseg byte
+ * ranges -- typically out of peers' mapped sources -- into its own device
+ * memory; the members then exchange "done reading" and the call completes
+ * (m.host_flag / m.epoch as for mi355_fused_allreduce). m.op/dtype/n/shard/
+ * src/dst are unused. */
+#define MI355_PULL_MAX_SEGS 64
+typedef struct MI355PullArgs {
+    MI355FusedArgs m;
+    int nseg;
+    void *dst[MI355_PULL_MAX_SEGS];
+    const void *src[MI355_PULL_MAX_SEGS];
+    unsigned long long nbytes[MI355_PULL_MAX_SEGS];
+} MI355PullArgs;
+int mi355_fused_pull (const MI355PullArgs *args, void *stream);
+
 /* Device-side barrier over the members (one 64-lane block): ordered on
  * `stream` after the work queued before it, and the work queued after it
  * runs once every member has reached its matching barrier. Uses

@@ -267,6 +267,49 @@ static void collective_exit (const struct cset *s, int dev)
         shmemi_barrier_set (s->start, s->stride, s->size);
 }
 
+/* Small broadcast / fcollect in ONE launch (mi355_fused_pull): arrive, pull
+ * this PE's segments, "done reading" -- instead of device barrier, copy
+ * kernel and device barrier. The choice depends on the call's arguments only
+ * (every member must make it alike); a member whose target the kernel cannot
+ * write (pageable host memory) pulls into its scratch C and copies out. */
+static int fused_pull_ok (const struct cset *s, size_t total)
+{
+    return s->size >= 2 && shmemi.fused_max != 0 && total <= shmemi.fused_max &&
+           total <= shmemi.scratch_chunk && shmemi_dev_barrier_ok (s->start, s->stride, s->size);
+}
+
+/* segments: byte offsets into this PE's target of `total` bytes */
+static void fused_pull (const char *fn, const struct cset *s, void *target, size_t total, const size_t *toff,
+                        const void *const *srcs, const size_t *nb, int k)
+{
+    char *t = NULL;
+    if (total != 0) {
+        t = is_device_ptr (target) ? (char *) target : (char *) shmemi_host_dev_ptr (target, total);
+        if (t == NULL)
+            t = shmemi.heap + shmemi.scratch_off + 2 * shmemi.scratch_chunk; /* scratch C, copied out below */
+    }
+    MI355PullArgs p;
+    memset (&p, 0, sizeof p);
+    shmemi_member_args (&p.m, s->start, s->stride, s->size, s->me);
+    p.nseg = k;
+    for (int i = 0; i < k; ++i) {
+        p.dst[i] = t + toff[i];
+        p.src[i] = srcs[i];
+        p.nbytes[i] = nb[i];
+    }
+    p.m.host_flag = shmemi.sig_flag;
+    p.m.epoch = shmemi_next_epoch ();
+    shmemi_order_after_caller (0); /* SHMEM_ENTRY_SYNC */
+    const int rc = mi355_fused_pull (&p, shmemi.stream);
+    if (rc != 0)
+        shmemi_fatal ("%s: fused pull launch failed: %d", fn, rc);
+    if (shmemi_wait_flag (p.m.epoch) != p.m.epoch)
+        shmemi_fatal ("%s: timed out waiting for the other PEs of the active set", fn);
+    if (t != NULL && t != (char *) target && t == shmemi.heap + shmemi.scratch_off + 2 * shmemi.scratch_chunk)
+        for (int i = 0; i < k; ++i)
+            blocking_copy ((char *) target + toff[i], t + toff[i], nb[i]);
+}
+
 static void broadcast_bytes (const char *fn, void *target, const void *source, size_t nbytes, int PE_root,
                              int PE_start, int logPE_stride, int PE_size)
 {
@@ -274,6 +317,16 @@ static void broadcast_bytes (const char *fn, void *target, const void *source, s
     if (PE_root < 0 || PE_root >= PE_size)
         shmemi_fatal ("%s: PE_root %d outside the active set of %d PEs", fn, PE_root, PE_size);
     const int root = PE_start + PE_root * s.stride;
+    if (nbytes != 0 && !shmemi_in_device_heap (source, nbytes))
+        shmemi_fatal ("%s: source %p is not in the device symmetric heap (allocate it with "
+                      "shmemx_malloc_device)", fn, source);
+    if (fused_pull_ok (&s, nbytes)) {
+        SHMEMI_TRACE (SHMEMI_LOG_BROADCAST, "%s: %zu bytes from PE %d, one fused launch", fn, nbytes, root);
+        const void *src = nbytes != 0 ? shmemi_peer_ptr (root, shmemi_heap_offset (source)) : NULL;
+        const size_t toff = 0;
+        fused_pull (fn, &s, target, nbytes, &toff, &src, &nbytes, shmemi.mype != root && nbytes != 0 ? 1 : 0);
+        return;
+    }
     const int dev = collective_entry (fn, source, nbytes, &s, 1);
     if (shmemi.mype != root && nbytes != 0) {
         void *d = target;
@@ -328,6 +381,21 @@ static void fcollect_bytes (const char *fn, void *target, const void *source, si
                             int logPE_stride, int PE_size)
 {
     struct cset s = make_set (fn, PE_start, logPE_stride, PE_size);
+    if (s.size <= MI355_PULL_MAX_SEGS && nbytes != 0 && fused_pull_ok (&s, nbytes * (size_t) s.size)) {
+        if (!shmemi_in_device_heap (source, nbytes))
+            shmemi_fatal ("%s: source %p is not in the device symmetric heap (allocate it with "
+                          "shmemx_malloc_device)", fn, source);
+        size_t toff[MI355_PULL_MAX_SEGS], nb[MI355_PULL_MAX_SEGS];
+        const void *srcs[MI355_PULL_MAX_SEGS];
+        for (int i = 0; i < s.size; ++i) {
+            toff[i] = (size_t) i * nbytes;
+            srcs[i] = shmemi_peer_ptr (s.start + i * s.stride, shmemi_heap_offset (source));
+            nb[i] = nbytes;
+        }
+        SHMEMI_TRACE (SHMEMI_LOG_COLLECT, "%s: %d x %zu bytes, one fused launch", fn, s.size, nbytes);
+        fused_pull (fn, &s, target, nbytes * (size_t) s.size, toff, srcs, nb, s.size);
+        return;
+    }
     const int dev = collective_entry (fn, source, nbytes, &s, 1);
     size_t *counts = (size_t *) malloc (sizeof (size_t) * (size_t) s.size);
     if (counts == NULL)

@@ -289,6 +289,32 @@ fail:
     finish(a, mine, cnt, false);
 }
 
+// One-launch pull collective: arrive, copy this member's segments (sources
+// are peers' mapped buffers, read after the acquire in wait_members), then
+// "done reading" (AGDONE) from every member before the call completes.
+__global__ __launch_bounds__(kBlock) void fused_pull(MI355PullArgs p) {
+    const MI355FusedArgs &a = p.m;
+    unsigned long long *mine = a.sig[a.me];
+    __shared__ int ok_all;
+    __shared__ unsigned long long cnt[MI355_FUSED_MAX_MEMBERS];
+    if (threadIdx.x == 0) ok_all = 1;
+    load_counts(a, mine, cnt);
+    if (blockIdx.x == 0 && threadIdx.x < a.nmembers && threadIdx.x != a.me)
+        st_sys_u64(a.sig[threadIdx.x] + MI355_SIG_ARRIVE + a.pe[a.me], cnt[threadIdx.x]);
+    __syncthreads();
+    if (!wait_members(a, mine, cnt, MI355_SIG_ARRIVE, false)) ok_all = 0;
+    __syncthreads();
+    if (ok_all)
+        for (int k = 0; k < p.nseg; ++k) block_copy(p.dst[k], p.src[k], p.nbytes[k], blockIdx.x, gridDim.x);
+    if (last_block(mine + MI355_SIG_AG_COUNT)) {
+        publish(a, cnt, MI355_SIG_AGDONE);
+        __syncthreads();
+        if (!wait_members(a, mine, cnt, MI355_SIG_AGDONE, true)) ok_all = 0;
+        __syncthreads();
+        finish(a, mine, cnt, ok_all != 0);
+    }
+}
+
 // Device barrier: one block; lanes of wave 0 handle one member each.
 __global__ __launch_bounds__(64) void device_barrier(MI355FusedArgs a) {
     unsigned long long *mine = a.sig[a.me];
@@ -402,6 +428,26 @@ extern "C" int mi355_fused_allreduce(const MI355FusedArgs *a, void *stream) {
     case MI355_COMPLEXD: return launch_op<cplxd>(*a, (unsigned)grid, st);
     default: return MI355_E_INVAL;
     }
+}
+
+extern "C" int mi355_fused_pull(const MI355PullArgs *p, void *stream) {
+    if (p == nullptr || p->nseg < 0 || p->nseg > MI355_PULL_MAX_SEGS) return MI355_E_INVAL;
+    const MI355FusedArgs *a = &p->m;
+    if (a->nmembers < 2 || a->nmembers > MI355_FUSED_MAX_MEMBERS || a->me < 0 || a->me >= a->nmembers)
+        return MI355_E_INVAL;
+    uint64_t total = 0;
+    for (int k = 0; k < p->nseg; ++k) {
+        if (p->nbytes[k] != 0 && (p->dst[k] == nullptr || p->src[k] == nullptr)) return MI355_E_INVAL;
+        total += p->nbytes[k];
+    }
+    for (int i = 0; i < a->nmembers; ++i)
+        if (a->sig[i] == nullptr || a->pe[i] < 0 || a->pe[i] >= MI355_SIG_RSDONE) return MI355_E_INVAL;
+    uint64_t grid = (total + 16 * kBlock - 1) / (16 * kBlock);
+    if (grid < 1) grid = 1;
+    if (grid > MI355_FUSED_MAX_BLOCKS) grid = MI355_FUSED_MAX_BLOCKS;
+    hipLaunchKernelGGL(fused_pull, dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)stream, *p);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
 }
 
 extern "C" int mi355_device_barrier(const MI355FusedArgs *a, void *stream) {

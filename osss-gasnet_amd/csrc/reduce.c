@@ -143,6 +143,13 @@ static void device_barrier (const MI355FusedArgs *a, hipStream_t st)
         shmemi_fatal ("device barrier launch failed: %d", rc);
 }
 
+/* For coll.c: the member list of an active set on the host channel. */
+void shmemi_member_args (MI355FusedArgs *a, int PE_start, int stride, int PE_size, int me)
+{
+    struct aset s = {PE_start, stride, PE_size, me};
+    member_args (a, &s, SHMEMI_CHAN_HOST);
+}
+
 /* For coll.c: a device barrier over an active set on the library stream
  * (host channel); `last` makes it carry the completion flag and waits. */
 int shmemi_dev_barrier_ok (int PE_start, int stride, int PE_size)

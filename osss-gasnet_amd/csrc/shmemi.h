@@ -136,6 +136,8 @@ void shmemi_peer_acquire (hipStream_t st);
 /* reduce.c: device-flag barrier on the library stream (host channel) */
 int shmemi_dev_barrier_ok (int PE_start, int stride, int PE_size);
 void shmemi_dev_barrier (int PE_start, int stride, int PE_size, int me, int last);
+struct MI355FusedArgs;
+void shmemi_member_args (struct MI355FusedArgs *a, int PE_start, int stride, int PE_size, int me);
 void shmemi_arm_signal (void);
 void shmemi_wait_signal (void);
 unsigned shmemi_next_epoch (void);

@@ -46,9 +46,13 @@ def run_datamove(shm, c, me, da, db, ha, hb, results):
     start, logstride, size = s
     mem = members(*s)
     x = dm_source(c, me)
-    tgt_host = c.get("target") == "host"
-    tgt = hb if tgt_host else db
+    kind_t = c.get("target", "device")
+    if kind_t == "mixed":  # pageable host target on odd PEs, device on even ones
+        kind_t = "pageable" if me % 2 else "device"
+    tgt_host = kind_t in ("host", "pageable")
     cap = c["cap"]
+    pageable = np.empty(cap * 8 + 64, dtype=np.uint8)  # plain malloc'd numpy memory
+    tgt = hb if kind_t == "host" else pageable.ctypes.data + 8 if kind_t == "pageable" else db
     sentinel = np.full(cap, -7, dtype=dt)
     if tgt_host:
         ctypes.memmove(tgt, sentinel.ctypes.data, sentinel.nbytes)

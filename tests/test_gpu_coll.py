@@ -47,7 +47,11 @@ def check_dm(results, cases):
                     assert (results[pe][str(c["id"]) + "_get"] == srcs[prv]).all(), (c, pe)
 
 
-def test_collectives_four_pes(tmp_path):
+@pytest.mark.parametrize("fused", ["fused", "barrier_copy_barrier"])
+def test_collectives_four_pes(tmp_path, fused):
+    """Small broadcast/fcollect run as one fused pull launch by default;
+    SHMEM_FUSED_MAX_BYTES=0 keeps them on device barrier + copy kernel +
+    device barrier (the path for messages above the fused limit)."""
     cases = []
     cid = 0
     for bits in (32, 64):
@@ -59,9 +63,12 @@ def test_collectives_four_pes(tmp_path):
         cases.append(case(cid, "fcollect", bits, 200, [[0, 0, 4]])); cid += 1
         cases.append(case(cid, "fcollect", bits, 33, [[1, 0, 3]])); cid += 1
         cases.append(case(cid, "fcollect", bits, 100, [[0, 0, 4]], target="host")); cid += 1
+        for tk in ("pageable", "mixed"):  # target the kernel cannot write: scratch + copy out
+            cases.append(case(cid, "broadcast", bits, 77, [[0, 0, 4]], root=3, target=tk)); cid += 1
+            cases.append(case(cid, "fcollect", bits, 45, [[0, 0, 4]], target=tk)); cid += 1
         cases.append(case(cid, "collect", bits, 4, [[0, 0, 4]])); cid += 1  # PE 0 contributes nothing
         cases.append(case(cid, "collect", bits, 3, [[0, 1, 2], [1, 1, 2]])); cid += 1
         cases.append(case(cid, "putget", bits, 100, [[0, 0, 4]])); cid += 1
         cases.append(case(cid, "putget", bits, 64, [[0, 0, 4]], target="host")); cid += 1
-    results = run_pes(4, cases, tmp_path)
+    results = run_pes(4, cases, tmp_path, extra_env=None if fused == "fused" else {"SHMEM_FUSED_MAX_BYTES": "0"})
     check_dm(results, cases)
