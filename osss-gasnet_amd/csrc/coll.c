@@ -85,7 +85,24 @@ static void put_bytes (const char *fn, void *dest, const void *src, size_t nbyte
         shmemi_fatal ("%s: no GPU (SHMEM_BOOTSTRAP_ONLY)", fn);
     if (nbytes == 0)
         return;
-    blocking_copy (remote_addr (fn, dest, nbytes, pe), src, nbytes);
+    void *to = remote_addr (fn, dest, nbytes, pe);
+    const void *from = is_device_ptr (src) ? src : shmemi_host_dev_ptr (src, nbytes);
+    if (from != NULL && from != to) {
+        /* (peer) device <- device or page-locked host: the streaming copy
+         * kernel pushes over xGMI (write-through stores); the call returns
+         * once every store has drained (local completion), and shmem_quiet /
+         * the barriers wait for the kernel's end, whose system-scope release
+         * makes the data visible to the target PE */
+        shmemi_order_after_caller (0);
+        size_t nb = nbytes;
+        shmemi_arm_signal ();
+        const int rc = mi355_copy_segments (&to, &from, &nb, 1, shmemi.stream);
+        if (rc != 0)
+            shmemi_fatal ("%s: copy kernel launch failed: %d", fn, rc);
+        shmemi_wait_signal ();
+        return;
+    }
+    blocking_copy (to, src, nbytes);
 }
 
 static void get_bytes (const char *fn, void *dest, const void *src, size_t nbytes, int pe)
@@ -320,6 +337,8 @@ static void broadcast_bytes (const char *fn, void *target, const void *source, s
     if (nbytes != 0 && !shmemi_in_device_heap (source, nbytes))
         shmemi_fatal ("%s: source %p is not in the device symmetric heap (allocate it with "
                       "shmemx_malloc_device)", fn, source);
+    if (s.size == 1)
+        return; /* the root does not write its own target, and there is nobody to wait for */
     if (fused_pull_ok (&s, nbytes)) {
         SHMEMI_TRACE (SHMEMI_LOG_BROADCAST, "%s: %zu bytes from PE %d, one fused launch", fn, nbytes, root);
         const void *src = nbytes != 0 ? shmemi_peer_ptr (root, shmemi_heap_offset (source)) : NULL;
@@ -381,6 +400,18 @@ static void fcollect_bytes (const char *fn, void *target, const void *source, si
                             int logPE_stride, int PE_size)
 {
     struct cset s = make_set (fn, PE_start, logPE_stride, PE_size);
+    if (s.size == 1) { /* one member: target = source, nobody to wait for */
+        if (nbytes != 0 && !shmemi_in_device_heap (source, nbytes))
+            shmemi_fatal ("%s: source %p is not in the device symmetric heap (allocate it with "
+                          "shmemx_malloc_device)", fn, source);
+        if (nbytes != 0 && target != source) {
+            shmemi_order_after_caller (0);
+            void *d = target;
+            const void *src = source;
+            pull (&d, &src, &nbytes, 1);
+        }
+        return;
+    }
     if (s.size <= MI355_PULL_MAX_SEGS && nbytes != 0 && fused_pull_ok (&s, nbytes * (size_t) s.size)) {
         if (!shmemi_in_device_heap (source, nbytes))
             shmemi_fatal ("%s: source %p is not in the device symmetric heap (allocate it with "

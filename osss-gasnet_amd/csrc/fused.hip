@@ -131,7 +131,9 @@ __device__ void finish(const MI355FusedArgs &a, unsigned long long *mine, const 
 // write-through at system scope (the destination is read by peers or by the
 // host next). A block that stored the byte tail (plain stores) releases at
 // system scope.
-__device__ void block_copy(void *dst, const void *src, uint64_t nbytes, unsigned bi, unsigned nblocks) {
+// block_copy_issue only issues the stores (true if this thread stored a
+// plain tail byte); block_drain waits for them and releases if needed.
+__device__ bool block_copy_issue(void *dst, const void *src, uint64_t nbytes, unsigned bi, unsigned nblocks) {
     const bool vec = ((((uintptr_t)dst) | ((uintptr_t)src)) & 15) == 0;
     const uint64_t nv = vec ? nbytes / 16 : 0;
     for (uint64_t v = (uint64_t)bi * kBlock + threadIdx.x; v < nv; v += (uint64_t)nblocks * kBlock)
@@ -142,8 +144,16 @@ __device__ void block_copy(void *dst, const void *src, uint64_t nbytes, unsigned
         ((char *)dst)[b] = ((const char *)src)[b];
         plain = true;
     }
+    return plain;
+}
+
+__device__ void block_drain(bool plain) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (__syncthreads_or(plain) && threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+
+__device__ void block_copy(void *dst, const void *src, uint64_t nbytes, unsigned bi, unsigned nblocks) {
+    block_drain(block_copy_issue(dst, src, nbytes, bi, nblocks));
 }
 
 template <int OP, typename T>
@@ -304,8 +314,13 @@ __global__ __launch_bounds__(kBlock) void fused_pull(MI355PullArgs p) {
     __syncthreads();
     if (!wait_members(a, mine, cnt, MI355_SIG_ARRIVE, false)) ok_all = 0;
     __syncthreads();
-    if (ok_all)
-        for (int k = 0; k < p.nseg; ++k) block_copy(p.dst[k], p.src[k], p.nbytes[k], blockIdx.x, gridDim.x);
+    if (ok_all) {
+        // every segment's loads in flight together (one segment per peer:
+        // all links busy at once), one drain at the end
+        bool plain = false;
+        for (int k = 0; k < p.nseg; ++k) plain |= block_copy_issue(p.dst[k], p.src[k], p.nbytes[k], blockIdx.x, gridDim.x);
+        block_drain(plain);
+    }
     if (last_block(mine + MI355_SIG_AG_COUNT)) {
         publish(a, cnt, MI355_SIG_AGDONE);
         __syncthreads();

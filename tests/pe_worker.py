@@ -80,7 +80,14 @@ def run_datamove(shm, c, me, da, db, ha, hb, results):
         f.argtypes = [vp, vp, sz, i]
         g = getattr(L, f"shmem_get{bits}")
         g.argtypes = [vp, vp, sz, i]
-        f(db + mem.index(me) * c["n"] * es, da, c["n"], nxt)
+        src = da
+        if c.get("put_from") == "host":  # page-locked shmem_malloc source
+            ctypes.memmove(ha, x.ctypes.data, x.nbytes)
+            src = ha
+        elif c.get("put_from") == "pageable":
+            keep = np.ascontiguousarray(x)
+            src = keep.ctypes.data
+        f(db + mem.index(me) * c["n"] * es, src, c["n"], nxt)
         L.shmem_barrier(start, logstride, size, psync)
         g(hb if tgt_host else db + size * c["n"] * es, da, c["n"], prv)
         L.shmem_barrier(start, logstride, size, psync)

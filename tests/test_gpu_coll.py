@@ -66,9 +66,14 @@ def test_collectives_four_pes(tmp_path, fused):
         for tk in ("pageable", "mixed"):  # target the kernel cannot write: scratch + copy out
             cases.append(case(cid, "broadcast", bits, 77, [[0, 0, 4]], root=3, target=tk)); cid += 1
             cases.append(case(cid, "fcollect", bits, 45, [[0, 0, 4]], target=tk)); cid += 1
+        for tk in ("device", "pageable"):  # one-member active sets (PEs 2 and 3 alone)
+            cases.append(case(cid, "broadcast", bits, 40, [[2, 0, 1], [3, 0, 1]], root=0, target=tk)); cid += 1
+            cases.append(case(cid, "fcollect", bits, 41, [[2, 0, 1], [3, 0, 1]], target=tk)); cid += 1
         cases.append(case(cid, "collect", bits, 4, [[0, 0, 4]])); cid += 1  # PE 0 contributes nothing
         cases.append(case(cid, "collect", bits, 3, [[0, 1, 2], [1, 1, 2]])); cid += 1
         cases.append(case(cid, "putget", bits, 100, [[0, 0, 4]])); cid += 1
         cases.append(case(cid, "putget", bits, 64, [[0, 0, 4]], target="host")); cid += 1
+        for pf in ("host", "pageable"):  # put from host memory (kernel over PCIe / DMA)
+            cases.append(case(cid, "putget", bits, 51, [[0, 0, 4]], put_from=pf)); cid += 1
     results = run_pes(4, cases, tmp_path, extra_env=None if fused == "fused" else {"SHMEM_FUSED_MAX_BYTES": "0"})
     check_dm(results, cases)
