@@ -48,6 +48,19 @@ def synth(pe, idx):
     return (mant - 0.5) * np.exp2(k)
 
 
+def synth_bits(pe, idx):
+    """Deterministic 64-bit words whose bits are 1 with probability 7/8 (OR
+    of three splitmix64 words), so an N-way AND is not all-zero (SURVEY 8d,
+    config 4's longlong and)."""
+    out = np.zeros(len(idx), dtype=np.uint64)
+    for r in range(3):
+        z = (np.uint64(pe + 1000 * (r + 1)) << np.uint64(40)) + idx.astype(np.uint64) + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        out = out | (z ^ (z >> np.uint64(31)))
+    return out.view(np.int64)
+
+
 def cpu_baseline(n, budget_s):
     """The reference algorithm (oracle restatement) at 1 PE on 1 core: median
     seconds per call over as many calls as fit in ~budget_s."""
@@ -74,6 +87,8 @@ def main():
     ap.add_argument("--no-rccl-compare", action="store_true",
                     help="N > 1: skip timing the same K calls through RCCL's ncclAllReduce (SHMEM_REDUCE_ALGORITHM"
                          "=rccl) beside the default P2P schedule")
+    ap.add_argument("--no-ops", action="store_true",
+                    help="skip the op-coverage leg (BASELINE config 4: float max + longlong and, 64 MiB per PE)")
     ap.add_argument("--host", action="store_true",
                     help="source/target in host memory (shmem_malloc, page-locked): the rate includes the "
                          "H2D/D2H staging copies (DESIGN.md); not the headline metric")
@@ -149,9 +164,12 @@ def main():
     if small_calls:
         steps(20, small_n)
         shm.barrier_all()
+        shm.sync()
         ts0 = time.perf_counter()
         steps(small_calls, small_n)
+        shm.sync()
         t_small = (time.perf_counter() - ts0) / small_calls
+        shm.barrier_all()
 
     # N > 1: the same K calls through RCCL (ncclAllReduce on the whole job,
     # SHMEM_REDUCE_ALGORITHM=rccl) for comparison with the P2P schedule; the
@@ -183,20 +201,23 @@ def main():
         t_rccl_local = time.perf_counter() - tr0
         shm.barrier_all()
         shm.set_algorithm(args.algorithm)
+        steps(1)  # the target again from the default schedule, for the check below
 
     # max over PEs, through the library's own host-staged double max reduction
-    tbuf = np.array([t_local], dtype=np.float64)
-    tout = np.zeros(1, dtype=np.float64)
-    shm.to_all("max", "double", tout.ctypes.data, tbuf.ctypes.data, 1, 0, 0, npes)
-    t_max = float(tout[0])
-    t_step = t_max / args.steps
+    def max_over_pes(x):
+        tbuf = np.array([x], dtype=np.float64)
+        tout = np.zeros(1, dtype=np.float64)
+        shm.to_all("max", "double", tout.ctypes.data, tbuf.ctypes.data, 1, 0, 0, npes)
+        return float(tout[0])
+
+    t_step = max_over_pes(t_local) / args.steps
+    if t_small is not None:
+        t_small = max_over_pes(t_small)
     rccl = None
     if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host and not rccl_ok:
         rccl = {"error": "RCCL communicator did not come up within 60 s on every PE; comparison skipped"}
     if t_rccl_local is not None:
-        tbuf[0] = t_rccl_local
-        shm.to_all("max", "double", tout.ctypes.data, tbuf.ctypes.data, 1, 0, 0, npes)
-        tr_step = float(tout[0]) / args.steps
+        tr_step = max_over_pes(t_rccl_local) / args.steps
         rccl = {"ms_per_step": round(tr_step * 1e3, 4), "value": round(npes * S / tr_step / GIB, 2),
                 "busbw_GB_s_per_pe": round(2.0 * (npes - 1) / npes * S / tr_step / 1e9, 1),
                 "p2p_speedup": round(tr_step / t_step, 3),
@@ -222,6 +243,42 @@ def main():
         check = "bit-exact vs reference order (PE_start), %d samples" % len(idx) if bad == 0 else \
             "MISMATCH %d of %d samples" % (bad, len(idx))
         del got_full
+
+    # BASELINE config 4 (op coverage): shmem_float_max_to_all and
+    # shmem_longlong_and_to_all on 64 MiB per PE, timed like the headline
+    # (C loop, max over PEs) and checked bit-exact on a sample
+    ops = None
+    if not args.no_ops and not args.host:
+        import oracle
+        ops = {}
+        ob = min(64 << 20, S)
+        for name, op, dtype, es, gen in (
+                ("float_max", "max", "float", 4, lambda pe, i: synth(pe, i).astype(np.float32)),
+                ("longlong_and", "and", "longlong", 8, synth_bits)):
+            no = ob // es
+            shm.put(src, gen(me, np.arange(no, dtype=np.uint64)))
+            oloop = shmem_reduce.bench_loop(name=name)
+            k = max(10, args.steps // 4)
+            oloop(dst, src, no, 0, 0, npes, None, shm._psync_ptr, 3)
+            shm.barrier_all()
+            shm.sync()
+            to0 = time.perf_counter()
+            oloop(dst, src, no, 0, 0, npes, None, shm._psync_ptr, k)
+            shm.sync()
+            t_op = max_over_pes(time.perf_counter() - to0) / k
+            shm.barrier_all()
+            ck = "skipped"
+            if not args.no_check:
+                idx = np.unique(np.random.default_rng(100 + me).integers(0, no, 1 << 14)).astype(np.uint64)
+                got = shm.get(dst, no, dtype)[idx.astype(np.int64)]
+                want = oracle.reduce_pe(op, dtype, [gen(p, idx) for p in range(npes)], 0)
+                bad = int((got.view(np.uint8) != want.view(np.uint8)).sum())
+                ck = "bit-exact, %d samples" % len(idx) if bad == 0 else "MISMATCH in %d bytes" % bad
+            ops[name] = {"bytes_per_pe": ob, "steps": k, "us_per_call": round(t_op * 1e6, 2),
+                         "value": round(npes * ob / t_op / GIB, 2), "per_pe_gib_s": round(ob / t_op / GIB, 2),
+                         "check": ck}
+        ops["note"] = ("BASELINE config 4 (op coverage): shmem_float_max_to_all and shmem_longlong_and_to_all, "
+                       "64 MiB per PE, GiB/s reduced whole job; longlong words with bits 1 at p = 7/8")
 
     # dominant kernel and its algorithmic bytes per launch
     if npes == 1:
@@ -294,8 +351,9 @@ def main():
             "cpu_baseline": cpu,
             "small_call": None if t_small is None else
             {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small * 1e6, 2), "calls": small_calls,
-             "note": "BASELINE config 5 shape: 4096 back-to-back 64 KiB shmem_double_sum_to_all calls, PE 0 clock"},
+             "note": "BASELINE config 5 shape: 4096 back-to-back 64 KiB shmem_double_sum_to_all calls, max over PEs"},
             "check": check,
+            "op_coverage": ops,
         }
         print(json.dumps(out), flush=True)
     if args.host:

@@ -21,3 +21,18 @@ void shmemb_double_sum_loop (double *target, double *source, int nreduce, int PE
     for (int i = 0; i < iters; ++i)
         shmem_double_sum_to_all (target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync);
 }
+
+/* BASELINE config 4's op-coverage pair, same shape of loop */
+void shmemb_float_max_loop (float *target, float *source, int nreduce, int PE_start, int logPE_stride,
+                            int PE_size, float *pWrk, long *pSync, int iters)
+{
+    for (int i = 0; i < iters; ++i)
+        shmem_float_max_to_all (target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync);
+}
+
+void shmemb_longlong_and_loop (long long *target, long long *source, int nreduce, int PE_start, int logPE_stride,
+                               int PE_size, long long *pWrk, long *pSync, int iters)
+{
+    for (int i = 0; i < iters; ++i)
+        shmem_longlong_and_to_all (target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync);
+}

@@ -212,12 +212,13 @@ class Shmem:
 BENCH_LIB_PATH = os.path.join(HERE, "lib", "libshmem_bench.so")
 
 
-def bench_loop(path=BENCH_LIB_PATH):
+def bench_loop(path=BENCH_LIB_PATH, name="double_sum"):
     """bench.py's timed loop in C (csrc/bench_loop.c): K back-to-back
-    shmem_double_sum_to_all calls. Load after the main library."""
+    shmem_<name>_to_all calls (double_sum, float_max, longlong_and). Load
+    after the main library."""
     if not os.path.exists(path):
         raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
-    f = ctypes.CDLL(path).shmemb_double_sum_loop
+    f = getattr(ctypes.CDLL(path), f"shmemb_{name}_loop")
     f.argtypes = [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i]
     f.restype = None
     return f
