@@ -322,6 +322,13 @@ def main():
                 if nag and ag_avg_ms > 0 else None,
                 "note": "busbw = 2(N-1)/N * S / t_step = bytes each PE receives over xGMI per second; "
                         "bound = (N-1) links x 153 GB/s (SURVEY 8d), or x 76.8 GB/s if 153.6 is both directions"}
+        import ctypes
+        lt, hp = ctypes.c_int(), ctypes.c_int()
+        links = {}
+        for q in range(1, npes):
+            if shm.lib.shmemx_peer_link(q, ctypes.byref(lt), ctypes.byref(hp)) == 0:
+                links[str(q)] = {"type": {4: "xgmi", 2: "pcie"}.get(lt.value, str(lt.value)), "hops": hp.value}
+        xgmi["links_from_pe0"] = links or None
         if not distinct_gpus:
             xgmi["note"] = ("the PEs share ONE GPU (test layout): peer 'xGMI' reads are local HBM reads, so "
                             "these figures are not xGMI rates")

@@ -300,10 +300,13 @@ static void fused_pull (const char *fn, const struct cset *s, void *target, size
                         const void *const *srcs, const size_t *nb, int k)
 {
     char *t = NULL;
+    int copy_out = 0;
     if (total != 0) {
         t = is_device_ptr (target) ? (char *) target : (char *) shmemi_host_dev_ptr (target, total);
-        if (t == NULL)
-            t = shmemi.heap + shmemi.scratch_off + 2 * shmemi.scratch_chunk; /* scratch C, copied out below */
+        if (t == NULL) {
+            t = shmemi.heap + shmemi.scratch_off + 2 * shmemi.scratch_chunk; /* scratch C */
+            copy_out = 1;
+        }
     }
     MI355PullArgs p;
     memset (&p, 0, sizeof p);
@@ -322,7 +325,7 @@ static void fused_pull (const char *fn, const struct cset *s, void *target, size
         shmemi_fatal ("%s: fused pull launch failed: %d", fn, rc);
     if (shmemi_wait_flag (p.m.epoch) != p.m.epoch)
         shmemi_fatal ("%s: timed out waiting for the other PEs of the active set", fn);
-    if (t != NULL && t != (char *) target && t == shmemi.heap + shmemi.scratch_off + 2 * shmemi.scratch_chunk)
+    if (copy_out)
         for (int i = 0; i < k; ++i)
             blocking_copy ((char *) target + toff[i], t + toff[i], nb[i]);
 }

@@ -1035,6 +1035,31 @@ int shmemx_get_reduce_algorithm (void) { return shmemi.algorithm; }
 
 int shmemx_device_id (void) { return shmemi.initialized ? shmemi.device : -1; }
 
+/* Link between this PE's GPU and PE pe's (bench.py's xgmi record):
+ * hsa_amd_link_info_type_t (4 = xGMI, 2 = PCIe) and hop count. -1 when pe is
+ * this PE, shares its GPU, or its GPU is not visible to this process. */
+int shmemx_peer_link (int pe, int *link_type, int *hops)
+{
+    if (!shmemi.initialized || shmemi.seg == NULL || pe < 0 || pe >= shmemi.npes || pe == shmemi.mype)
+        return -1;
+    int peer_dev = -1;
+    const char *bus = seg_info (pe)->pci_bus_id;
+    if (bus[0] == '\0' || hipDeviceGetByPCIBusId (&peer_dev, bus) != hipSuccess || peer_dev == shmemi.device) {
+        (void) hipGetLastError ();
+        return -1;
+    }
+    uint32_t t = 0, h = 0;
+    if (hipExtGetLinkTypeAndHopCount (shmemi.device, peer_dev, &t, &h) != hipSuccess) {
+        (void) hipGetLastError ();
+        return -1;
+    }
+    if (link_type != NULL)
+        *link_type = (int) t;
+    if (hops != NULL)
+        *hops = (int) h;
+    return 0;
+}
+
 void shmemx_device_synchronize (void) { SHMEMI_HIP (hipDeviceSynchronize ()); }
 
 void shmemx_memcpy (void *dst, const void *src, size_t nbytes)

@@ -47,6 +47,7 @@ def load(path=LIB_PATH):
         "shmemx_is_device_symmetric": ([_vp], _i),
         "shmemx_set_reduce_algorithm": ([_i], _i), "shmemx_get_reduce_algorithm": ([], _i),
         "shmemx_device_id": ([], _i), "shmemx_device_synchronize": ([], None),
+        "shmemx_peer_link": ([_i, ctypes.POINTER(_i), ctypes.POINTER(_i)], _i),
         "shmemx_memcpy": ([_vp, _vp, _sz], None), "shmemx_wtime": ([], ctypes.c_double),
         "shmemx_kernel_timing": ([_i], None),
         "shmemx_rccl_init": ([ctypes.c_double], _i),

@@ -119,6 +119,13 @@ def test_kernel_timing_counts_launches(shm):
     shm.free_device(a)
 
 
+def test_peer_link_has_no_self_link(shm):
+    t, h = ctypes.c_int(-7), ctypes.c_int(-7)
+    assert shm.lib.shmemx_peer_link(0, ctypes.byref(t), ctypes.byref(h)) == -1   # PE 0 is this PE
+    assert shm.lib.shmemx_peer_link(5, ctypes.byref(t), ctypes.byref(h)) == -1   # no such PE
+    assert (t.value, h.value) == (-7, -7)
+
+
 def test_psync_is_left_at_sync_value(shm):
     psync = np.full(shmem_reduce.SHMEM_REDUCE_SYNC_SIZE, -1, dtype=np.int64)
     x = np.ones(100)
