@@ -103,6 +103,8 @@ def test_four_pes_all_44_pairs_p2p_and_exact(tmp_path, fused_max, oneshot_max):
     cases += make_cases(oracle.PAIRS, 1000, [[0, 0, 4]], "dev", "p2p", 0)
     cases += make_cases(oracle.PAIRS, 257, [[0, 0, 4]], "dev", "exact", 100)
     cases += make_cases(oracle.PAIRS, 1000, [[0, 0, 4]], "inplace", "p2p", 200)  # in place: never one-shot
+    cases += make_cases(SOME, 9, [[0, 0, 4]], "dev", "p2p", 300)      # less than one 16-byte vector per element type
+    cases += make_cases(SOME, 4099, [[1, 0, 3]], "dev", "p2p", 400)  # several blocks and an element tail
     results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_FUSED_MAX_BYTES": fused_max,
                                                      "SHMEM_ONESHOT_MAX_BYTES": oneshot_max})
     check(results, cases)
