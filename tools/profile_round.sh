@@ -1,7 +1,7 @@
 #!/bin/bash
 # Refresh the judged profiles for one round, on the GPU box, from the repo root:
 #   tools/profile_round.sh r01
-# 1. rocprofv3 --kernel-trace --stats of bench.py (N = 1, 256 MiB, no small-call
+# 1. rocprofv3 --kernel-trace --stats of bench.py (N = 1, 256 MiB, no small-call or op-coverage
 #    leg, so the dominant kernel's average is the 256 MiB copy's)
 # 2. two separate --pmc passes (FETCH_SIZE, WRITE_SIZE) of the same command,
 #    turned into HBM bytes per launch by tools/pmc_traffic.py
@@ -14,7 +14,7 @@ OUT=gpurun_out/prof_$R
 DST=gpurun_out/profiles/$R
 mkdir -p "$OUT" "$DST/pmc"
 export TMPDIR=/tmp
-BENCH=(bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-small)
+BENCH=(bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-small --no-ops)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "${BENCH[@]}" \
     > "$OUT/bench_trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 "${BENCH[@]}" --no-check \
