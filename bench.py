@@ -293,6 +293,10 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
                 "kernel": kname, "alg_bytes_per_launch": alg_bytes, "kernel_avg_us": round(k_avg_ms * 1e3, 2),
                 "launches_timed": nk, "ms_per_step_with_events": round(t_local_ev / args.steps * 1e3, 4)}
+    if npes > 1:
+        roofline["note"] = ("N > 1: (N-1)/N of this kernel's reads cross xGMI, so the HBM fraction is not its "
+                            "bound; the link-side figures are in `xgmi` (rs_kernel_remote_read_GB_s against "
+                            "mesh_bound_GB_s_per_pe)")
     traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(traffic_file) and not args.host:
         try:
