@@ -97,6 +97,11 @@ int mi355_signal_launch (void *stream);
  * that precedes reads of other PEs' buffers. */
 int mi355_acquire_system (void *stream);
 
+/* n elements short -> int32 (widen != 0) or int32 -> short (truncating), on
+ * `stream`: the RCCL schedule's 16-bit integer support (RCCL has no 16-bit
+ * integer type). */
+int mi355_convert_short (int widen, const void *src, void *dst, size_t n, void *stream);
+
 /* ---- one-launch P2P reduction for small messages (fused.hip) ----
  * Signal region: per PE, MI355_SIG_WORDS 8-byte words of uncached device
  * memory mapped into every peer; all zero before first use. It holds

@@ -628,3 +628,30 @@ extern "C" void mi355_time_next_launch(void *start_event, void *stop_event) {
     t_ev_start = (hipEvent_t)start_event;
     t_ev_stop = (hipEvent_t)stop_event;
 }
+
+// short <-> int32 for the RCCL schedule (RCCL has no 16-bit integer type):
+// sum/prod wrap mod 2^32 in int32, and truncating to 16 bits afterwards gives
+// the same bits as the reference's per-step promote-and-truncate (truncation
+// is a ring homomorphism); min/max are exact on widened values.
+__global__ __launch_bounds__(256) void widen_short_k(const int16_t *s, int32_t *d, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        d[i] = s[i];
+}
+__global__ __launch_bounds__(256) void narrow_int_k(const int32_t *s, int16_t *d, uint64_t n) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (uint64_t)gridDim.x * 256)
+        d[i] = (int16_t)s[i];
+}
+
+extern "C" int mi355_convert_short(int widen, const void *src, void *dst, size_t n, void *stream) {
+    if (n == 0) return 0;
+    if (src == nullptr || dst == nullptr) return MI355_E_INVAL;
+    const unsigned grid = grid_for(256, n, 2);
+    if (widen)
+        hipLaunchKernelGGL(widen_short_k, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const int16_t *)src,
+                           (int32_t *)dst, (uint64_t)n);
+    else
+        hipLaunchKernelGGL(narrow_int_k, dim3(grid), dim3(256), 0, (hipStream_t)stream, (const int32_t *)src,
+                           (int16_t *)dst, (uint64_t)n);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}

@@ -23,6 +23,7 @@ int shmemi_rccl_supported (int op, int dtype)
     if (op == MI355_OP_AND || op == MI355_OP_OR || op == MI355_OP_XOR)
         return 0;
     switch (dtype) {
+    case MI355_SHORT: /* widened to int32 through scratch C */
     case MI355_INT:
     case MI355_LONG:
     case MI355_LONGLONG:
@@ -129,8 +130,12 @@ void shmemi_rccl_destroy (void)
     }
 }
 
+static int rccl_allreduce_short (int op, const void *src, void *dst, size_t n);
+
 int shmemi_rccl_allreduce (int op, int dtype, const void *src, void *dst, size_t n)
 {
+    if (dtype == MI355_SHORT)
+        return rccl_allreduce_short (op, src, dst, n);
     ncclDataType_t t;
     size_t count = n;
     switch (dtype) {
@@ -159,6 +164,27 @@ int shmemi_rccl_allreduce (int op, int dtype, const void *src, void *dst, size_t
     r = rccl_settle ((ncclComm_t) comm, r, shmemi.barrier_timeout); /* non-blocking communicator */
     if (r != ncclSuccess)
         return -1;
+    SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    return 0;
+}
+
+/* short: widen a chunk into the first half of scratch C, ncclAllReduce int32
+ * into the second half, truncate into dst. Scratch C is free here: the
+ * callers' sources/targets are user buffers or scratch A/B (staged()). */
+static int rccl_allreduce_short (int op, const void *src, void *dst, size_t n)
+{
+    const size_t half = shmemi.scratch_chunk / 2 / 256 * 256;
+    const size_t per = half / sizeof (int32_t);
+    char *win = shmemi.heap + shmemi.scratch_off + 2 * shmemi.scratch_chunk, *wout = win + half;
+    for (size_t b = 0; b < n; b += per) {
+        const size_t cn = n - b < per ? n - b : per;
+        if (mi355_convert_short (1, (const short *) src + b, win, cn, shmemi.stream) != 0)
+            return -1;
+        if (shmemi_rccl_allreduce (op, MI355_INT, win, wout, cn) != 0) /* synchronizes the stream */
+            return -1;
+        if (mi355_convert_short (0, wout, (short *) dst + b, cn, shmemi.stream) != 0)
+            return -1;
+    }
     SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
     return 0;
 }

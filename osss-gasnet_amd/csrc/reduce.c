@@ -385,7 +385,7 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
     const int same = dst_off == src_off;
     if (s->size > 1 && shmemi.p2p_broken)
         shmemi_fatal ("peer GPU memory reads failed the init self-test; only the RCCL pairs "
-                      "(sum/prod/min/max on int/long/float/double, complex sum) can run");
+                      "(sum/prod/min/max on short/int/long/float/double, complex sum) can run");
     const int overlap = ranges_overlap (dst_off, src_off, nbytes);
 
     if (s->size == 1) {

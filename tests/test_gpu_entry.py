@@ -135,10 +135,12 @@ def test_psync_is_left_at_sync_value(shm):
 
 
 @pytest.mark.parametrize("op,dtype", [("sum", "double"), ("max", "float"), ("min", "int"), ("prod", "long"),
-                                      ("sum", "complexd"), ("sum", "complexf")])
+                                      ("sum", "complexd"), ("sum", "complexf"),
+                                      ("sum", "short"), ("prod", "short"), ("min", "short")])
 def test_rccl_glue_one_rank(shm, op, dtype):
     """The RCCL schedule's glue (csrc/rccl.c: non-blocking communicator
-    bring-up with a deadline, type/op mapping, complex sum as 2n reals) on a
+    bring-up with a deadline, type/op mapping, complex sum as 2n reals, short
+    widened to int32 and truncated back) on a
     1-rank communicator, where ncclAllReduce is the identity. Multi-rank RCCL
     needs one GPU per rank (RCCL refuses two ranks on one device), so this is
     what the one-GPU box can run."""
