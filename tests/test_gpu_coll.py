@@ -77,3 +77,17 @@ def test_collectives_four_pes(tmp_path, fused):
             cases.append(case(cid, "putget", bits, 51, [[0, 0, 4]], put_from=pf)); cid += 1
     results = run_pes(4, cases, tmp_path, extra_env=None if fused == "fused" else {"SHMEM_FUSED_MAX_BYTES": "0"})
     check_dm(results, cases)
+
+
+def test_collectives_eight_pes(tmp_path):
+    """Broadcast and fcollect over 8 PE processes (one fused pull launch below
+    the fused limit, barrier + copy kernel + barrier above it), and over two
+    interleaved strided sets of 4."""
+    cases = []
+    cid = 0
+    for n in (100, 40000):  # 800 B / 320 KB per PE (fcollect: 8x that into every PE)
+        cases.append(case(cid, "broadcast", 64, n, [[0, 0, 8]], root=5, cap=40960)); cid += 1
+        cases.append(case(cid, "fcollect", 64, n // 8, [[0, 0, 8]], cap=40960)); cid += 1
+        cases.append(case(cid, "fcollect", 32, n // 8, [[0, 1, 4], [1, 1, 4]], cap=40960)); cid += 1
+    results = run_pes(8, cases, tmp_path)
+    check_dm(results, cases)
