@@ -91,3 +91,40 @@ def test_collectives_eight_pes(tmp_path):
         cases.append(case(cid, "fcollect", 32, n // 8, [[0, 1, 4], [1, 1, 4]], cap=40960)); cid += 1
     results = run_pes(8, cases, tmp_path)
     check_dm(results, cases)
+
+
+def test_mixed_collectives_stress(tmp_path):
+    """200 back-to-back calls on 4 PEs mixing reductions (fused and multi-launch
+    sizes), broadcast, fcollect, collect and put/get with random sizes, targets
+    and active sets: every collective kind advances the same per-pair counts
+    of the signal region, so a kind that miscounted would deadlock or let a
+    PE read a buffer too early here."""
+    from test_gpu_multipe import check as check_red
+    rng = np.random.default_rng(4242)
+    sets_choices = [[[0, 0, 4]], [[0, 1, 2], [1, 1, 2]], [[1, 0, 3]], [[0, 0, 2], [2, 0, 2]]]
+    cases = []
+    for cid in range(200):
+        sets = sets_choices[rng.integers(len(sets_choices))]
+        k = int(rng.integers(6))
+        if k <= 1:
+            op, dtype = oracle.PAIRS[rng.integers(len(oracle.PAIRS))]
+            cases.append({"id": cid, "op": op, "dtype": dtype, "n": int(rng.choice([1, 100, 3000, 40000])),
+                          "sets": sets, "mode": str(rng.choice(["dev", "inplace", "host"])),
+                          "algorithm": "p2p", "seed": 9000 + cid})
+            continue
+        bits = int(rng.choice([32, 64]))
+        tgt = str(rng.choice(["device", "device", "host", "pageable"]))
+        if k == 2:
+            size = sets[0][2]
+            cases.append(case(cid, "broadcast", bits, int(rng.choice([0, 5, 300, 3000])), sets,
+                              root=int(rng.integers(size)), target=tgt))
+        elif k == 3:
+            cases.append(case(cid, "fcollect", bits, int(rng.choice([1, 50, 900])), sets, target=tgt))
+        elif k == 4:
+            cases.append(case(cid, "collect", bits, 5, sets))
+        else:
+            cases.append(case(cid, "putget", bits, int(rng.choice([3, 64, 500])), [[0, 0, 4]]))
+    results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_DEVICE_HEAP_SIZE": "64M",
+                                                     "SHMEM_DEVICE_SCRATCH_SIZE": "3M"})
+    check_red(results, [c for c in cases if "op" in c and "kind" not in c])
+    check_dm(results, [c for c in cases if "kind" in c])
