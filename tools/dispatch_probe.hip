@@ -20,6 +20,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <type_traits>
 #include <vector>
 
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
@@ -35,6 +36,24 @@ struct Args {
 extern "C" __global__ __launch_bounds__(64) void probe_k(Args a) {
     if (threadIdx.x == 0) __hip_atomic_store(a.flag, a.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+
+// the same kernel with a larger argument block (the fused kernel's is 1.5 KiB)
+template <int PAD>
+struct BigArgs {
+    unsigned *flag;
+    unsigned epoch;
+    unsigned long long pad[PAD];
+};
+template <int PAD>
+__global__ __launch_bounds__(64) void probe_big_k(BigArgs<PAD> a) {
+    if (threadIdx.x == 0) __hip_atomic_store(a.flag, a.epoch + (unsigned)a.pad[PAD - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// main() is host-only below: instantiate the kernels where the device pass sees them
+template __global__ void probe_big_k<4>(BigArgs<4>);
+template __global__ void probe_big_k<64>(BigArgs<64>);
+template __global__ void probe_big_k<188>(BigArgs<188>);
+template __global__ void probe_big_k<380>(BigArgs<380>);
 
 #ifndef __HIP_DEVICE_COMPILE__
 static double now() {
@@ -119,6 +138,31 @@ int main(int argc, char **argv) {
         report("hip: hipExtLaunchKernelGGL", api, rt);
     }
     CHECK(hipStreamSynchronize(st));
+    auto big = [&](auto tag, const char *name) {
+        constexpr int PAD = decltype(tag)::value;
+        std::vector<double> api, rt;
+        for (int i = 0; i < calls + 200; ++i) {
+            BigArgs<PAD> a{};
+            a.flag = flag;
+            a.epoch = ++epoch;
+            const double t0 = now();
+            hipExtLaunchKernelGGL(probe_big_k<PAD>, dim3(1), dim3(64), 0, st, nullptr, nullptr, 0, a);
+            const double t1 = now();
+            spin(flag, epoch);
+            const double t2 = now();
+            if (i >= 200) {
+                api.push_back(t1 - t0);
+                rt.push_back(t2 - t0);
+            }
+        }
+        report(name, api, rt);
+    };
+    big(std::integral_constant<int, 4>{}, "hip: 48 B of kernel arguments");
+    big(std::integral_constant<int, 64>{}, "hip: 528 B of kernel arguments");
+    big(std::integral_constant<int, 188>{}, "hip: 1.5 KiB of kernel arguments");
+    big(std::integral_constant<int, 380>{}, "hip: 3 KiB of kernel arguments");
+    CHECK(hipStreamSynchronize(st));
+    if (argc > 2) return 0;  // HIP part only
 
     // ---- HSA direct dispatch
     HCHECK(hsa_init());
