@@ -314,7 +314,11 @@ __global__ __launch_bounds__(kBlock) void fused_pull(MI355PullArgs p) {
     __syncthreads();
     if (!wait_members(a, mine, cnt, MI355_SIG_ARRIVE, false)) ok_all = 0;
     __syncthreads();
-    if (ok_all) {
+    if (!ok_all) {  // this block timed out: report it (the host aborts the job)
+        finish(a, mine, cnt, false);
+        return;
+    }
+    {
         // every segment's loads in flight together (one segment per peer:
         // all links busy at once), one drain at the end
         bool plain = false;
