@@ -190,6 +190,18 @@ def main():
         allok = np.zeros(1, dtype=np.int32)
         shm.to_all("min", "int", allok.ctypes.data, mine.ctypes.data, 1, 0, 0, npes)
         rccl_ok = bool(allok[0])
+        if rccl_ok:
+            # one probe allreduce through the glue, which reports a failure
+            # instead of aborting the job (the timed loop below goes through
+            # the public entry point, where a failure is fatal)
+            import ctypes
+            f = shm.lib.shmemi_rccl_allreduce
+            f.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t]
+            f.restype = ctypes.c_int
+            mine[0] = 1 if f(shmem_reduce.OPS.index("sum"), shmem_reduce.DTYPES.index("double"), src, dst,
+                             1024) == 0 else 0
+            shm.to_all("min", "int", allok.ctypes.data, mine.ctypes.data, 1, 0, 0, npes)
+            rccl_ok = bool(allok[0])
     if rccl_ok:
         shm.set_algorithm("rccl")
         steps(3)
