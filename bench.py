@@ -213,7 +213,8 @@ def main():
         t_rccl_local = time.perf_counter() - tr0
         shm.barrier_all()
         shm.set_algorithm(args.algorithm)
-        steps(1)  # the target again from the default schedule, for the check below
+    if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host:
+        steps(1)  # the target again from the default schedule (RCCL wrote it), for the check below
 
     # max over PEs, through the library's own host-staged double max reduction
     def max_over_pes(x):
@@ -227,7 +228,8 @@ def main():
         t_small = max_over_pes(t_small)
     rccl = None
     if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host and not rccl_ok:
-        rccl = {"error": "RCCL communicator did not come up within 60 s on every PE; comparison skipped"}
+        rccl = {"error": "RCCL did not come up (communicator within 60 s, or a probe allreduce) on every PE; "
+                         "comparison skipped"}
     if t_rccl_local is not None:
         tr_step = max_over_pes(t_rccl_local) / args.steps
         rccl = {"ms_per_step": round(tr_step * 1e3, 4), "value": round(npes * S / tr_step / GIB, 2),
