@@ -87,6 +87,8 @@ def main():
     ap.add_argument("--no-rccl-compare", action="store_true",
                     help="N > 1: skip timing the same K calls through RCCL's ncclAllReduce (SHMEM_REDUCE_ALGORITHM"
                          "=rccl) beside the default P2P schedule")
+    ap.add_argument("--force-rccl-compare", action="store_true",
+                    help="attempt the RCCL comparison even when PEs share a GPU (exercises its failure path)")
     ap.add_argument("--no-ops", action="store_true",
                     help="skip the op-coverage leg (BASELINE config 4: float max + longlong and, 64 MiB per PE)")
     ap.add_argument("--host", action="store_true",
@@ -182,8 +184,13 @@ def main():
         lo, hi = np.zeros(1, dtype=np.int32), np.zeros(1, dtype=np.int32)
         shm.to_all("min", "int", lo.ctypes.data, dev.ctypes.data, 1, 0, 0, npes)
         shm.to_all("max", "int", hi.ctypes.data, dev.ctypes.data, 1, 0, 0, npes)
-        distinct_gpus = int(lo[0]) != int(hi[0])
+        distinct_gpus = int(lo[0]) != int(hi[0]) or args.force_rccl_compare
     rccl_ok = False
+    # RCCL prints a version banner on stdout at communicator creation; keep
+    # stdout to the one JSON line by pointing fd 1 at stderr meanwhile
+    sys.stdout.flush()
+    saved_stdout = os.dup(1)
+    os.dup2(2, 1)
     if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host:
         # non-blocking RCCL bring-up with a deadline; every PE must have it
         mine = np.array([1 if shm.lib.shmemx_rccl_init(60.0) == 0 else 0], dtype=np.int32)
@@ -215,6 +222,9 @@ def main():
         shm.set_algorithm(args.algorithm)
     if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host:
         steps(1)  # the target again from the default schedule (RCCL wrote it), for the check below
+    sys.stdout.flush()
+    os.dup2(saved_stdout, 1)
+    os.close(saved_stdout)
 
     # max over PEs, through the library's own host-staged double max reduction
     def max_over_pes(x):
