@@ -21,11 +21,12 @@
  *
  * The remote side of put/get, and every collective's source, must be in the
  * device symmetric heap (shmemx_malloc_device): that is where peers can read
- * it over xGMI. Local sides may be any host or device memory. A put goes
- * through hipMemcpy on the peer-mapped pointer (the HIP runtime's P2P copy
- * contract makes the bytes visible to the peer's later kernels: a push into
- * another GPU's memory must not be left to this library's own kernels, whose
- * write-through only reaches memory, not the peer's L2). A get into device
+ * it over xGMI. Local sides may be any host or device memory. A put into
+ * another GPU's memory goes through hipMemcpy on the peer-mapped pointer (the
+ * HIP runtime's P2P copy contract makes the bytes visible to the peer's later
+ * kernels; this library's kernels only ever write their own GPU's memory, so
+ * no coherence question about a peer GPU's L2 arises); a put whose target is
+ * on this GPU (a PE sharing it, or this PE) runs the copy kernel. A get into device
  * memory, and every collective, PULLS with the streaming copy kernel: every
  * PE reads the members' sources over xGMI into its own target, between two
  * barriers -- the same producer/consumer pattern as the reduction's
@@ -87,12 +88,13 @@ static void put_bytes (const char *fn, void *dest, const void *src, size_t nbyte
         return;
     void *to = remote_addr (fn, dest, nbytes, pe);
     const void *from = is_device_ptr (src) ? src : shmemi_host_dev_ptr (src, nbytes);
-    if (from != NULL && from != to) {
-        /* (peer) device <- device or page-locked host: the streaming copy
-         * kernel pushes over xGMI (write-through stores); the call returns
-         * once every store has drained (local completion), and shmem_quiet /
-         * the barriers wait for the kernel's end, whose system-scope release
-         * makes the data visible to the target PE */
+    if (from != NULL && from != to && shmemi_pe_same_device (pe)) {
+        /* target memory on this GPU (this PE's own heap, or a PE sharing the
+         * GPU) <- device or page-locked host: the streaming copy kernel; the
+         * call returns once every store has drained (local completion), and
+         * shmem_quiet / the barriers wait for the kernel's end. A target on
+         * ANOTHER GPU keeps the runtime's P2P copy below: this library's
+         * kernels never write another GPU's memory (see the file header). */
         shmemi_order_after_caller (0);
         size_t nb = nbytes;
         shmemi_arm_signal ();

@@ -725,6 +725,18 @@ void *pshmem_malloc (size_t size)
 /* Device-accessible address of [p, p + nbytes) when it lies inside one
  * page-locked shmem_malloc block (kernels can then read and write it over
  * PCIe directly), else NULL. */
+/* 1 if PE pe runs on this PE's GPU (same PCI bus id): its device heap is
+ * this GPU's own memory. */
+int shmemi_pe_same_device (int pe)
+{
+    if (pe == shmemi.mype)
+        return 1;
+    if (shmemi.seg == NULL || pe < 0 || pe >= shmemi.npes)
+        return 0;
+    const char *mine = seg_info (shmemi.mype)->pci_bus_id, *theirs = seg_info (pe)->pci_bus_id;
+    return mine[0] != '\0' && strcmp (mine, theirs) == 0;
+}
+
 void *shmemi_host_dev_ptr (const void *p, size_t nbytes)
 {
     const char *c = (const char *) p;

@@ -129,6 +129,7 @@ int shmemi_in_device_heap (const void *p, size_t nbytes);
 size_t shmemi_heap_offset (const void *p);
 void *shmemi_peer_ptr (int pe, size_t off);
 void *shmemi_host_dev_ptr (const void *p, size_t nbytes);
+int shmemi_pe_same_device (int pe);
 void shmemi_order_after_caller (int host_wait);
 void shmemi_check_stream_err (const char *fn);
 void shmemi_peer_acquire (hipStream_t st);
