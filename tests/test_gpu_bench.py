@@ -1,0 +1,54 @@
+"""GPU: bench.py's contract with the driver, on a short run -- exactly one
+JSON line on stdout (rank 0), the metric/config of BASELINE.json, a bit-exact
+check, and the roofline / cpu_baseline / op_coverage records. The N = 2 run
+shares the one test GPU and forces the RCCL comparison, which then fails
+(RCCL refuses two ranks on one device): the line must still come out, with
+the comparison marked as skipped and the target re-checked on the default
+schedule."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+
+
+def run(cmd, timeout=240):
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout[-3000:]
+    return json.loads(lines[0])
+
+
+def common(d, n):
+    assert d["metric"] == METRIC and d["unit"] == "GiB/s" and d["n_gpus"] == n
+    assert d["value"] > 0 and d["ms_per_step"] > 0 and d["higher_is_better"] is True
+    assert d["check"].startswith("bit-exact"), d["check"]
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] < 1.2 and r["achieved"] > 0
+    for name in ("float_max", "longlong_and"):
+        assert d["op_coverage"][name]["check"].startswith("bit-exact"), d["op_coverage"]
+    assert d["small_call"]["us_per_call"] > 0
+
+
+def test_bench_one_gpu_line():
+    d = run([sys.executable, "bench.py", "--steps", "5", "--warmup", "2", "--cpu-seconds", "0.5"])
+    common(d, 1)
+    assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] == 1
+    assert d["config"]["bytes_per_pe"] == 256 << 20
+
+
+@pytest.mark.multipe
+def test_bench_two_ranks_line_with_failed_rccl_comparison():
+    d = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+             "--master-addr", "127.0.0.1", "--master-port", "29563", "bench.py", "--gpus", "2", "--steps", "5",
+             "--warmup", "2", "--force-rccl-compare"])
+    common(d, 2)
+    assert d["cpu_baseline"] is None
+    assert "error" in d["rccl_compare"], d["rccl_compare"]
+    assert d["xgmi"]["busbw_GB_s_per_pe"] > 0
