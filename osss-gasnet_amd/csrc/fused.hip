@@ -44,6 +44,7 @@ namespace {
 using namespace mi355;
 
 constexpr int kBlock = 256;
+constexpr int kBatch = 8;  // members' vectors in flight per lane in the fold
 
 __device__ __forceinline__ void st_sys_u64(unsigned long long *p, unsigned long long v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -203,20 +204,43 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
             u32x4 *d = (u32x4 *)((char *)a.dst[a.me] + lo * sizeof(T));
             for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < nv;
                  v += (uint64_t)gridDim.x * kBlock) {
-                Pack<T> acc, x;
-                acc.v = ((const u32x4 *)((const char *)a.src[0] + lo * sizeof(T)))[v];
-                for (int k = 1; k < nm; ++k) {
-                    x.v = ((const u32x4 *)((const char *)a.src[k] + lo * sizeof(T)))[v];
+                // kBatch members' vectors are loaded before any is folded, so
+                // their (xGMI) latencies overlap instead of adding up; the
+                // fold itself stays in member order
+                Pack<T> acc;
+                for (int k0 = 0; k0 < nm; k0 += kBatch) {
+                    Pack<T> x[kBatch];
 #pragma unroll
-                    for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x.e[e]);
+                    for (int j = 0; j < kBatch; ++j)
+                        if (k0 + j < nm) x[j].v = ((const u32x4 *)((const char *)a.src[k0 + j] + lo * sizeof(T)))[v];
+#pragma unroll
+                    for (int j = 0; j < kBatch; ++j) {
+                        if (k0 + j >= nm) break;
+                        if (k0 + j == 0) {
+                            acc = x[0];
+                        } else {
+#pragma unroll
+                            for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[j].e[e]);
+                        }
+                    }
                 }
                 st16_sys(d + v, acc.v);
             }
             const uint64_t tail0 = lo + nv * V;
             if (tail0 < hi && blockIdx.x == 0 && threadIdx.x < hi - tail0) {
                 const uint64_t i = tail0 + threadIdx.x;
-                T acc = ((const T *)a.src[0])[i];
-                for (int k = 1; k < nm; ++k) acc = apply<OP>(acc, ((const T *)a.src[k])[i]);
+                T acc;
+                for (int k0 = 0; k0 < nm; k0 += kBatch) {
+                    T x[kBatch];
+#pragma unroll
+                    for (int j = 0; j < kBatch; ++j)
+                        if (k0 + j < nm) x[j] = ((const T *)a.src[k0 + j])[i];
+#pragma unroll
+                    for (int j = 0; j < kBatch; ++j) {
+                        if (k0 + j >= nm) break;
+                        acc = k0 + j == 0 ? x[0] : apply<OP>(acc, x[j]);
+                    }
+                }
                 ((T *)a.dst[a.me])[i] = acc;
             }
             if (tail0 < hi && blockIdx.x == 0) {
