@@ -67,6 +67,19 @@ int mi355_op_supported (int op, int dtype);
 int mi355_combine (int op, int dtype, void *dst, const void *const *srcs,
                    int nsrc, size_t n, void *stream);
 
+/* Every member's reference result at once: for each q < nsrc with dsts[q] != NULL,
+ *   dsts[q][i] = (((srcs[q][i] op srcs[0][i]) op srcs[1][i]) ... op srcs[nsrc-1][i])
+ * with srcs[q] itself skipped after the first operand: member q's OWN source
+ * first, then the others in active-set order -- the order the reference folds
+ * in on member q (reduce-op.c:226-264, the self-skip at :235). The P2P
+ * schedule's owner of a shard computes every member's version of it from one
+ * pass over the sources (the sources are read once, whatever nsrc). dsts[q]
+ * may alias srcs[q] exactly (in place); other overlaps are undefined, and above
+ * 8 sources at most one fold may be in place. 1 <= nsrc <= 32. */
+#define MI355_ORDERS_MAX_SOURCES 32
+int mi355_combine_orders (int op, int dtype, void *const *dsts, const void *const *srcs,
+                          int nsrc, size_t n, void *stream);
+
 /* nseg independent byte copies dsts[i] <- srcs[i] of nbytes[i] bytes in ONE
  * launch (the all-gather leg of the shard schedule). nseg <= 64. */
 int mi355_copy_segments (void *const *dsts, const void *const *srcs,
@@ -145,11 +158,20 @@ typedef struct MI355FusedArgs {
     /* 1: one-shot -- every member folds the whole array from all members' sources (one flag exchange
      * fewer than reduce-scatter + all-gather; for small messages). Needs dst != src. */
     int oneshot;
+    /* 0: every member receives member 0's result (the fold in member order).
+     * 1: every member receives the reference's result for ITSELF: its own source first, then the
+     *    others in member order (reduce-op.c:226-264). One-shot folds in that order directly; the
+     *    two-shot owner of shard j folds it in every member's order, keeps its own version in dst[j]
+     *    and member q's in its version area, ver[j] + s * shard * esize with s = q < j ? q : q - 1
+     *    (nmembers - 1 slots), and each member gathers its own version of the other shards there. */
+    int ordered;
+    void *ver[MI355_FUSED_MAX_MEMBERS];              /* members' version areas (mapped), if ordered */
 } MI355FusedArgs;
 
 /* Reduce-scatter + all-gather of n elements over the members in ONE launch:
- * every member ends with the fold, in member order, of all members' sources
- * (the reference's result on the first member). Every member must make the
+ * every member ends with the fold of all members' sources -- in member order
+ * (the reference's result on the first member), or with `ordered` in its own
+ * reference order (the reference's result on that member). Every member must make the
  * matching call; buffers 16-byte aligned; dst == src or disjoint.
  *
  * Pair counts live on the device (MI355_SIG_CALLS): the kernel reads them at

@@ -30,8 +30,8 @@ int shmemx_is_device_symmetric (const void *ptr);
  *   SHMEMX_REDUCE_AUTO  = P2P shard schedule (below)
  *   SHMEMX_REDUCE_P2P   = each PE reduces 1/N of the elements from every
  *                         PE's source over xGMI, then gathers the other
- *                         shards; every PE receives identical bits, equal to
- *                         the reference's result on PE_start
+ *                         shards; every PE receives the reference's result
+ *                         for itself (or PE_start's, see the result order)
  *   SHMEMX_REDUCE_EXACT = each PE folds all N sources in the reference order
  *                         (own first, then ascending); bit-identical to the
  *                         reference on every PE
@@ -46,6 +46,26 @@ enum shmemx_reduce_algorithm {
 };
 int shmemx_set_reduce_algorithm (int algorithm); /* returns the previous one */
 int shmemx_get_reduce_algorithm (void);
+
+/* Whose result the P2P schedules (and the stream-ordered calls) deliver
+ * (env SHMEM_REDUCE_ORDER=reference|pe_start sets the default at init):
+ *   SHMEMX_ORDER_REFERENCE (default) = every PE receives the result the
+ *       reference computes on THAT PE: its own source first, then the others
+ *       in ascending active-set order (reduce-op.c:226-264). Where the order
+ *       matters (floating-point sum/prod from 3 PEs, floating-point min/max
+ *       from 2: rounding, NaN and +-0 selects) the owner of each shard folds it
+ *       in every member's order in one pass over the sources and each PE
+ *       gathers its own version: the same xGMI traffic as the shard schedule,
+ *       plus (N-1)/N of the message written to local HBM.
+ *   SHMEMX_ORDER_PE_START = every PE receives PE_start's result (identical bits
+ *       on all PEs, the plain shard schedule).
+ * Integer and bitwise reductions are order-independent: both give the same. */
+enum shmemx_reduce_order {
+    SHMEMX_ORDER_REFERENCE = 0,
+    SHMEMX_ORDER_PE_START = 1
+};
+int shmemx_set_reduce_order (int order); /* returns the previous one */
+int shmemx_get_reduce_order (void);
 
 /* Device and timing helpers (used by bench.py and the tests). */
 int shmemx_device_id (void);                 /* HIP ordinal of this PE's GPU */
@@ -80,8 +100,8 @@ int shmemx_rccl_init (double timeout_s);
  * one-block device barriers), so a call can be captured into a HIP graph and
  * replayed; every replay is one more collective for all members.
  *   - target and source lie in the device symmetric heap, equal or disjoint
- *   - PE_size <= 32; P2P schedule (results identical on all members, equal
- *     to the reference's on PE_start) whatever the reduce algorithm setting
+ *   - PE_size <= 32; P2P schedule whatever the reduce algorithm setting,
+ *     delivering the result order set by shmemx_set_reduce_order
  *   - every member issues the same sequence of collectives, host-side and
  *     stream-ordered interleaved in the same order; one PE's stream-ordered
  *     calls run one at a time: one stream, or streams the caller orders

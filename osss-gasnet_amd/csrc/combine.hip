@@ -183,6 +183,86 @@ __global__ __launch_bounds__(kBlock) void combine_scalar(CombineParams p) {
     signal_done(p.sig, true);
 }
 
+// Every member's reference order in one pass (mi355_combine_orders). On
+// member q the reference folds its OWN source first and then the others in
+// active-set order (reduce-op.c:226-264), so for order-sensitive operators (FP
+// rounding; the NaN and +-0 selects of min/max) the members' results differ.
+// The owner of a shard loads the NSRC sources once and computes every fold
+// from registers: dst[q] = fold(src[q], src[0], .., src[q-1], src[q+1], ..).
+// A null dst[q] skips fold q (a kernel argument: the branch is uniform).
+struct OrdersParams {
+    void *dst[kMaxSrc];
+    const void *src[kMaxSrc];
+    uint64_t nvec;  // as CombineParams
+    uint32_t tail;
+    uint32_t head;
+    Signal sig;
+};
+
+template <int OP, typename T, int NSRC>
+__device__ __forceinline__ void orders_element(const OrdersParams &p, int64_t i) {
+    T v[NSRC];
+#pragma unroll
+    for (int k = 0; k < NSRC; ++k) v[k] = ((const T *)p.src[k])[i];
+#pragma unroll
+    for (int q = 0; q < NSRC; ++q) {
+        if (p.dst[q] == nullptr) continue;
+        T acc = v[q];
+#pragma unroll
+        for (int k = 0; k < NSRC; ++k)
+            if (k != q) acc = apply<OP>(acc, v[k]);
+        ((T *)p.dst[q])[i] = acc;
+    }
+}
+
+template <int OP, typename T, int NSRC, int UNROLL, int POL>
+__global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
+    constexpr int V = 16 / sizeof(T);
+    const uint64_t nvec = p.nvec;
+    const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
+    for (uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x; base < nvec;
+         base += step) {
+        Pack<T> x[UNROLL][NSRC];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = base + (uint64_t)u * kBlock;
+            if (i < nvec) {
+#pragma unroll
+                for (int k = 0; k < NSRC; ++k) x[u][k].v = ld16<POL>((const u32x4 *)p.src[k] + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = base + (uint64_t)u * kBlock;
+            if (i >= nvec) continue;
+#pragma unroll
+            for (int q = 0; q < NSRC; ++q) {
+                if (p.dst[q] == nullptr) continue;
+                Pack<T> acc = x[u][q];
+#pragma unroll
+                for (int k = 0; k < NSRC; ++k) {
+                    if (k == q) continue;
+#pragma unroll
+                    for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[u][k].e[e]);
+                }
+                st16((u32x4 *)p.dst[q] + i, acc.v);
+            }
+        }
+    }
+    const bool tail_block = V > 1 && p.tail != 0 && blockIdx.x == 0;
+    if (tail_block && threadIdx.x < p.tail) orders_element<OP, T, NSRC>(p, (int64_t)(nvec * V + threadIdx.x));
+    const bool head_block = V > 1 && p.head != 0 && blockIdx.x == 0;
+    if (head_block && threadIdx.x < p.head) orders_element<OP, T, NSRC>(p, (int64_t)threadIdx.x - (int64_t)p.head);
+    signal_done(p.sig, tail_block || head_block);
+}
+
+template <int OP, typename T, int NSRC>
+__global__ __launch_bounds__(kBlock) void combine_orders_scalar(OrdersParams p) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < p.nvec; i += (uint64_t)gridDim.x * kBlock)
+        orders_element<OP, T, NSRC>(p, (int64_t)i);
+    signal_done(p.sig, true);
+}
+
 // Byte copy of up to NS segments in one launch; blockIdx.y = segment. NS = 1
 // (the 1-PE identity, the bench's call) keeps the kernel arguments at 48
 // bytes instead of 1.5 KiB for the 64-segment form (the all-gather leg).
@@ -371,38 +451,59 @@ template <int NSRC, typename T> struct Shape {
     static constexpr int policy = POL_NT_LOAD;
 };
 
+// mi355_combine_orders: NSRC loads and up to NSRC stores per vector (every
+// member's fold); the loads in flight per lane are those of the fold of the
+// same width. Complex types: one vector per lane (NSRC*(NSRC-1) complex
+// products per vector do not fit the registers of deeper unrolling; the
+// loads in flight come from more blocks instead).
+template <int NSRC, typename T> struct OrdersShape {
+    static constexpr bool cplx = std::is_same<T, cplxf>::value || std::is_same<T, cplxd>::value;
+    using S = Shape<NSRC, T>;
+    static constexpr int unroll = cplx ? 1 : S::unroll;
+    static constexpr int blocks_per_cu = cplx ? (S::blocks_per_cu * S::unroll < 8 ? S::blocks_per_cu * S::unroll : 8)
+                                              : S::blocks_per_cu;
+    static constexpr int policy = POL_NT_LOAD;
+};
+
+// How a launch over these pointers can run as 16-byte vectors: 0 = every
+// pointer aligned; h > 0 = every pointer equally misaligned by whole elements
+// (a user offset into the arrays): fold the first h elements element-wise and
+// the rest as vectors from the advanced pointers (peeled to a 128-byte line
+// when all share the misalignment within the line, else to 16 bytes); -1 =
+// element-wise kernel.
+template <typename T>
+long vector_head(const void *const *ptrs, int np, size_t n) {
+    constexpr int V = 16 / sizeof(T);
+    uintptr_t orbits = 0;
+    for (int k = 0; k < np; ++k) orbits |= (uintptr_t)ptrs[k];
+    if ((orbits & 15) == 0) return 0;
+    if (V == 1) return -1;
+    uintptr_t mis = (uintptr_t)ptrs[0] & 127;
+    bool line = true;
+    for (int k = 1; k < np; ++k) line = line && ((uintptr_t)ptrs[k] & 127) == mis;
+    if (!line) mis &= 15;
+    bool same = mis % sizeof(T) == 0;
+    for (int k = 1; k < np; ++k) same = same && ((uintptr_t)ptrs[k] & (line ? 127 : 15)) == mis;
+    const size_t head = ((line ? 128 : 16) - mis) / sizeof(T);
+    return same && n > head ? (long)head : -1;
+}
+
 template <int OP, typename T, int NSRC>
 int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, bool final) {
     CombineParams p{};
+    const void *ptrs[kMaxSrc + 1];
     p.dst = dst;
-    uintptr_t orbits = (uintptr_t)dst;
-    for (int k = 0; k < NSRC; ++k) {
-        p.src[k] = srcs[k];
-        orbits |= (uintptr_t)srcs[k];
-    }
+    ptrs[0] = dst;
+    for (int k = 0; k < NSRC; ++k) p.src[k] = ptrs[1 + k] = srcs[k];
     constexpr int V = 16 / sizeof(T);
-    // every pointer equally misaligned by whole elements (a user offset into
-    // the arrays): the first `head` elements are folded element-wise and the
-    // rest as 16-byte vectors from the advanced, aligned pointers
-    if ((orbits & 15) != 0 && V > 1) {
-        // all equally misaligned within a 128-byte line: peel to the line
-        // (whole-line accesses); else within 16 bytes: peel to 16
-        uintptr_t mis = (uintptr_t)dst & 127;
-        bool line = true;
-        for (int k = 0; k < NSRC; ++k) line = line && ((uintptr_t)srcs[k] & 127) == mis;
-        if (!line) mis &= 15;
-        bool same = mis % sizeof(T) == 0;
-        for (int k = 0; k < NSRC; ++k) same = same && ((uintptr_t)srcs[k] & (line ? 127 : 15)) == mis;
-        const size_t head = ((line ? 128 : 16) - mis) / sizeof(T);
-        if (same && n > head) {
+    const long head = vector_head<T>(ptrs, NSRC + 1, n);
+    if (head >= 0) {
+        if (head > 0) {
             p.head = (uint32_t)head;
             p.dst = (char *)dst + head * sizeof(T);
             for (int k = 0; k < NSRC; ++k) p.src[k] = (const char *)srcs[k] + head * sizeof(T);
-            n -= head;
-            orbits = 0;
+            n -= (size_t)head;
         }
-    }
-    if ((orbits & 15) == 0) {
         using S = Shape<NSRC, T>;
         p.nvec = n / V;
         p.tail = (uint32_t)(n % V);
@@ -413,6 +514,40 @@ int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, b
     p.tail = 0;
     const unsigned grid = grid_for((uint64_t)kBlock * 4, n);
     return launch(combine_scalar<OP, T, NSRC>, dim3(grid), st, p, final);
+}
+
+// mi355_combine_orders for NSRC <= kMaxSrc sources: one launch
+template <int OP, typename T, int NSRC>
+int launch_orders_fixed(void *const *dsts, const void *const *srcs, size_t n, hipStream_t st) {
+    OrdersParams p{};
+    const void *ptrs[2 * kMaxSrc];
+    int np = 0;
+    for (int k = 0; k < NSRC; ++k) {
+        p.src[k] = ptrs[np++] = srcs[k];
+        p.dst[k] = dsts[k];
+        if (dsts[k] != nullptr) ptrs[np++] = dsts[k];
+    }
+    constexpr int V = 16 / sizeof(T);
+    const long head = vector_head<T>(ptrs, np, n);
+    if (head >= 0) {
+        if (head > 0) {
+            p.head = (uint32_t)head;
+            for (int k = 0; k < NSRC; ++k) {
+                p.src[k] = (const char *)srcs[k] + head * sizeof(T);
+                if (dsts[k] != nullptr) p.dst[k] = (char *)dsts[k] + head * sizeof(T);
+            }
+            n -= (size_t)head;
+        }
+        using S = OrdersShape<NSRC, T>;
+        p.nvec = n / V;
+        p.tail = (uint32_t)(n % V);
+        const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, S::blocks_per_cu);
+        return launch(combine_orders_vec<OP, T, NSRC, S::unroll, S::policy>, dim3(grid), st, p);
+    }
+    p.nvec = n;
+    p.tail = 0;
+    const unsigned grid = grid_for((uint64_t)kBlock * 4, n);
+    return launch(combine_orders_scalar<OP, T, NSRC>, dim3(grid), st, p);
 }
 
 template <int OP, typename T>
@@ -431,14 +566,15 @@ int launch_n(int nsrc, void *dst, const void *const *srcs, size_t n, hipStream_t
 }
 
 // Left fold of any number of sources: first kMaxSrc into dst, then dst
-// stays the accumulator (first operand) of every following launch.
+// stays the accumulator (first operand) of every following launch. `final`:
+// the last launch carries the armed completion signal.
 template <int OP, typename T>
-int launch_fold(void *dst, const void *const *srcs, int nsrc, size_t n, hipStream_t st) {
+int launch_fold(void *dst, const void *const *srcs, int nsrc, size_t n, hipStream_t st, bool final = true) {
     if constexpr (!valid_pair<OP, T>()) {
         return MI355_E_UNSUP;
     } else {
         int first = nsrc < kMaxSrc ? nsrc : kMaxSrc;
-        int rc = launch_n<OP, T>(first, dst, srcs, n, st, first == nsrc);
+        int rc = launch_n<OP, T>(first, dst, srcs, n, st, final && first == nsrc);
         int done = first;
         while (rc == 0 && done < nsrc) {
             const void *chunk[kMaxSrc];
@@ -446,7 +582,7 @@ int launch_fold(void *dst, const void *const *srcs, int nsrc, size_t n, hipStrea
             int take = nsrc - done < kMaxSrc - 1 ? nsrc - done : kMaxSrc - 1;
             for (int k = 0; k < take; ++k) chunk[1 + k] = srcs[done + k];
             done += take;
-            rc = launch_n<OP, T>(1 + take, dst, chunk, n, st, done == nsrc);
+            rc = launch_n<OP, T>(1 + take, dst, chunk, n, st, final && done == nsrc);
         }
         return rc;
     }
@@ -462,6 +598,61 @@ int dispatch_op(int op, void *dst, const void *const *srcs, int nsrc, size_t n, 
     case MI355_OP_XOR: return launch_fold<MI355_OP_XOR, T>(dst, srcs, nsrc, n, st);
     case MI355_OP_MIN: return launch_fold<MI355_OP_MIN, T>(dst, srcs, nsrc, n, st);
     case MI355_OP_MAX: return launch_fold<MI355_OP_MAX, T>(dst, srcs, nsrc, n, st);
+    default: return MI355_E_INVAL;
+    }
+}
+
+// Every member's order (mi355_combine_orders): one launch up to kMaxSrc
+// sources. Beyond that, each member's fold is its own multi-launch left fold
+// in that member's order; a fold whose target is its own source (in place)
+// runs last, since the other folds still read that source.
+template <int OP, typename T>
+int launch_orders(void *const *dsts, const void *const *srcs, int nsrc, size_t n, hipStream_t st) {
+    if constexpr (!valid_pair<OP, T>()) {
+        return MI355_E_UNSUP;
+    } else {
+        switch (nsrc) {
+        case 2: return launch_orders_fixed<OP, T, 2>(dsts, srcs, n, st);
+        case 3: return launch_orders_fixed<OP, T, 3>(dsts, srcs, n, st);
+        case 4: return launch_orders_fixed<OP, T, 4>(dsts, srcs, n, st);
+        case 5: return launch_orders_fixed<OP, T, 5>(dsts, srcs, n, st);
+        case 6: return launch_orders_fixed<OP, T, 6>(dsts, srcs, n, st);
+        case 7: return launch_orders_fixed<OP, T, 7>(dsts, srcs, n, st);
+        case 8: return launch_orders_fixed<OP, T, 8>(dsts, srcs, n, st);
+        default: break;
+        }
+        int alias = -1, last = -1;
+        for (int q = 0; q < nsrc; ++q) {
+            if (dsts[q] == nullptr) continue;
+            if (dsts[q] == srcs[q]) alias = q;
+            else last = q;
+        }
+        const int final_q = alias >= 0 ? alias : last;
+        const void *order[MI355_ORDERS_MAX_SOURCES];
+        int rc = 0;
+        for (int j = 0; j <= nsrc && rc == 0; ++j) {
+            const int q = j < nsrc ? j : alias;  // the in-place fold, if any, after all others
+            if (q < 0 || dsts[q] == nullptr || (j < nsrc && q == alias)) continue;
+            order[0] = srcs[q];
+            int m = 1;
+            for (int k = 0; k < nsrc; ++k)
+                if (k != q) order[m++] = srcs[k];
+            rc = launch_fold<OP, T>(dsts[q], order, nsrc, n, st, q == final_q);
+        }
+        return rc;
+    }
+}
+
+template <typename T>
+int dispatch_orders(int op, void *const *dsts, const void *const *srcs, int nsrc, size_t n, hipStream_t st) {
+    switch (op) {
+    case MI355_OP_SUM: return launch_orders<MI355_OP_SUM, T>(dsts, srcs, nsrc, n, st);
+    case MI355_OP_PROD: return launch_orders<MI355_OP_PROD, T>(dsts, srcs, nsrc, n, st);
+    case MI355_OP_AND: return launch_orders<MI355_OP_AND, T>(dsts, srcs, nsrc, n, st);
+    case MI355_OP_OR: return launch_orders<MI355_OP_OR, T>(dsts, srcs, nsrc, n, st);
+    case MI355_OP_XOR: return launch_orders<MI355_OP_XOR, T>(dsts, srcs, nsrc, n, st);
+    case MI355_OP_MIN: return launch_orders<MI355_OP_MIN, T>(dsts, srcs, nsrc, n, st);
+    case MI355_OP_MAX: return launch_orders<MI355_OP_MAX, T>(dsts, srcs, nsrc, n, st);
     default: return MI355_E_INVAL;
     }
 }
@@ -496,11 +687,23 @@ static int combine_impl(int op, int dtype, void *dst, const void *const *srcs, i
                         void *stream);
 static int copy_segments_impl(void *const *dsts, const void *const *srcs, const size_t *nbytes, int nseg,
                               void *stream);
+static int combine_orders_impl(int op, int dtype, void *const *dsts, const void *const *srcs, int nsrc, size_t n,
+                               void *stream);
 
 // Every error return cancels an armed signal/timing request (nothing carries them).
 extern "C" int mi355_combine(int op, int dtype, void *dst, const void *const *srcs, int nsrc,
                              size_t n, void *stream) {
     const int rc = combine_impl(op, dtype, dst, srcs, nsrc, n, stream);
+    if (rc != 0) {
+        t_sig = Signal{nullptr, nullptr, 0};
+        t_ev_start = t_ev_stop = nullptr;
+    }
+    return rc;
+}
+
+extern "C" int mi355_combine_orders(int op, int dtype, void *const *dsts, const void *const *srcs, int nsrc,
+                                    size_t n, void *stream) {
+    const int rc = combine_orders_impl(op, dtype, dsts, srcs, nsrc, n, stream);
     if (rc != 0) {
         t_sig = Signal{nullptr, nullptr, 0};
         t_ev_start = t_ev_stop = nullptr;
@@ -545,6 +748,40 @@ static int combine_impl(int op, int dtype, void *dst, const void *const *srcs, i
     case MI355_LONGDOUBLE: return dispatch_op<x80>(op, dst, srcs, nsrc, n, st);
     case MI355_COMPLEXF: return dispatch_op<cplxf>(op, dst, srcs, nsrc, n, st);
     case MI355_COMPLEXD: return dispatch_op<cplxd>(op, dst, srcs, nsrc, n, st);
+    default: return MI355_E_INVAL;
+    }
+}
+
+static int combine_orders_impl(int op, int dtype, void *const *dsts, const void *const *srcs, int nsrc, size_t n,
+                               void *stream) {
+    if (!mi355_op_supported(op, dtype)) return MI355_E_UNSUP;
+    if (nsrc < 1 || nsrc > MI355_ORDERS_MAX_SOURCES || dsts == nullptr || srcs == nullptr) return MI355_E_INVAL;
+    int ndst = 0, nalias = 0;
+    for (int k = 0; k < nsrc; ++k) {
+        if (srcs[k] == nullptr) return MI355_E_INVAL;
+        if (dsts[k] != nullptr) {
+            ++ndst;
+            if (dsts[k] == srcs[k]) ++nalias;
+        }
+    }
+    // beyond one launch's sources the folds run one after another: only one may be in place
+    if (nsrc > kMaxSrc && nalias > 1) return MI355_E_INVAL;
+    hipStream_t st = (hipStream_t)stream;
+    if (n == 0 || ndst == 0) {
+        fire_on_host(st);
+        return 0;
+    }
+    if (nsrc == 1) return combine_impl(op, dtype, dsts[0], srcs, 1, n, stream);
+    switch (dtype) {
+    case MI355_SHORT: return dispatch_orders<int16_t>(op, dsts, srcs, nsrc, n, st);
+    case MI355_INT: return dispatch_orders<int32_t>(op, dsts, srcs, nsrc, n, st);
+    case MI355_LONG:
+    case MI355_LONGLONG: return dispatch_orders<int64_t>(op, dsts, srcs, nsrc, n, st);
+    case MI355_FLOAT: return dispatch_orders<float>(op, dsts, srcs, nsrc, n, st);
+    case MI355_DOUBLE: return dispatch_orders<double>(op, dsts, srcs, nsrc, n, st);
+    case MI355_LONGDOUBLE: return dispatch_orders<x80>(op, dsts, srcs, nsrc, n, st);
+    case MI355_COMPLEXF: return dispatch_orders<cplxf>(op, dsts, srcs, nsrc, n, st);
+    case MI355_COMPLEXD: return dispatch_orders<cplxd>(op, dsts, srcs, nsrc, n, st);
     default: return MI355_E_INVAL;
     }
 }

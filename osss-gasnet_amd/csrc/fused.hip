@@ -14,10 +14,14 @@
 //            acquires at system scope (invalidates this CU's stale lines)
 //   reduce   fold shard `me` of every member's source, in active-set order
 //            (the reference's PE_start order), into this PE's target shard,
-//            with system-scope write-through stores
+//            with system-scope write-through stores -- or (ordered) in EVERY
+//            member's reference order (own source first, reduce-op.c:226-264):
+//            this PE's version into its target, member q's into slot q of
+//            this PE's version area, from which q gathers it
 //   rsdone   the last block of the grid publishes RSDONE[my PE] to every
 //            member; every block waits for all members' RSDONE, acquires
-//   gather   copy the other members' shards from their targets
+//   gather   copy the other members' shards from their targets (ordered:
+//            this PE's version of them from their version areas)
 //   agdone   the last block publishes AGDONE, waits for every member's AGDONE
 //            (nobody reads this PE's buffers any more) and stores the call's
 //            epoch to the host-coherent flag
@@ -36,6 +40,7 @@
 // Every wait is bounded by p.timeout_ticks of the 100 MHz real-time counter.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 
 #include "ops.h"
 
@@ -157,6 +162,105 @@ __device__ void block_copy(void *dst, const void *src, uint64_t nbytes, unsigned
     block_drain(block_copy_issue(dst, src, nbytes, bi, nblocks));
 }
 
+// Member at position j of the fold order that starts with member `first`
+// and continues with the others in member order (first = 0: member order;
+// first = q: member q's reference order, reduce-op.c:226-264).
+__device__ __forceinline__ int order_member(int j, int first) {
+    return j == 0 ? first : (j - 1 < first ? j - 1 : j);
+}
+
+// Vector v of the shard starting at element lo, folded over every member in
+// the order starting with `first`. kBatch members' vectors are loaded before
+// any is folded, so their (xGMI) latencies overlap instead of adding up.
+template <int OP, typename T>
+__device__ __forceinline__ Pack<T> fold_vec(const MI355FusedArgs &a, uint64_t lo, uint64_t v, int first) {
+    constexpr int V = 16 / sizeof(T);
+    const int nm = a.nmembers;
+    Pack<T> acc;
+    for (int k0 = 0; k0 < nm; k0 += kBatch) {
+        Pack<T> x[kBatch];
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j)
+            if (k0 + j < nm)
+                x[j].v = ((const u32x4 *)((const char *)a.src[order_member(k0 + j, first)] + lo * sizeof(T)))[v];
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) {
+            if (k0 + j >= nm) break;
+            if (k0 + j == 0) {
+                acc = x[0];
+            } else {
+#pragma unroll
+                for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[j].e[e]);
+            }
+        }
+    }
+    return acc;
+}
+
+template <int OP, typename T>
+__device__ __forceinline__ T fold_elem(const MI355FusedArgs &a, uint64_t i, int first) {
+    const int nm = a.nmembers;
+    T acc;
+    for (int k0 = 0; k0 < nm; k0 += kBatch) {
+        T x[kBatch];
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j)
+            if (k0 + j < nm) x[j] = ((const T *)a.src[order_member(k0 + j, first)])[i];
+#pragma unroll
+        for (int j = 0; j < kBatch; ++j) {
+            if (k0 + j >= nm) break;
+            acc = k0 + j == 0 ? x[0] : apply<OP>(acc, x[j]);
+        }
+    }
+    return acc;
+}
+
+// Where member q's version of element r of this PE's shard goes: its target
+// shard for q == me, else slot (q < me ? q : q - 1) of this PE's version area.
+template <typename T>
+__device__ __forceinline__ T *version_elem(const MI355FusedArgs &a, int q, uint64_t r) {
+    if (q == a.me) return (T *)a.dst[a.me] + (uint64_t)a.me * a.shard + r;
+    return (T *)((char *)a.ver[a.me] + (uint64_t)(q < a.me ? q : q - 1) * a.shard * sizeof(T)) + r;
+}
+
+// Vector v of shard `me` in EVERY member's reference order. Up to kBatch
+// members the sources are loaded once and all folds come from registers;
+// beyond that (and for the software x87 type, whose fold is long code) one
+// fold per member re-reads the vectors (cache hits after the first).
+template <int OP, typename T>
+__device__ __forceinline__ void versions_vec(const MI355FusedArgs &a, uint64_t lo, uint64_t v) {
+    constexpr int V = 16 / sizeof(T);
+    const int nm = a.nmembers;
+    if constexpr (!std::is_same<T, x80>::value) {
+        if (nm <= kBatch) {
+            Pack<T> x[kBatch];
+#pragma unroll
+            for (int j = 0; j < kBatch; ++j)
+                if (j < nm) x[j].v = ((const u32x4 *)((const char *)a.src[j] + lo * sizeof(T)))[v];
+#pragma unroll
+            for (int q = 0; q < kBatch; ++q) {
+                if (q >= nm) break;
+                Pack<T> acc = x[q];
+#pragma unroll
+                for (int k = 0; k < kBatch; ++k) {
+                    if (k >= nm) break;
+                    if (k == q) continue;
+#pragma unroll
+                    for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[k].e[e]);
+                }
+                st16_sys((u32x4 *)version_elem<T>(a, q, v * V), acc.v);
+            }
+            return;
+        }
+    }
+    // this PE's own version last: in place (dst == src) it overwrites the
+    // source vector the other folds still read
+    for (int j = 0; j < nm; ++j) {
+        const int q = j < a.me ? j : j + 1 < nm ? j + 1 : a.me;
+        st16_sys((u32x4 *)version_elem<T>(a, q, v * V), fold_vec<OP, T>(a, lo, v, q).v);
+    }
+}
+
 template <int OP, typename T>
 __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
     constexpr int V = 16 / sizeof(T);
@@ -193,55 +297,34 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
     {
         // ---- fold: one-shot = the whole array from every member's source
         // (no reduce-scatter/all-gather split, one flag exchange fewer);
-        // otherwise shard `me` (the reduce-scatter leg)
+        // otherwise shard `me` (the reduce-scatter leg). Ordered one-shot
+        // folds in this PE's own reference order; ordered two-shot computes
+        // every member's order of shard `me` (versions_vec).
         const bool oneshot = a.oneshot != 0;
+        const bool versions = a.ordered != 0 && !oneshot;
+        const int first = a.ordered != 0 && oneshot ? a.me : 0;
         bool tail_plain = false;
         const uint64_t lo = oneshot ? 0 : (uint64_t)a.me * a.shard;
         const uint64_t hi = oneshot ? a.n : (lo + a.shard < a.n ? lo + a.shard : a.n);
         if (hi > lo) {
             const uint64_t nv = (hi - lo) / V;
-            const int nm = a.nmembers;
             u32x4 *d = (u32x4 *)((char *)a.dst[a.me] + lo * sizeof(T));
             for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < nv;
                  v += (uint64_t)gridDim.x * kBlock) {
-                // kBatch members' vectors are loaded before any is folded, so
-                // their (xGMI) latencies overlap instead of adding up; the
-                // fold itself stays in member order
-                Pack<T> acc;
-                for (int k0 = 0; k0 < nm; k0 += kBatch) {
-                    Pack<T> x[kBatch];
-#pragma unroll
-                    for (int j = 0; j < kBatch; ++j)
-                        if (k0 + j < nm) x[j].v = ((const u32x4 *)((const char *)a.src[k0 + j] + lo * sizeof(T)))[v];
-#pragma unroll
-                    for (int j = 0; j < kBatch; ++j) {
-                        if (k0 + j >= nm) break;
-                        if (k0 + j == 0) {
-                            acc = x[0];
-                        } else {
-#pragma unroll
-                            for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[j].e[e]);
-                        }
-                    }
-                }
-                st16_sys(d + v, acc.v);
+                if (versions) versions_vec<OP, T>(a, lo, v);
+                else st16_sys(d + v, fold_vec<OP, T>(a, lo, v, first).v);
             }
             const uint64_t tail0 = lo + nv * V;
             if (tail0 < hi && blockIdx.x == 0 && threadIdx.x < hi - tail0) {
                 const uint64_t i = tail0 + threadIdx.x;
-                T acc;
-                for (int k0 = 0; k0 < nm; k0 += kBatch) {
-                    T x[kBatch];
-#pragma unroll
-                    for (int j = 0; j < kBatch; ++j)
-                        if (k0 + j < nm) x[j] = ((const T *)a.src[k0 + j])[i];
-#pragma unroll
-                    for (int j = 0; j < kBatch; ++j) {
-                        if (k0 + j >= nm) break;
-                        acc = k0 + j == 0 ? x[0] : apply<OP>(acc, x[j]);
+                if (!versions) {
+                    ((T *)a.dst[a.me])[i] = fold_elem<OP, T>(a, i, first);
+                } else {
+                    for (int j = 0; j < a.nmembers; ++j) {  // own version last (in place, as versions_vec)
+                        const int q = j < a.me ? j : j + 1 < a.nmembers ? j + 1 : a.me;
+                        *version_elem<T>(a, q, i - lo) = fold_elem<OP, T>(a, i, q);
                     }
                 }
-                ((T *)a.dst[a.me])[i] = acc;
             }
             if (tail0 < hi && blockIdx.x == 0) {
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -257,20 +340,26 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
             __syncthreads();
             if (!ok_all) goto fail;
 
-            // ---- gather the other shards: one grid-stride loop over all of them
+            // ---- gather the other shards: one grid-stride loop over all of
+            // them, from their owners' targets, or (ordered) from the slot of
+            // this PE's version in the owners' version areas
             const uint64_t shard_v = a.shard / V;  // a.shard is a multiple of V
             const uint64_t total_v = shard_v * (uint64_t)a.nmembers;
             for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < total_v;
                  g += (uint64_t)gridDim.x * kBlock) {
                 const int j = (int)(g / shard_v);
                 if (j == a.me) continue;
-                const uint64_t e0 = (uint64_t)j * a.shard + (g - (uint64_t)j * shard_v) * V;
+                const uint64_t r0 = (g - (uint64_t)j * shard_v) * V;  // element within shard j
+                const uint64_t e0 = (uint64_t)j * a.shard + r0;
                 if (e0 >= a.n) continue;
+                const T *from = versions ? (const T *)((const char *)a.ver[j] +
+                                                       (uint64_t)(a.me < j ? a.me : a.me - 1) * a.shard * sizeof(T)) - e0 + r0
+                                         : (const T *)a.dst[j];
                 if (e0 + V <= a.n) {
-                    const u32x4 v = *(const u32x4 *)((const char *)a.dst[j] + e0 * sizeof(T));
+                    const u32x4 v = *(const u32x4 *)(from + e0);
                     st16_sys((u32x4 *)((char *)a.dst[a.me] + e0 * sizeof(T)), v);
                 } else {
-                    for (uint64_t e = e0; e < a.n; ++e) ((T *)a.dst[a.me])[e] = ((const T *)a.dst[j])[e];
+                    for (uint64_t e = e0; e < a.n; ++e) ((T *)a.dst[a.me])[e] = from[e];
                     tail_plain = true;
                 }
             }
@@ -452,6 +541,9 @@ extern "C" int mi355_fused_allreduce(const MI355FusedArgs *a, void *stream) {
             a->pe[i] >= MI355_SIG_RSDONE)
             return MI355_E_INVAL;
     if (a->oneshot && a->src[a->me] == a->dst[a->me]) return MI355_E_INVAL;  // it overwrites dst while peers read src
+    if (a->ordered && !a->oneshot)
+        for (int i = 0; i < a->nmembers; ++i)
+            if (a->ver[i] == nullptr || ((uintptr_t)a->ver[i] & 15) != 0) return MI355_E_INVAL;
     // enough blocks for the larger of the two legs (one-shot: the whole
     // array), all of them co-resident
     const uint64_t vecs = a->oneshot ? (a->n * es + 15) / 16 : (a->shard * es / 16) * (uint64_t)(a->nmembers - 1);

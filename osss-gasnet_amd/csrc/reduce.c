@@ -12,11 +12,17 @@
  *
  *   P2P (default)  split the nreduce elements into PE_size contiguous shards
  *                  (256-byte aligned); PE i folds shard i of every member's
- *                  source, in active-set order, into its own target shard;
- *                  barrier; PE i gathers the other shards from the members'
- *                  targets. Every PE gets the same bits, which equal the
- *                  reference's result on PE_start (whose fold order is the
- *                  ascending active-set order).
+ *                  source into its own target shard; barrier; PE i gathers
+ *                  the other shards from the members' targets. Result order
+ *                  (shmemx.h): where the reference's members disagree
+ *                  (floating point; see ordered_pair), PE i folds shard i in
+ *                  EVERY member's reference order at once -- own source first,
+ *                  then the others ascending (:226-264) -- keeps its own
+ *                  version and leaves member q's in slot q of its version
+ *                  area, from which q gathers it: every PE ends with the
+ *                  reference's result for itself. Elsewhere (and with
+ *                  SHMEM_REDUCE_ORDER=pe_start) every PE gets PE_start's
+ *                  result, the fold in ascending active-set order.
  *   EXACT          every PE folds the full arrays in ITS reference order
  *                  (own source first, then the others ascending): bit-identical
  *                  to the reference on every PE, at PE_size x the xGMI reads.
@@ -111,6 +117,62 @@ void mi355_shard_bounds (size_t n, size_t es, int size, int i, size_t *lo, size_
 }
 
 /* ---------------------------------------------------------------------- */
+/* result order (shmemx.h, SHMEMX_ORDER_REFERENCE)                          */
+/* ---------------------------------------------------------------------- */
+/* The reference's members disagree on this reduction: floating point (the
+ * integer and bitwise operators wrap, select identical bits or are exact, so
+ * any order gives the same bits), and either 3+ members (the rounding follows
+ * the order) or min/max (`a < b ? a : b` picks by position when a NaN or a
+ * +-0 pair is involved, reduce-op.c:138-150, from 2 members on). Two-member
+ * sum/prod agree: IEEE (and x87, and the Annex G complex multiply) a + b and
+ * a * b are commutative, NaN payloads aside. */
+static int order_sensitive (int op, int dtype, int size)
+{
+    if (shmemi.order != SHMEMX_ORDER_REFERENCE || size < 2)
+        return 0;
+    if (dtype != MI355_FLOAT && dtype != MI355_DOUBLE && dtype != MI355_LONGDOUBLE && dtype != MI355_COMPLEXF &&
+        dtype != MI355_COMPLEXD)
+        return 0;
+    return size > 2 || op == MI355_OP_MIN || op == MI355_OP_MAX;
+}
+
+/* The shard schedules deliver every member's order up to
+ * MI355_ORDERS_MAX_SOURCES members (mi355_combine_orders); larger
+ * order-sensitive active sets run the EXACT schedule instead. */
+static int ordered_pair (int op, int dtype, int size)
+{
+    return order_sensitive (op, dtype, size) && size <= MI355_ORDERS_MAX_SOURCES;
+}
+
+/* Version areas: on every PE, one per signal-region channel, (size - 1)
+ * slots of one shard each; slot s of owner i holds member q's version of
+ * shard i, s = q < i ? q : q - 1. Each slot starts at the target's offset
+ * within 256 bytes, so the gather copies run as aligned vectors. */
+static size_t ver_slot_bytes (size_t n, size_t es, int size)
+{
+    const size_t b = shard_chunk (n, es, size) * es;
+    return (b + 255) / 256 * 256 + 256;
+}
+
+static size_t ver_off (int chan, int owner, int q, size_t slot_bytes, size_t dst_off)
+{
+    return shmemi.order_off + (size_t) chan * shmemi.order_chunk + (size_t) (q < owner ? q : q - 1) * slot_bytes +
+           (dst_off & 255);
+}
+
+/* Elements per round of an ordered P2P reduction: the largest message whose
+ * versions fit one channel's version area (longer messages run in rounds). */
+static size_t ordered_round_elems (size_t es, int size)
+{
+    const size_t align = es >= 256 ? 1 : 256 / es;
+    const size_t per_slot = shmemi.order_chunk / (size_t) (size - 1);
+    if (per_slot < 512 + align * es)
+        shmemi_fatal ("SHMEM_DEVICE_ORDER_SIZE (%zu bytes per channel) is too small for %d PEs", shmemi.order_chunk,
+                      size);
+    return (per_slot - 512) / es / align * align * (size_t) size;
+}
+
+/* ---------------------------------------------------------------------- */
 /* device-resident schedules on symmetric heap offsets                     */
 /* ---------------------------------------------------------------------- */
 
@@ -172,37 +234,51 @@ void shmemi_dev_barrier (int PE_start, int stride, int PE_size, int me, int last
         shmemi_fatal ("device barrier timed out waiting for the other PEs of the active set");
 }
 
-/* P2P shard schedule, dst and src disjoint or identical, with the three
- * barriers as one-block device-barrier kernels on the library stream: five
- * launches queued back to back, one host wait (the last barrier carries the
- * completion flag). The first barrier also orders the sources: each PE's
- * arrival is stream-ordered after its caller's work. */
-static void p2p_range_dev (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
-                           const struct aset *s)
+/* The reduce-scatter leg: fold this PE's shard of every member's source
+ * into its target shard -- in member order, or (ordered) in every member's
+ * reference order with the other members' versions going to this PE's
+ * version area on channel `chan`. Returns the launch's status (0: queued, or
+ * nothing to do: empty shard). */
+static int fold_shard (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n, const struct aset *s,
+                       int ordered, int chan, hipStream_t st)
 {
-    MI355FusedArgs a;
-    member_args (&a, s, SHMEMI_CHAN_HOST);
-    const void *sp[MI355_FUSED_MAX_MEMBERS];
-    void *dsts[MI355_FUSED_MAX_MEMBERS];
-    size_t nb[MI355_FUSED_MAX_MEMBERS];
+    const void *sp[MI355_FUSED_MAX_MEMBERS > MI355_ORDERS_MAX_SOURCES ? MI355_FUSED_MAX_MEMBERS
+                                                                       : MI355_ORDERS_MAX_SOURCES];
     size_t lo, hi;
     mi355_shard_bounds (n, es, s->size, s->me, &lo, &hi);
-
-    device_barrier (&a, shmemi.stream); /* every source is ready */
-    if (hi > lo) {
-        shmemi_peer_acquire (shmemi.stream);
-        for (int i = 0; i < s->size; ++i)
-            sp[i] = shmemi_peer_ptr (a.pe[i], src_off + lo * es);
-        shmemi_timed_begin ();
-        const int rc = mi355_combine (op, dtype, shmemi_peer_ptr (shmemi.mype, dst_off + lo * es), sp, s->size,
-                                      hi - lo, shmemi.stream);
-        shmemi_timed_end ();
-        if (rc != 0)
-            shmemi_fatal ("combine kernel launch failed (op %d, dtype %d, %d sources, %zu elements): %d", op,
-                          dtype, s->size, hi - lo, rc);
+    if (hi <= lo)
+        return 0;
+    const void **spp = sp;
+    if (s->size > (int) (sizeof sp / sizeof sp[0])) {
+        spp = (const void **) malloc (sizeof (void *) * (size_t) s->size);
+        if (spp == NULL)
+            shmemi_fatal ("out of host memory");
     }
-    device_barrier (&a, shmemi.stream); /* every shard is reduced */
-    shmemi_peer_acquire (shmemi.stream);
+    for (int i = 0; i < s->size; ++i)
+        spp[i] = shmemi_peer_ptr (aset_pe (s, i), src_off + lo * es);
+    void *dst = shmemi_peer_ptr (shmemi.mype, dst_off + lo * es);
+    int rc;
+    if (!ordered) {
+        rc = mi355_combine (op, dtype, dst, spp, s->size, hi - lo, st);
+    } else {
+        void *dsts[MI355_ORDERS_MAX_SOURCES];
+        const size_t slot = ver_slot_bytes (n, es, s->size);
+        for (int q = 0; q < s->size; ++q)
+            dsts[q] = q == s->me ? dst : shmemi_peer_ptr (shmemi.mype, ver_off (chan, s->me, q, slot, dst_off));
+        rc = mi355_combine_orders (op, dtype, dsts, spp, s->size, hi - lo, st);
+    }
+    if (spp != sp)
+        free (spp);
+    return rc;
+}
+
+/* The all-gather leg's segments: the other members' shards, from their
+ * targets, or (ordered) this PE's version of them from their version areas.
+ * Returns the number of segments (arrays of s->size entries). */
+static int gather_segments (size_t es, size_t dst_off, size_t n, const struct aset *s, int ordered, int chan,
+                            void **dsts, const void **sp, size_t *nb)
+{
+    const size_t slot = ver_slot_bytes (n, es, s->size);
     int k = 0;
     for (int i = 0; i < s->size; ++i) {
         size_t l, h;
@@ -210,13 +286,42 @@ static void p2p_range_dev (int op, int dtype, size_t es, size_t dst_off, size_t 
         if (i == s->me || h <= l)
             continue;
         dsts[k] = shmemi_peer_ptr (shmemi.mype, dst_off + l * es);
-        sp[k] = shmemi_peer_ptr (a.pe[i], dst_off + l * es);
+        sp[k] = ordered ? shmemi_peer_ptr (aset_pe (s, i), ver_off (chan, i, s->me, slot, dst_off))
+                        : shmemi_peer_ptr (aset_pe (s, i), dst_off + l * es);
         nb[k] = (h - l) * es;
         ++k;
     }
+    return k;
+}
+
+/* P2P shard schedule, dst and src disjoint or identical, with the three
+ * barriers as one-block device-barrier kernels on the library stream: five
+ * launches queued back to back, one host wait (the last barrier carries the
+ * completion flag). The first barrier also orders the sources: each PE's
+ * arrival is stream-ordered after its caller's work. */
+static void p2p_range_dev (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
+                           const struct aset *s, int ordered)
+{
+    MI355FusedArgs a;
+    member_args (&a, s, SHMEMI_CHAN_HOST);
+    void *dsts[MI355_FUSED_MAX_MEMBERS];
+    const void *sp[MI355_FUSED_MAX_MEMBERS];
+    size_t nb[MI355_FUSED_MAX_MEMBERS];
+
+    device_barrier (&a, shmemi.stream); /* every source is ready */
+    shmemi_peer_acquire (shmemi.stream);
+    shmemi_timed_begin ();
+    int rc = fold_shard (op, dtype, es, dst_off, src_off, n, s, ordered, SHMEMI_CHAN_HOST, shmemi.stream);
+    shmemi_timed_end ();
+    if (rc != 0)
+        shmemi_fatal ("combine kernel launch failed (op %d, dtype %d, %d sources, %zu elements): %d", op, dtype,
+                      s->size, n, rc);
+    device_barrier (&a, shmemi.stream); /* every shard is reduced */
+    shmemi_peer_acquire (shmemi.stream);
+    const int k = gather_segments (es, dst_off, n, s, ordered, SHMEMI_CHAN_HOST, dsts, sp, nb);
     if (k > 0) {
         shmemi_timed_begin_phase (1);
-        const int rc = mi355_copy_segments (dsts, sp, nb, k, shmemi.stream);
+        rc = mi355_copy_segments (dsts, sp, nb, k, shmemi.stream);
         shmemi_timed_end ();
         if (rc != 0)
             shmemi_fatal ("copy kernel launch failed: %d", rc);
@@ -244,13 +349,14 @@ static void host_order (void)
 
 /* P2P shard schedule (host barriers), dst and src disjoint or identical. */
 static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
-                       const struct aset *s)
+                       const struct aset *s, int ordered)
 {
     const void **sp = (const void **) malloc (sizeof (void *) * (size_t) s->size);
     void **dsts = (void **) malloc (sizeof (void *) * (size_t) s->size);
     size_t *nb = (size_t *) malloc (sizeof (size_t) * (size_t) s->size);
     if (sp == NULL || dsts == NULL || nb == NULL)
         shmemi_fatal ("out of host memory");
+
     size_t lo, hi;
     mi355_shard_bounds (n, es, s->size, s->me, &lo, &hi);
 
@@ -258,27 +364,20 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
     shmemi_barrier_set (s->start, s->stride, s->size); /* every source is ready */
     if (hi > lo) {
         shmemi_peer_acquire (shmemi.stream);
-        for (int i = 0; i < s->size; ++i)
-            sp[i] = shmemi_peer_ptr (aset_pe (s, i), src_off + lo * es);
-        combine_wait (op, dtype, shmemi_peer_ptr (shmemi.mype, dst_off + lo * es), sp, s->size, hi - lo, 1);
+        shmemi_timed_begin ();
+        shmemi_arm_signal ();
+        int rc = fold_shard (op, dtype, es, dst_off, src_off, n, s, ordered, SHMEMI_CHAN_HOST, shmemi.stream);
+        shmemi_timed_end ();
+        if (rc != 0)
+            shmemi_fatal ("combine kernel launch failed (op %d, dtype %d, %d sources, %zu elements): %d", op,
+                          dtype, s->size, n, rc);
+        shmemi_wait_signal ();
     }
     shmemi_barrier_set (s->start, s->stride, s->size); /* every shard is reduced */
     shmemi_peer_acquire (shmemi.stream);
 
-    /* gather the other members' shards from their targets: one launch */
-    int k = 0;
-    for (int i = 0; i < s->size; ++i) {
-        if (i == s->me)
-            continue;
-        size_t l, h;
-        mi355_shard_bounds (n, es, s->size, i, &l, &h);
-        if (h <= l)
-            continue;
-        dsts[k] = shmemi_peer_ptr (shmemi.mype, dst_off + l * es);
-        sp[k] = shmemi_peer_ptr (aset_pe (s, i), dst_off + l * es);
-        nb[k] = (h - l) * es;
-        ++k;
-    }
+    /* gather the other members' shards: one launch */
+    const int k = gather_segments (es, dst_off, n, s, ordered, SHMEMI_CHAN_HOST, dsts, sp, nb);
     copy_wait (dsts, sp, nb, k, 1);
     shmemi_barrier_set (s->start, s->stride, s->size); /* peers are done reading us */
     free (nb);
@@ -286,28 +385,50 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
     free (sp);
 }
 
+/* The multi-launch P2P schedule over [0, n): one round, or (ordered, when the
+ * versions outgrow the version area) several, each a complete schedule. */
 static void p2p_any (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n, const struct aset *s)
 {
-    if (device_flags_ok (s)) {
-        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: P2P shards, device barriers (%zu elements, %d members)", n,
-                      s->size);
-        p2p_range_dev (op, dtype, es, dst_off, src_off, n, s);
-    } else {
-        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: P2P shards, host barriers (%zu elements, %d members)", n,
-                      s->size);
-        p2p_range (op, dtype, es, dst_off, src_off, n, s);
-    }
+    const int ordered = ordered_pair (op, dtype, s->size);
+    const int dev = device_flags_ok (s);
+    const size_t round = ordered ? ordered_round_elems (es, s->size) : n;
+    SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: P2P shards, %s barriers, %s (%zu elements, %d members%s)",
+                  dev ? "device" : "host", ordered ? "every member's reference order" : "PE_start order", n, s->size,
+                  ordered && n > round ? ", several rounds" : "");
+    size_t b = 0;
+    do {
+        const size_t cn = n - b < round ? n - b : round;
+        if (dev)
+            p2p_range_dev (op, dtype, es, dst_off + b * es, src_off + b * es, cn, s, ordered);
+        else
+            p2p_range (op, dtype, es, dst_off + b * es, src_off + b * es, cn, s, ordered);
+        b += cn;
+    } while (b < n);
 }
 
 /* The fused one-launch schedule (fused.hip) applies: small enough, few
- * enough members, 16-byte aligned symmetric offsets, dst == src or disjoint. */
-static int fused_eligible (size_t es, size_t dst_off, size_t src_off, size_t n, const struct aset *s)
+ * enough members, 16-byte aligned symmetric offsets, dst == src or disjoint,
+ * and (ordered) the versions fit the version area. */
+static int fused_eligible (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
+                           const struct aset *s)
 {
     return s->size > 1 && s->size <= MI355_FUSED_MAX_MEMBERS && n * es <= shmemi.fused_max &&
            shmemi.npes <= MI355_SIG_RSDONE &&
            shmemi.sigmem != NULL && ((dst_off | src_off) & 15) == 0 && es <= 256 &&
            (dst_off == src_off || !ranges_overlap (dst_off, src_off, n * es)) &&
-           shmemi.algorithm != SHMEMX_REDUCE_EXACT;
+           shmemi.algorithm != SHMEMX_REDUCE_EXACT &&
+           (!ordered_pair (op, dtype, s->size) ||
+            (size_t) (s->size - 1) * shard_chunk (n, es, s->size) * es <= shmemi.order_chunk);
+}
+
+/* The fused kernel's result order: ordered two-shot calls read and write the
+ * members' version areas of channel `chan` (mi355_reduce.h). */
+static void fused_order (MI355FusedArgs *a, const struct aset *s, int chan)
+{
+    a->ordered = ordered_pair (a->op, a->dtype, s->size);
+    if (a->ordered && !a->oneshot)
+        for (int i = 0; i < s->size; ++i)
+            a->ver[i] = shmemi_peer_ptr (aset_pe (s, i), shmemi.order_off + (size_t) chan * shmemi.order_chunk);
 }
 
 /* host_src/host_dst: device-accessible page-locked host buffers of this PE
@@ -315,8 +436,9 @@ static int fused_eligible (size_t es, size_t dst_off, size_t src_off, size_t n, 
 static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
                          const struct aset *s, const void *host_src, void *host_dst)
 {
-    SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: fused one-launch P2P, %s (%zu elements, %d members)%s",
-                  n * es <= shmemi.oneshot_max && dst_off != src_off ? "one-shot" : "reduce-scatter + all-gather", n,
+    SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: fused one-launch P2P, %s, %s (%zu elements, %d members)%s",
+                  n * es <= shmemi.oneshot_max && dst_off != src_off ? "one-shot" : "reduce-scatter + all-gather",
+                  ordered_pair (op, dtype, s->size) ? "every member's reference order" : "PE_start order", n,
                   s->size, host_src != NULL ? ", staging host buffers in-kernel" : "");
     MI355FusedArgs a;
     memset (&a, 0, sizeof a);
@@ -340,6 +462,7 @@ static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t sr
     a.host_src = host_src;
     a.host_dst = host_dst;
     a.oneshot = n * es <= shmemi.oneshot_max && dst_off != src_off;
+    fused_order (&a, s, SHMEMI_CHAN_HOST);
     const int rc = mi355_fused_allreduce (&a, shmemi.stream);
     if (rc != 0)
         shmemi_fatal ("fused reduction launch failed (op %d, dtype %d, %d PEs, %zu elements): %d", op, dtype,
@@ -381,7 +504,10 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
                               const struct aset *s)
 {
     const size_t nbytes = n * es;
-    const int exact = shmemi.algorithm == SHMEMX_REDUCE_EXACT;
+    /* EXACT by request, or for an order-sensitive set too large for the
+     * shard schedules' every-order fold (ordered_pair) */
+    const int exact = shmemi.algorithm == SHMEMX_REDUCE_EXACT ||
+                      (order_sensitive (op, dtype, s->size) && !ordered_pair (op, dtype, s->size));
     const int same = dst_off == src_off;
     if (s->size > 1 && shmemi.p2p_broken)
         shmemi_fatal ("peer GPU memory reads failed the init self-test; only the RCCL pairs "
@@ -400,7 +526,7 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
             return;
         }
     } else if (!exact && (same || !overlap)) {
-        if (fused_eligible (es, dst_off, src_off, n, s))
+        if (fused_eligible (op, dtype, es, dst_off, src_off, n, s))
             fused_range (op, dtype, es, dst_off, src_off, n, s, NULL, NULL);
         else
             p2p_any (op, dtype, es, dst_off, src_off, n, s);
@@ -576,7 +702,7 @@ static int local_direct (int op, int dtype, void *target, const void *source, si
     if (nbytes > SHMEMI_SMALL_LOCAL_MAX || nbytes > half)
         return 0;
     const size_t a_off = shmemi.scratch_off, b_off = shmemi.scratch_off + shmemi.scratch_chunk;
-    if (!fused_eligible (es, b_off, a_off, n, s))
+    if (!fused_eligible (op, dtype, es, b_off, a_off, n, s))
         return 0;
     fused_range (op, dtype, es, b_off, a_off, n, s, hs, ht);
     return 1;
@@ -759,7 +885,12 @@ static void reduce_on_stream (int op, int dtype, const char *fn, void *target, c
         const size_t dst_off = shmemi_heap_offset (target), src_off = shmemi_heap_offset (source);
         MI355FusedArgs a;
         member_args (&a, &s, SHMEMI_CHAN_STREAM);
-        if (n * es <= shmemi.fused_max && ((dst_off | src_off) & 15) == 0 && es <= 256) {
+        const int ordered = ordered_pair (op, dtype, s.size);
+        if (order_sensitive (op, dtype, s.size) && !ordered)
+            shmemi_fatal ("%s: %d PEs: the stream-ordered schedules deliver each PE's reference order up to %d "
+                          "PEs (set SHMEM_REDUCE_ORDER=pe_start)", fn, s.size, MI355_ORDERS_MAX_SOURCES);
+        if (n * es <= shmemi.fused_max && ((dst_off | src_off) & 15) == 0 && es <= 256 &&
+            (!ordered || (size_t) (s.size - 1) * shard_chunk (n, es, s.size) * es <= shmemi.order_chunk)) {
             a.op = op;
             a.dtype = dtype;
             a.n = n;
@@ -769,45 +900,29 @@ static void reduce_on_stream (int op, int dtype, const char *fn, void *target, c
                 a.dst[i] = shmemi_peer_ptr (a.pe[i], dst_off);
             }
             a.oneshot = n * es <= shmemi.oneshot_max && dst_off != src_off;
+            fused_order (&a, &s, SHMEMI_CHAN_STREAM);
             const int rc = mi355_fused_allreduce (&a, st);
             if (rc != 0)
                 shmemi_fatal ("%s: fused reduction launch failed: %d", fn, rc);
         } else {
-            const void **sp = (const void **) malloc (sizeof (void *) * (size_t) s.size);
-            void **dsts = (void **) malloc (sizeof (void *) * (size_t) s.size);
-            size_t *nb = (size_t *) malloc (sizeof (size_t) * (size_t) s.size);
-            if (sp == NULL || dsts == NULL || nb == NULL)
-                shmemi_fatal ("out of host memory");
-            size_t lo, hi;
-            mi355_shard_bounds (n, es, s.size, s.me, &lo, &hi);
-            stream_barrier (fn, &s, st); /* every source is ready */
-            if (hi > lo) {
+            void *dsts[MI355_FUSED_MAX_MEMBERS];
+            const void *sp[MI355_FUSED_MAX_MEMBERS];
+            size_t nb[MI355_FUSED_MAX_MEMBERS];
+            const size_t round = ordered ? ordered_round_elems (es, s.size) : n;
+            for (size_t b = 0; b < n; b += round) {
+                const size_t cn = n - b < round ? n - b : round;
+                const size_t d0 = dst_off + b * es, s0 = src_off + b * es;
+                stream_barrier (fn, &s, st); /* every source is ready */
                 shmemi_peer_acquire (st);
-                for (int i = 0; i < s.size; ++i)
-                    sp[i] = shmemi_peer_ptr (a.pe[i], src_off + lo * es);
-                const int rc = mi355_combine (op, dtype, shmemi_peer_ptr (shmemi.mype, dst_off + lo * es), sp,
-                                              s.size, hi - lo, st);
+                const int rc = fold_shard (op, dtype, es, d0, s0, cn, &s, ordered, SHMEMI_CHAN_STREAM, st);
                 if (rc != 0)
                     shmemi_fatal ("%s: combine kernel launch failed: %d", fn, rc);
+                stream_barrier (fn, &s, st); /* every shard is reduced */
+                shmemi_peer_acquire (st);
+                const int k = gather_segments (es, d0, cn, &s, ordered, SHMEMI_CHAN_STREAM, dsts, sp, nb);
+                stream_copy (fn, dsts, sp, nb, k, st);
+                stream_barrier (fn, &s, st); /* peers are done reading this target and version area */
             }
-            stream_barrier (fn, &s, st); /* every shard is reduced */
-            shmemi_peer_acquire (st);
-            int k = 0;
-            for (int i = 0; i < s.size; ++i) {
-                size_t l, h;
-                mi355_shard_bounds (n, es, s.size, i, &l, &h);
-                if (i == s.me || h <= l)
-                    continue;
-                dsts[k] = shmemi_peer_ptr (shmemi.mype, dst_off + l * es);
-                sp[k] = shmemi_peer_ptr (a.pe[i], dst_off + l * es);
-                nb[k] = (h - l) * es;
-                ++k;
-            }
-            stream_copy (fn, dsts, sp, nb, k, st);
-            stream_barrier (fn, &s, st); /* peers are done reading this target */
-            free (nb);
-            free (dsts);
-            free (sp);
         }
     }
 }

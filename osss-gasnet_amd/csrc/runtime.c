@@ -141,6 +141,13 @@ static size_t env_size (const char *name, size_t dflt)
 
 static size_t round_up (size_t x, size_t a) { return (x + a - 1) / a * a; }
 
+static int parse_order (const char *v)
+{
+    if (v == NULL || strcasecmp (v, "reference") == 0 || strcasecmp (v, "pe") == 0) return SHMEMX_ORDER_REFERENCE;
+    if (strcasecmp (v, "pe_start") == 0 || strcasecmp (v, "uniform") == 0) return SHMEMX_ORDER_PE_START;
+    shmemi_fatal ("unknown SHMEM_REDUCE_ORDER=\"%s\" (reference|pe_start)", v);
+}
+
 static int parse_algorithm (const char *v)
 {
     if (v == NULL || strcasecmp (v, "auto") == 0) return SHMEMX_REDUCE_AUTO;
@@ -323,7 +330,14 @@ static void heap_init (void)
         scratch = 3 * 65536;
     shmemi.scratch_off = shmemi.user_size;
     shmemi.scratch_chunk = scratch / 3 / SHMEMI_ALIGN * SHMEMI_ALIGN;
-    shmemi.heap_size = shmemi.user_size + scratch;
+    /* version areas of the per-PE-order P2P schedule (reduce.c), one per
+     * signal-region channel (host-launched / stream-ordered calls) */
+    size_t order = round_up (env_size ("SHMEM_DEVICE_ORDER_SIZE", (size_t) 512 << 20), 2 * SHMEMI_ALIGN);
+    if (order < 2 * 65536)
+        order = 2 * 65536;
+    shmemi.order_off = shmemi.scratch_off + scratch;
+    shmemi.order_chunk = order / 2 / SHMEMI_ALIGN * SHMEMI_ALIGN;
+    shmemi.heap_size = shmemi.user_size + scratch + order;
     void *p = NULL;
     hipError_t e = hipMalloc (&p, shmemi.heap_size);
     if (e != hipSuccess)
@@ -799,6 +813,7 @@ void pshmem_init (void)
     static const char *es_env[] = {"SHMEM_ENTRY_SYNC", NULL};
     shmemi.entry_sync = (int) env_long (es_env, 0);
     shmemi.algorithm = parse_algorithm (getenv ("SHMEM_REDUCE_ALGORITHM"));
+    shmemi.order = parse_order (getenv ("SHMEM_REDUCE_ORDER"));
 
     /* test hook: bring up PEs, barriers and the host heap without a GPU (CPU
      * tests of the bootstrap); every reduction then aborts, there is no CPU path */
@@ -861,13 +876,15 @@ void pshmem_init (void)
         static const char *const alg[] = {"auto", "p2p", "exact", "rccl"};
         SHMEMI_TRACE (SHMEMI_LOG_INIT, "%s: PE %d of %d on GPU %d (%s)", SHMEMX_VERSION_STRING, shmemi.mype,
                       shmemi.npes, shmemi.device, bus);
-        SHMEMI_TRACE (SHMEMI_LOG_INIT, "device heap %zu bytes (user %zu, scratch 3 x %zu), signal region %s",
-                      shmemi.heap_size, shmemi.user_size, shmemi.scratch_chunk,
+        SHMEMI_TRACE (SHMEMI_LOG_INIT,
+                      "device heap %zu bytes (user %zu, scratch 3 x %zu, version areas 2 x %zu), signal region %s",
+                      shmemi.heap_size, shmemi.user_size, shmemi.scratch_chunk, shmemi.order_chunk,
                       shmemi.sig_broken ? "off (self-test failed)" : "on");
         SHMEMI_TRACE (SHMEMI_LOG_INIT,
-                      "reduce algorithm %s, fused path up to %zu bytes, peer heap reads %s, peer L2 acquire %s",
-                      alg[shmemi.algorithm & 3], shmemi.fused_max, shmemi.p2p_broken ? "FAILED (RCCL)" : "ok",
-                      shmemi.peer_acquire ? "on" : "off");
+                      "reduce algorithm %s, result order %s, fused path up to %zu bytes, peer heap reads %s, "
+                      "peer L2 acquire %s",
+                      alg[shmemi.algorithm & 3], shmemi.order == SHMEMX_ORDER_REFERENCE ? "reference (per PE)" : "PE_start",
+                      shmemi.fused_max, shmemi.p2p_broken ? "FAILED (RCCL)" : "ok", shmemi.peer_acquire ? "on" : "off");
     }
     shmemi_trace_show_info ();
     static int registered = 0;
@@ -1044,6 +1061,17 @@ int shmemx_set_reduce_algorithm (int algorithm)
 }
 
 int shmemx_get_reduce_algorithm (void) { return shmemi.algorithm; }
+
+int shmemx_set_reduce_order (int order)
+{
+    if (order != SHMEMX_ORDER_REFERENCE && order != SHMEMX_ORDER_PE_START)
+        shmemi_fatal ("shmemx_set_reduce_order(%d): unknown order", order);
+    int old = shmemi.order;
+    shmemi.order = order;
+    return old;
+}
+
+int shmemx_get_reduce_order (void) { return shmemi.order; }
 
 int shmemx_device_id (void) { return shmemi.initialized ? shmemi.device : -1; }
 

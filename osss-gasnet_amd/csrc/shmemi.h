@@ -67,6 +67,7 @@ struct shmemi_state {
     hipStream_t stream_in, stream_out;  /* staging copies (blocking streams) */
     hipEvent_t ev_in[2], ev_out[2];
     int algorithm;              /* enum shmemx_reduce_algorithm */
+    int order;                  /* enum shmemx_reduce_order */
     double barrier_timeout;     /* seconds */
     int debug;
     int entry_sync;             /* SHMEM_ENTRY_SYNC: hipDeviceSynchronize on entry */
@@ -86,6 +87,8 @@ struct shmemi_state {
     size_t user_size;           /* user part */
     size_t scratch_off;         /* = user_size */
     size_t scratch_chunk;       /* bytes per staging buffer (3 buffers) */
+    size_t order_off;           /* version areas of the per-PE-order schedule: 2 channels after scratch */
+    size_t order_chunk;         /* bytes per channel */
     char **peer_heap;           /* [npes]: mapped base of every PE's heap */
     struct shmemi_block *blocks;
 

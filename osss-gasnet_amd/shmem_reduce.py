@@ -22,6 +22,7 @@ NP = {
     "complexf": np.complex64, "complexd": np.complex128,
 }
 ALGORITHMS = {"auto": 0, "p2p": 1, "exact": 2, "rccl": 3}          # enum shmemx_reduce_algorithm
+ORDERS = {"reference": 0, "pe_start": 1}                            # enum shmemx_reduce_order
 SHMEM_REDUCE_SYNC_SIZE = 128
 SHMEM_REDUCE_MIN_WRKDATA_SIZE = 64
 SHMEM_SYNC_VALUE = -1
@@ -46,6 +47,7 @@ def load(path=LIB_PATH):
         "shmemx_malloc_device": ([_sz], _vp), "shmemx_free_device": ([_vp], None),
         "shmemx_is_device_symmetric": ([_vp], _i),
         "shmemx_set_reduce_algorithm": ([_i], _i), "shmemx_get_reduce_algorithm": ([], _i),
+        "shmemx_set_reduce_order": ([_i], _i), "shmemx_get_reduce_order": ([], _i),
         "shmemx_device_id": ([], _i), "shmemx_device_synchronize": ([], None),
         "shmemx_peer_link": ([_i, ctypes.POINTER(_i), ctypes.POINTER(_i)], _i),
         "shmemx_memcpy": ([_vp, _vp, _sz], None), "shmemx_wtime": ([], ctypes.c_double),
@@ -57,6 +59,7 @@ def load(path=LIB_PATH):
                                               ctypes.POINTER(ctypes.c_double)], None),
         "mi355_dtype_size": ([_i], _sz), "mi355_op_supported": ([_i, _i], _i),
         "mi355_combine": ([_i, _i, _vp, ctypes.POINTER(_vp), _i, _sz, _vp], _i),
+        "mi355_combine_orders": ([_i, _i, ctypes.POINTER(_vp), ctypes.POINTER(_vp), _i, _sz, _vp], _i),
         "mi355_copy_segments": ([ctypes.POINTER(_vp), ctypes.POINTER(_vp), ctypes.POINTER(_sz), _i, _vp], _i),
         "mi355_shard_bounds": ([_sz, _sz, _i, _i, ctypes.POINTER(_sz), ctypes.POINTER(_sz)], None),
     }
@@ -115,6 +118,10 @@ class Shmem:
 
     def set_algorithm(self, name):
         return self.lib.shmemx_set_reduce_algorithm(ALGORITHMS[name])
+
+    def set_order(self, name):
+        """"reference": every PE gets the reference's result for itself; "pe_start": PE_start's everywhere"""
+        return self.lib.shmemx_set_reduce_order(ORDERS[name])
 
     def sync(self):
         self.lib.shmemx_device_synchronize()
@@ -194,6 +201,12 @@ class Shmem:
     def combine(self, op, dtype, dst, srcs, n, stream=None):
         arr = (_vp * len(srcs))(*srcs)
         return self.lib.mi355_combine(OPS.index(op), DTYPES.index(dtype), dst, arr, len(srcs), n, stream)
+
+    def combine_orders(self, op, dtype, dsts, srcs, n, stream=None):
+        """dsts[q] (or None) <- the fold in member q's reference order (mi355_combine_orders)"""
+        d = (_vp * len(dsts))(*[x if x else None for x in dsts])
+        s = (_vp * len(srcs))(*srcs)
+        return self.lib.mi355_combine_orders(OPS.index(op), DTYPES.index(dtype), d, s, len(srcs), n, stream)
 
     def kernel_timing(self, enable):
         self.lib.shmemx_kernel_timing(1 if enable else 0)

@@ -122,6 +122,7 @@ def run_stream(shm, c, me, da, db, results):
         if me in members(*s):
             mine = s
     if mine is not None:
+        shm.set_order(c.get("order", "reference"))
         bufs = [base + i * stride + off * es for i in range(k + 1)]
         st = shm.stream_create()
 
@@ -236,7 +237,11 @@ def main():
             continue
         op, dtype, n = c["op"], c["dtype"], c["n"]
         es = np.dtype(shmem_reduce.NP[dtype]).itemsize
-        x = source(op, dtype, n, c["seed"], me)
+        if "golden" in c:  # the committed fixture's inputs (tests/golden/), member i's row
+            g = np.load(os.path.join(HERE, "golden", f"golden_{op}_{dtype}.npz"))
+            x = np.ascontiguousarray(g[f"in_{c['golden']}"][members(*mine).index(me)])
+        else:
+            x = source(op, dtype, n, c["seed"], me)
         mode = c["mode"]
         if mode == "dev":
             src, dst = da, db
@@ -275,6 +280,7 @@ def main():
             else:
                 shm.put(src, x)
         shm.set_algorithm(c.get("algorithm", "auto"))
+        shm.set_order(c.get("order", "reference"))
         if c.get("api") == "fortran":
             fortran_to_all(shm, op, dtype, dst, src, n, *mine)
         else:

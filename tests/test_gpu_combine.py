@@ -72,6 +72,59 @@ def test_combine_reproduces_every_pe_of_golden(shm, dev, op, dtype):
         dev.free()
 
 
+def gpu_orders(shm, dev, op, dtype, srcs, offset_elems=0, skip=(), inplace=None):
+    """mi355_combine_orders: member q's reference order into dst q (None for q in skip);
+    inplace = q: dst q is src q itself. Returns {q: result}."""
+    n = len(srcs[0])
+    es = np.dtype(oracle.NP[dtype]).itemsize
+    pad = np.zeros(offset_elems, dtype=oracle.NP[dtype])
+    sp = [dev.upload(np.concatenate([pad, s])) + offset_elems * es for s in srcs]
+    dp = []
+    for q in range(len(srcs)):
+        if q in skip:
+            dp.append(None)
+        elif q == inplace:
+            dp.append(sp[q])
+        else:
+            dp.append(dev.empty((n + offset_elems) * es) + offset_elems * es)
+    rc = shm.combine_orders(op, dtype, dp, sp, n)
+    assert rc == 0, rc
+    shm.sync()
+    return {q: shm.get(d, n, dtype) for q, d in enumerate(dp) if d is not None}
+
+
+@pytest.mark.parametrize("op,dtype", oracle.PAIRS)
+def test_combine_orders_reproduces_every_pe_of_golden(shm, dev, op, dtype):
+    """One launch over the golden sources yields every member's reference
+    result (the owner-computes-every-order fold of the P2P schedule)."""
+    for npes, ins, outs in load_cases(op, dtype):
+        if ins.shape[1] == 0 or npes < 2:
+            continue
+        got = gpu_orders(shm, dev, op, dtype, [ins[i] for i in range(npes)])
+        for me in range(npes):
+            assert_match(got[me], outs[me], op, dtype, ctx=f"golden npes={npes} me={me}")
+        dev.free()
+
+
+@pytest.mark.parametrize("op,dtype", [("sum", "double"), ("max", "float"), ("min", "double"), ("prod", "complexd"),
+                                      ("sum", "longdouble"), ("xor", "short")])
+@pytest.mark.parametrize("nsrc", [2, 3, 8, 9, 13, 32])
+def test_combine_orders_any_number_of_sources(shm, dev, op, dtype, nsrc):
+    """Up to 8 sources in one launch, beyond that one left fold per member;
+    one member in place, one skipped, element tails, user offsets."""
+    import gen_golden
+    rng = np.random.default_rng(100 + nsrc)
+    n = 2051
+    srcs = [gen_golden.values(rng, op, dtype, n) for _ in range(nsrc)]
+    want = oracle.reduce_all(op, dtype, srcs)
+    for off, skip, inplace in ((0, (), None), (1, (nsrc - 1,), 0), (3, (0,), nsrc - 1)):
+        got = gpu_orders(shm, dev, op, dtype, srcs, offset_elems=off, skip=skip, inplace=inplace)
+        assert sorted(got) == [q for q in range(nsrc) if q not in skip]
+        for q, g in got.items():
+            assert_match(g, want[q], op, dtype, ctx=f"nsrc={nsrc} off={off} member {q}")
+        dev.free()
+
+
 @pytest.mark.parametrize("op,dtype", [("sum", "double"), ("xor", "int"), ("max", "float"), ("prod", "complexf"),
                                       ("min", "longdouble"), ("sum", "short")])
 @pytest.mark.parametrize("nsrc", [1, 2, 5, 8, 9, 12, 17])

@@ -2,9 +2,10 @@
 
 Inputs follow SURVEY.md §8(d) (tests/_configs.py); PEs share this box's one
 GPU (8 PE processes for the 8-GPU configs: same kernels and IPC mappings,
-without xGMI). Every PE's whole target is compared with the oracle's result on
-PE_start through a SHA-256 of its bytes (the P2P schedule is bit-exact there;
-these inputs hold no NaNs), with a strided sample kept for diagnostics.
+without xGMI). Every PE's whole target is compared with the oracle's result
+for THAT PE (the reference's own-source-first order, which the default result
+order delivers) through a SHA-256 of its bytes, with a strided sample kept for
+diagnostics.
 """
 import numpy as np
 import pytest
@@ -16,16 +17,16 @@ from test_gpu_multipe import run_pes
 pytestmark = [pytest.mark.gpu, pytest.mark.multipe]
 
 
-def want_digest(config, n, npes, slot=0):
+def want_digest(config, n, npes, slot=0, pe=0):
     op, dtype = _configs.CONFIGS[config]
     srcs = [_configs.source(config, n, p, slot) for p in range(npes)]
-    return _configs.digest(oracle.reduce_pe(op, dtype, srcs, 0))
+    return _configs.digest(oracle.reduce_pe(op, dtype, srcs, pe))
 
 
 def check(results, c, npes):
     for k in range(c.get("slots", 1)):
-        h, sample = want_digest(c["config"], c["n"], npes, k)
         for pe in range(npes):
+            h, sample = want_digest(c["config"], c["n"], npes, k, pe)
             got_h = bytes(results[pe][f"{c['id']}_{k}_sha"]).hex()
             if got_h != h:
                 got = results[pe][f"{c['id']}_{k}_sample"]

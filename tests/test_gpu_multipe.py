@@ -6,8 +6,11 @@ across GPUs (the xGMI case differs only in where the bytes travel). Each run
 starts N pe_worker.py processes from this (not yet GPU-initialised) pytest
 process, then checks every PE's target against the oracle:
 
-  P2P   every member's result == the reference's result on PE_start
-        (bit-exact, NaN-payloads aside), i.e. identical on all members
+  P2P   member i's result == the reference's result on member i
+        (bit-exact, NaN payloads aside): the default result order
+        (SHMEM_REDUCE_ORDER=reference) folds every member's order for the
+        order-sensitive pairs; with order "pe_start" every member's result
+        == the reference's result on PE_start
   EXACT member i's result == the reference's result on member i
 """
 import itertools
@@ -73,19 +76,19 @@ def check(results, cases):
         for s in c["sets"]:
             mem = members(*s)
             srcs = [source(op, dtype, n, c["seed"], pe) for pe in mem]
+            per_pe = c.get("algorithm") == "exact" or c.get("order", "reference") == "reference"
             for i, pe in enumerate(mem):
                 got = results[pe][str(c["id"])]
-                exact = c.get("algorithm") == "exact"
-                want = oracle.reduce_pe(op, dtype, srcs, i if exact else 0)
+                want = oracle.reduce_pe(op, dtype, srcs, i if per_pe else 0)
                 assert_match(got, want, op, dtype, ctx=f"case {c['id']} {c['mode']} {c.get('algorithm')} "
-                                                        f"set {s} PE {pe}:")
+                                                        f"{c.get('order', 'reference')} set {s} PE {pe}:")
 
 
-def make_cases(pairs, n, sets, mode, algorithm, start_id, seed=11):
+def make_cases(pairs, n, sets, mode, algorithm, start_id, seed=11, order="reference"):
     out = []
     for k, (op, dtype) in enumerate(pairs):
         out.append({"id": start_id + k, "op": op, "dtype": dtype, "n": n, "sets": sets, "mode": mode,
-                    "algorithm": algorithm, "seed": seed + start_id + k})
+                    "algorithm": algorithm, "seed": seed + start_id + k, "order": order})
     return out
 
 
@@ -105,9 +108,77 @@ def test_four_pes_all_44_pairs_p2p_and_exact(tmp_path, fused_max, oneshot_max):
     cases += make_cases(oracle.PAIRS, 1000, [[0, 0, 4]], "inplace", "p2p", 200)  # in place: never one-shot
     cases += make_cases(SOME, 9, [[0, 0, 4]], "dev", "p2p", 300)      # less than one 16-byte vector per element type
     cases += make_cases(SOME, 4099, [[1, 0, 3]], "dev", "p2p", 400)  # several blocks and an element tail
+    cases += make_cases(oracle.PAIRS, 1000, [[0, 0, 4]], "dev", "p2p", 500, order="pe_start")
+    cases += make_cases(SOME, 4099, [[0, 0, 4]], "inplace", "p2p", 600, order="pe_start")
     results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_FUSED_MAX_BYTES": fused_max,
                                                      "SHMEM_ONESHOT_MAX_BYTES": oneshot_max})
     check(results, cases)
+
+
+GOLDEN_ROWS = json.load(open(os.path.join(HERE, "golden", "manifest.json")))["cases"]
+
+
+@pytest.mark.parametrize("fused_max,oneshot_max", [("1M", "64K"), ("1M", "0"), ("0", "0")],
+                         ids=["fused-oneshot", "fused-twoshot", "multi-launch"])
+def test_golden_fixtures_on_every_pe(tmp_path, fused_max, oneshot_max):
+    """The committed golden vectors (outputs of the reference's own compiled
+    operators in each member's fold order, NaN / +-0 / Inf / x87 encodings
+    included) through the public entry points on 2-8 PE processes: member i's
+    target must equal the fixture's row i for every one of the 44 pairs, on the
+    one-shot, two-shot and multi-launch schedules."""
+    import gen_golden  # noqa: F401  (same fixtures as tests/golden)
+    cases, cid = [], 0
+    for op, dtype in oracle.PAIRS:
+        for k, row in enumerate(GOLDEN_ROWS[f"{op}_{dtype}"]):
+            if row["npes"] < 2 or row["n"] == 0:
+                continue
+            cases.append({"id": cid, "op": op, "dtype": dtype, "n": row["n"], "sets": [[0, 0, row["npes"]]],
+                          "mode": "dev", "algorithm": "p2p", "seed": 0, "golden": k})
+            cid += 1
+    results = run_pes(8, cases, tmp_path, extra_env={"SHMEM_FUSED_MAX_BYTES": fused_max,
+                                                     "SHMEM_ONESHOT_MAX_BYTES": oneshot_max})
+    for c in cases:
+        g = np.load(os.path.join(HERE, "golden", f"golden_{c['op']}_{c['dtype']}.npz"))
+        outs = g[f"out_{c['golden']}"]
+        for i in range(c["sets"][0][2]):
+            assert_match(results[i][str(c["id"])], outs[i], c["op"], c["dtype"],
+                         ctx=f"golden {c['op']}/{c['dtype']} case {c['golden']} PE {i}:")
+
+
+def test_pe_start_order_within_stated_fp_tolerance(tmp_path):
+    """SHMEM_REDUCE_ORDER=pe_start gives every PE PE_start's result. For FP
+    sum/prod on PE p != PE_start that differs from the reference's own result
+    by rounding only: |r - ref_p| <= 2 (N-1) u sum|x_i| (sum) and
+    <= 2 (N-1) u |prod x_i| (prod), u = 2^-53 / 2^-24,
+    wherever every input is finite and normal and neither result overflowed;
+    where an input is NaN both results must be NaN."""
+    pairs = [("sum", "double"), ("sum", "float"), ("prod", "double"), ("prod", "float")]
+    cases = make_cases(pairs, 20000, [[0, 0, 5]], "dev", "p2p", 0, order="pe_start")
+    cases += make_cases(pairs, 300, [[0, 0, 5]], "dev", "p2p", 100, order="pe_start")
+    results = run_pes(5, cases, tmp_path)
+    for c in cases:
+        op, dtype, n = c["op"], c["dtype"], c["n"]
+        srcs = [source(op, dtype, n, c["seed"], pe) for pe in range(5)]
+        x = np.stack(srcs).astype(np.float64)
+        u = 2.0 ** -53 if dtype == "double" else 2.0 ** -24
+        with np.errstate(all="ignore"):
+            bound = 2 * 4 * u * (np.abs(x).sum(axis=0) if op == "sum" else np.abs(np.prod(x, axis=0)))
+        finite_in = np.isfinite(x).all(axis=0)
+        # subnormal inputs round relative to the subnormal grid, not to u
+        normal_in = ((np.abs(x) >= np.finfo(oracle.NP[dtype]).tiny) | (x == 0)).all(axis=0)
+        differs = 0
+        for p in range(5):
+            got = results[p][str(c["id"])].astype(np.float64)
+            ref = oracle.reduce_pe(op, dtype, srcs, p).astype(np.float64)
+            both = finite_in & normal_in & np.isfinite(got) & np.isfinite(ref)
+            err = np.abs(got - ref)
+            assert (err[both] <= bound[both]).all(), f"{op}/{dtype} PE {p}: error above the stated bound"
+            # a NaN input makes the result NaN in every order (an Inf may give Inf or NaN by order)
+            nan_in = np.isnan(x).any(axis=0)
+            assert (np.isnan(got[nan_in]) & np.isnan(ref[nan_in])).all(), f"{op}/{dtype} PE {p}"
+            differs += int((got[both] != ref[both]).sum())
+        if n > 1000:
+            assert differs > 0, "inputs too benign: no PE's result differed from PE_start's"
 
 
 @pytest.mark.parametrize("fused_max", ["1M", "0"], ids=["fused", "multi-launch"])
@@ -278,6 +349,9 @@ def test_random_sequence_stress(tmp_path):
         sets = sets_choices[rng.integers(len(sets_choices))]
         cases.append({"id": cid, "op": op, "dtype": dtype, "n": n, "sets": sets, "mode": mode,
                       "algorithm": alg, "seed": 7000 + cid})
+    # version areas of 128 KiB per channel: order-sensitive calls above ~160 KiB
+    # run the multi-launch schedule in several rounds
     results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_DEVICE_HEAP_SIZE": "64M",
-                                                     "SHMEM_DEVICE_SCRATCH_SIZE": "3M"})
+                                                     "SHMEM_DEVICE_SCRATCH_SIZE": "3M",
+                                                     "SHMEM_DEVICE_ORDER_SIZE": "256K"})
     check(results, cases)

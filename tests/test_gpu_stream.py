@@ -4,9 +4,10 @@ device barrier (shmemx_barrier_on_stream) across PE processes on one GPU.
 Each case enqueues a chain buf[i+1] <- reduce(buf[i]) on a HIP stream with no
 host wait between the calls, so every cross-PE step of the chain is ordered by
 device-side flags alone (fused kernel or device barriers). The expected chain
-is computed with the oracle: step 1 folds the members' sources in active-set
-order (the reference's result on PE_start), step i+1 folds size copies of
-step i's (identical) result.
+is computed with the oracle: step 1 gives member q the reference's result
+for q (its own source first, the default result order), step i+1 reduces the
+members' step-i results the same way (with order "pe_start": PE_start's
+result on every member, so step i+1 folds size copies of it).
 """
 import numpy as np
 import pytest
@@ -19,13 +20,16 @@ from test_gpu_multipe import members, run_pes
 pytestmark = [pytest.mark.gpu, pytest.mark.multipe]
 
 
-def chain_want(op, dtype, n, seed, mem, k):
+def chain_want(op, dtype, n, seed, mem, k, pe, order="reference"):
+    """Step results 1..k on member `pe` of `mem`."""
+    def step(xs):
+        return [oracle.reduce_pe(op, dtype, xs, i if order == "reference" else 0) for i in range(len(mem))]
     ys = []
-    y = oracle.reduce_pe(op, dtype, [source(op, dtype, n, seed, pe) for pe in mem], 0)
-    ys.append(y)
+    y = step([source(op, dtype, n, seed, q) for q in mem])
+    ys.append(y[mem.index(pe)])
     for _ in range(k - 1):
-        y = oracle.reduce_pe(op, dtype, [y] * len(mem), 0)
-        ys.append(y)
+        y = step(y)
+        ys.append(y[mem.index(pe)])
     return ys
 
 
@@ -43,17 +47,19 @@ def check_stream(results, cases):
             mem = members(*s)
             for pe in mem:
                 res = results[pe]
+                order = c.get("order", "reference")
                 if c.get("graph"):
                     for r in range(c["graph"]):
-                        want = chain_want(op, dtype, n, c["seed"] + r, mem, k)[-1]
+                        want = chain_want(op, dtype, n, c["seed"] + r, mem, k, pe, order)[-1]
                         assert_match(res[f"{c['id']}_r{r}"], want, op, dtype,
                                      ctx=f"case {c['id']} graph replay {r} set {s} PE {pe}:")
                     continue
-                for i, want in enumerate(chain_want(op, dtype, n, c["seed"], mem, k), start=1):
+                for i, want in enumerate(chain_want(op, dtype, n, c["seed"], mem, k, pe, order), start=1):
                     assert_match(res[f"{c['id']}_{i}"], want, op, dtype,
                                  ctx=f"case {c['id']} step {i} set {s} PE {pe}:")
                 if c.get("mixed"):
-                    want = oracle.reduce_pe(op, dtype, [source(op, dtype, n, c["seed"] + 1, q) for q in mem], 0)
+                    want = oracle.reduce_pe(op, dtype, [source(op, dtype, n, c["seed"] + 1, q) for q in mem],
+                                            mem.index(pe) if order == "reference" else 0)
                     assert_match(res[f"{c['id']}_host"], want, op, dtype, ctx=f"case {c['id']} host call PE {pe}:")
 
 
@@ -75,7 +81,13 @@ def test_stream_chains_fused_and_multi_launch(tmp_path):
     cases.append(stream_case(cid, "and", "long", 777, [[2, 0, 1]])); cid += 1
     cases.append(stream_case(cid, "sum", "double", 0, [[0, 0, 4]], barriers=True)); cid += 1
     cases.append(stream_case(cid, "sum", "float", 1, [[1, 0, 3]])); cid += 1
-    results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_FUSED_MAX_BYTES": "256K"})
+    # PE_start order on every member
+    cases.append(stream_case(cid, "sum", "double", 1000, [[0, 0, 4]], order="pe_start")); cid += 1
+    cases.append(stream_case(cid, "max", "float", 70000, [[0, 0, 4]], order="pe_start")); cid += 1
+    # every member's order through version areas too small for one round
+    cases.append(stream_case(cid, "sum", "float", 90001, [[0, 0, 4]])); cid += 1
+    results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_FUSED_MAX_BYTES": "256K",
+                                                     "SHMEM_DEVICE_ORDER_SIZE": "512K"})
     check_stream(results, cases)
 
 
