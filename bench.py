@@ -61,14 +61,161 @@ def synth_bits(pe, idx):
     return out.view(np.int64)
 
 
-def cpu_baseline(n, budget_s):
-    """The reference algorithm (oracle restatement) at 1 PE on 1 core: median
-    seconds per call over as many calls as fit in ~budget_s."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def cpu_baseline(S, n_gpus, budget_s):
+    """The reference algorithm (reduce-op.c:226-266 restated in C,
+    oracle/reduce_oracle.c: copy loop, barrier, 64-element pWrk chunks folded
+    with one indirect operator call per element, barrier) on this box's host
+    cores, in this run, before the GPU is touched: N = max(2, n_gpus) forked
+    PE processes, PE p pinned to the p-th CPU of this process's affinity mask,
+    shared-memory transport. Bounded sample: as many calls as fit in about
+    budget_s. Also the 1-PE call (the N = 1 headline's workload) and BASELINE
+    config 1 (int sum, 2 PEs, 4 KiB)."""
     import oracle
-    t1 = oracle.cpu_baseline_double_sum(1, n, 0, 1)
-    reps = int(max(3, min(200, budget_s / max(t1, 1e-6))))
-    t = oracle.cpu_baseline_double_sum(1, n, 1, reps)
-    return t, reps
+    npes = max(2, n_gpus)
+    n = S // 8
+
+    def timed(op, dtype, pes, nel, share):
+        t1, _ = oracle.cpu_baseline(op, dtype, pes, nel, 0, 1)
+        reps = int(max(3, min(100000, share / max(t1, 1e-7))))
+        t, cpus = oracle.cpu_baseline(op, dtype, pes, nel, 1, reps)
+        return t, reps, cpus
+
+    t, reps, cpus = timed("sum", "double", npes, n, 0.6 * budget_s)
+    t1, reps1, cpus1 = timed("sum", "double", 1, n, 0.3 * budget_s)
+    tc, repsc, cpusc = timed("sum", "int", 2, 1024, 0.1 * budget_s)
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = None
+    mib = S >> 20
+    return {"value": round(npes * S / t / GIB, 4), "unit": "GiB/s", "cores": npes, "kind": "port",
+            "sample": f"{reps} calls of shmem_double_sum_to_all's reference algorithm (restated in C, "
+                      f"oracle/reduce_oracle.c) on {npes} PE processes x {mib} MiB, one pinned core each "
+                      f"(CPUs {cpus}); median per call {t * 1e3:.1f} ms, max over PEs; whole-job GiB/s",
+            "ms_per_call": round(t * 1e3, 3), "per_pe_gib_s": round(S / t / GIB, 4),
+            "one_pe": {"value": round(S / t1 / GIB, 4), "cores": 1, "calls": reps1, "ms_per_call": round(t1 * 1e3, 3),
+                       "cpus": cpus1, "note": f"1 PE x {mib} MiB: the N = 1 headline's workload"},
+            "config1": {"workload": "shmem_int_sum_to_all, 2 PEs, 4 KiB (BASELINE config 1; shared-memory "
+                                    "transport in place of GASNet udp/mpi loopback)",
+                        "us_per_call": round(tc * 1e6, 3), "per_pe_gib_s": round(4096 / tc / GIB, 4), "calls": repsc,
+                        "cores": 2, "cpus": cpusc},
+            "host": {"nproc": os.cpu_count(), "allowed_cpus": allowed, "cpu_model": cpu_model()}}
+
+
+# ---------------------------------------------------------------------------
+# kernel legs (N = 1): the fold kernels themselves, timed on one GPU
+# ---------------------------------------------------------------------------
+KERNEL_LEGS = [
+    # name, kernel, op, dtype, sources, bytes per source, every-member orders
+    ("fold_k2_double_sum", "combine_vec<sum,double,2>", "sum", "double", 2, 256 << 20, False),
+    ("fold_k8_double_sum", "combine_vec<sum,double,8>", "sum", "double", 8, 256 << 20, False),
+    ("rs_shard_n8_double_sum", "combine_orders_vec<sum,double,8>", "sum", "double", 8, 32 << 20, True),
+    ("fold_k8_float_max", "combine_vec<max,float,8>", "max", "float", 8, 64 << 20, False),
+    ("fold_k8_longlong_and", "combine_vec<and,longlong,8>", "and", "longlong", 8, 64 << 20, False),
+    ("rs_shard_n8_float_max", "combine_orders_vec<max,float,8>", "max", "float", 8, 8 << 20, True),
+]
+
+
+def kernel_legs(shm, reps, check):
+    """The reduction's fold kernels on this GPU, called through the C ABI
+    (include/mi355_reduce.h) on hipMalloc'd buffers, each launch stamped by a
+    HIP event pair on its own stream (mi355_time_next_launch):
+      fold_k*      mi355_combine: dst = src0 (+) ... (+) src(k-1), the
+                   reduce-scatter kernel's shape with k local sources
+                   (algorithmic bytes (k+1) x per-source bytes);
+      rs_shard_n8  mi355_combine_orders: what each GPU runs in BASELINE
+                   config 3 / 4 at N = 8 with the default result order -- 8
+                   sources of one shard, 8 outputs (every member's reference
+                   order), algorithmic bytes 16 x shard bytes.
+    Sources: (uniform - 0.5) doubles, full mantissa (the float/longlong legs
+    read the same bytes as their type). Checked bit-exact against the oracle
+    on a sample of every output."""
+    import ctypes
+    import oracle
+    L = shm.lib
+    vp = ctypes.c_void_p
+    L.mi355_time_next_launch.argtypes = [vp, vp]
+    L.mi355_time_next_launch.restype = None
+    L.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), vp, vp]
+    big = max(b for *_, b, _ in KERNEL_LEGS)
+    nbuf = max(k for *_, k, _, _ in KERNEL_LEGS)
+    srcs, hosts = [], []
+
+    def dmalloc(nbytes):
+        p = vp()
+        if L.hipMalloc(ctypes.byref(p), ctypes.c_size_t(nbytes)) != 0:
+            raise RuntimeError("hipMalloc failed")
+        return p.value
+
+    for p in range(nbuf):
+        x = np.random.default_rng(77 + p).random(big // 8) - 0.5
+        d = dmalloc(big)
+        shm.put(d, x)
+        srcs.append(d)
+        hosts.append(x)
+    outs = [dmalloc(big) for _ in range(nbuf)]
+    ev = [vp() for _ in range(2 * reps)]
+    for e in ev:
+        L.hipEventCreate(ctypes.byref(e))
+    res = {}
+    for name, kname, op, dtype, k, nbytes, orders in KERNEL_LEGS:
+        es = np.dtype(shmem_reduce.NP[dtype]).itemsize
+        n = nbytes // es
+        nout = k if orders else 1
+
+        def launch():
+            if orders:
+                return shm.combine_orders(op, dtype, outs[:k], srcs[:k], n)
+            return shm.combine(op, dtype, outs[0], srcs[:k], n)
+
+        for _ in range(3):
+            assert launch() == 0
+        shm.sync()
+        for r in range(reps):
+            L.mi355_time_next_launch(ev[2 * r], ev[2 * r + 1])
+            assert launch() == 0
+        shm.sync()
+        ts = []
+        for r in range(reps):
+            ms = ctypes.c_float()
+            L.hipEventElapsedTime(ctypes.byref(ms), ev[2 * r], ev[2 * r + 1])
+            ts.append(ms.value * 1e-3)
+        t = float(np.mean(ts))
+        alg = (k + nout) * nbytes
+        gbs = alg / t / 1e9
+        ck = "skipped"
+        if check:
+            idx = np.unique(np.random.default_rng(5).integers(0, n, 1 << 14))
+            samp = [np.ascontiguousarray(h.view(np.uint8)[:nbytes].view(shmem_reduce.NP[dtype])[idx])
+                    for h in hosts[:k]]
+            bad = 0
+            for q in range(nout):
+                got = shm.get(outs[q], n, dtype)[idx]
+                want = oracle.reduce_pe(op, dtype, samp, q)
+                bad += int((got.view(np.uint8) != want.view(np.uint8)).sum())
+            ck = (f"bit-exact vs the oracle, {len(idx)} samples x {nout} output(s)" if bad == 0
+                  else f"MISMATCH in {bad} bytes")
+        res[name] = {"kernel": kname, "sources": k, "outputs": nout, "bytes_per_source": nbytes,
+                     "alg_bytes_per_launch": alg, "kernel_avg_us": round(t * 1e6, 2),
+                     "kernel_median_us": round(float(np.median(ts)) * 1e6, 2), "launches": reps,
+                     "achieved_GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "check": ck}
+    for e in ev:
+        L.hipEventDestroy(e)
+    for d in srcs + outs:
+        L.hipFree(vp(d))
+    res["note"] = ("fold kernels timed alone (HIP event pair per launch on its stream), algorithmic bytes = "
+                   "(sources + outputs) x bytes; frac against the 8 TB/s HBM peak")
+    return res
 
 
 def main():
@@ -78,7 +225,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--mib", type=int, default=256, help="MiB per PE")
     ap.add_argument("--algorithm", default=os.environ.get("SHMEM_REDUCE_ALGORITHM", "auto"))
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--no-small", action="store_true",
@@ -91,6 +238,10 @@ def main():
                     help="attempt the RCCL comparison even when PEs share a GPU (exercises its failure path)")
     ap.add_argument("--no-ops", action="store_true",
                     help="skip the op-coverage leg (BASELINE config 4: float max + longlong and, 64 MiB per PE)")
+    ap.add_argument("--no-kernels", action="store_true",
+                    help="N = 1: skip the kernel legs (the fold kernels timed alone: k = 2 / 8 sources of "
+                         "256 MiB, config 3 / 4's per-GPU reduce-scatter shapes)")
+    ap.add_argument("--kernel-reps", type=int, default=50)
     ap.add_argument("--host", action="store_true",
                     help="source/target in host memory (shmem_malloc, page-locked): the rate includes the "
                          "H2D/D2H staging copies (DESIGN.md); not the headline metric")
@@ -106,10 +257,7 @@ def main():
     # CPU baseline first, before this process initialises the GPU
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        t, reps = cpu_baseline(n, args.cpu_seconds)
-        cpu = {"value": round(S / t / GIB, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
-               "sample": f"{reps} calls of the reference algorithm (restated in C, oracle/reduce_oracle.c) "
-                         f"at 1 PE on {args.mib} MiB double, median per call {t * 1e3:.1f} ms"}
+        cpu = cpu_baseline(S, args.gpus, args.cpu_seconds)
 
     os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(2 * S + (64 << 20)))
     os.environ.setdefault("SHMEM_DEVICE_SCRATCH_SIZE", str(96 << 20))
@@ -179,12 +327,14 @@ def main():
     t_rccl_local = None
     distinct_gpus = False
     if npes > 1:
-        # RCCL refuses two ranks on one device: compare only with one GPU per PE
-        dev = np.array([shm.lib.shmemx_device_id()], dtype=np.int32)
-        lo, hi = np.zeros(1, dtype=np.int32), np.zeros(1, dtype=np.int32)
-        shm.to_all("min", "int", lo.ctypes.data, dev.ctypes.data, 1, 0, 0, npes)
-        shm.to_all("max", "int", hi.ctypes.data, dev.ctypes.data, 1, 0, 0, npes)
-        distinct_gpus = int(lo[0]) != int(hi[0]) or args.force_rccl_compare
+        # RCCL refuses two ranks on one device: compare only with one GPU per
+        # PE. Same GPU = same PCI bus id (not the HIP ordinal, which is 0 on
+        # every rank under a launcher that shows each rank one GPU).
+        shared = np.array([sum(shm.lib.shmemx_pe_same_device(q) for q in range(npes) if q != me)],
+                          dtype=np.int32)
+        anyshared = np.zeros(1, dtype=np.int32)
+        shm.to_all("max", "int", anyshared.ctypes.data, shared.ctypes.data, 1, 0, 0, npes)
+        distinct_gpus = int(anyshared[0]) == 0 or args.force_rccl_compare
     rccl_ok = False
     # RCCL prints a version banner on stdout at communicator creation; keep
     # stdout to the one JSON line by pointing fd 1 at stderr meanwhile
@@ -248,8 +398,8 @@ def main():
                 "note": "same K calls with SHMEM_REDUCE_ALGORITHM=rccl (ncclAllReduce, RCCL's order: "
                         "FP results within tolerance, not bit-exact); comparison only, not the headline"}
 
-    # correctness of the last result on a sample: the P2P schedule's result is
-    # the reference's result on PE_start (own-first = ascending order)
+    # correctness of the last result on a sample: every PE holds the
+    # reference's result for itself (own source first, then ascending)
     check = "skipped"
     if not args.no_check:
         idx = np.unique(np.random.default_rng(me).integers(0, n, 1 << 16).astype(np.uint64))
@@ -262,11 +412,16 @@ def main():
         got = got_full[idx.astype(np.int64)]
         import oracle
         srcs = [synth(p, idx) for p in range(npes)]
-        want = oracle.reduce_pe("sum", "double", srcs, 0)
+        want = oracle.reduce_pe("sum", "double", srcs, me)
         bad = int((got.view(np.uint64) != want.view(np.uint64)).sum())
-        check = "bit-exact vs reference order (PE_start), %d samples" % len(idx) if bad == 0 else \
-            "MISMATCH %d of %d samples" % (bad, len(idx))
+        bad = int(max_over_pes(bad))
+        check = "bit-exact vs the reference's per-PE order on every PE, %d samples each" % len(idx) if bad == 0 \
+            else "MISMATCH %d of %d samples (worst PE)" % (bad, len(idx))
         del got_full
+
+    kernels = None
+    if npes == 1 and not args.no_kernels and not args.host:
+        kernels = kernel_legs(shm, args.kernel_reps, not args.no_check)
 
     # BASELINE config 4 (op coverage): shmem_float_max_to_all and
     # shmem_longlong_and_to_all on 64 MiB per PE, timed like the headline
@@ -295,8 +450,8 @@ def main():
             if not args.no_check:
                 idx = np.unique(np.random.default_rng(100 + me).integers(0, no, 1 << 14)).astype(np.uint64)
                 got = shm.get(dst, no, dtype)[idx.astype(np.int64)]
-                want = oracle.reduce_pe(op, dtype, [gen(p, idx) for p in range(npes)], 0)
-                bad = int((got.view(np.uint8) != want.view(np.uint8)).sum())
+                want = oracle.reduce_pe(op, dtype, [gen(p, idx) for p in range(npes)], me)
+                bad = int(max_over_pes(int((got.view(np.uint8) != want.view(np.uint8)).sum())))
                 ck = "bit-exact, %d samples" % len(idx) if bad == 0 else "MISMATCH in %d bytes" % bad
             ops[name] = {"bytes_per_pe": ob, "steps": k, "us_per_call": round(t_op * 1e6, 2),
                          "value": round(npes * ob / t_op / GIB, 2), "per_pe_gib_s": round(ob / t_op / GIB, 2),
@@ -308,19 +463,37 @@ def main():
     if npes == 1:
         kname = "copy_segments<4> (identity fold, PE_size=1)"
         alg_bytes = 2 * S
+        achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                    "kernel": kname, "alg_bytes_per_launch": alg_bytes, "kernel_avg_us": round(k_avg_ms * 1e3, 2),
+                    "launches_timed": nk, "ms_per_step_with_events": round(t_local_ev / args.steps * 1e3, 4)}
     else:
-        kname = f"combine_vec<sum,double,{npes}> (reduce-scatter leg, {npes - 1} sources over xGMI)"
+        # N > 1: the reduce-scatter fold reads N-1 of its N shard sources from
+        # peers over xGMI, so its bound is the links into this GPU: achieved =
+        # those remote bytes / the fold's duration against (N-1) x 153 GB/s.
+        # Its local-HBM view (all source and output bytes) is kept in `hbm`.
         shard = S // npes
-        alg_bytes = (npes + 1) * shard
-    achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
-    roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                "kernel": kname, "alg_bytes_per_launch": alg_bytes, "kernel_avg_us": round(k_avg_ms * 1e3, 2),
-                "launches_timed": nk, "ms_per_step_with_events": round(t_local_ev / args.steps * 1e3, 4)}
-    if npes > 1:
-        roofline["note"] = ("N > 1: (N-1)/N of this kernel's reads cross xGMI, so the HBM fraction is not its "
-                            "bound; the link-side figures are in `xgmi` (rs_kernel_remote_read_GB_s against "
-                            "mesh_bound_GB_s_per_pe)")
+        kname = (f"combine_orders_vec<sum,double,{npes}> (reduce-scatter leg: every PE's reference order)"
+                 if npes <= 8 else f"mi355_combine_orders, {npes} sources (one left fold per member)")
+        remote = (npes - 1) * shard
+        hbm_bytes = 2 * npes * shard
+        achieved = remote / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
+        peak = (npes - 1) * XGMI_LINK_GBS
+        hbm_gbs = hbm_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
+        roofline = {"bound": "xgmi", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
+                    "frac": round(achieved / peak, 4), "traffic": None, "kernel": kname,
+                    "alg_bytes_per_launch": remote, "kernel_avg_us": round(k_avg_ms * 1e3, 2),
+                    "launches_timed": nk, "ms_per_step_with_events": round(t_local_ev / args.steps * 1e3, 4),
+                    "peak_note": "(N-1) links x 153 GB/s into this GPU (SURVEY 8d); if 153.6 GB/s counts both "
+                                 "directions the one-way bound is half: see xgmi.frac_one_direction",
+                    "hbm": {"bytes_per_launch": hbm_bytes, "achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS,
+                            "frac": round(hbm_gbs / HBM_PEAK_GBS, 4),
+                            "note": "the same fold counted as local HBM traffic: N shard sources read + N "
+                                    "outputs (this PE's target shard and N-1 versions) written"}}
+        if not distinct_gpus:
+            roofline["note"] = ("the PEs share ONE GPU (test layout): the 'remote' reads are this GPU's own HBM, "
+                                "so achieved/frac here are not xGMI figures")
     traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     if os.path.exists(traffic_file) and not args.host:
         try:
@@ -389,6 +562,7 @@ def main():
              "note": "BASELINE config 5 shape: 4096 back-to-back 64 KiB shmem_double_sum_to_all calls, max over PEs"},
             "check": check,
             "op_coverage": ops,
+            "kernels": kernels,
         }
         print(json.dumps(out), flush=True)
     if args.host:

@@ -72,6 +72,8 @@ int shmemx_device_id (void);                 /* HIP ordinal of this PE's GPU */
 /* Link from this PE's GPU to PE pe's: type (hsa_amd_link_info_type_t: 4 =
  * xGMI, 2 = PCIe) and hop count; -1 if pe shares this GPU or is not visible. */
 int shmemx_peer_link (int pe, int *link_type, int *hops);
+/* 1 if PE pe's GPU is this PE's GPU (same PCI bus id), else 0. */
+int shmemx_pe_same_device (int pe);
 void shmemx_device_synchronize (void);        /* hipDeviceSynchronize, checked */
 /* hipMemcpy (kind inferred from the pointers), checked; blocking. */
 void shmemx_memcpy (void *dst, const void *src, size_t nbytes);

@@ -51,6 +51,9 @@ def _load():
         lib.oracle_reduce_pe.restype = ctypes.c_int
         lib.oracle_cpu_baseline_double_sum.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int]
         lib.oracle_cpu_baseline_double_sum.restype = ctypes.c_double
+        lib.oracle_cpu_baseline.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                            ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+        lib.oracle_cpu_baseline.restype = ctypes.c_double
         _lib = lib
     return _lib
 
@@ -103,6 +106,18 @@ def cpu_baseline_double_sum(npes, n, warm=1, reps=3):
     """Median seconds per call of the reference algorithm (restated) on npes
     host processes with a shared-memory transport, max over PEs."""
     return _load().oracle_cpu_baseline_double_sum(npes, n, warm, reps)
+
+
+def cpu_baseline(op, dtype, npes, n, warm=1, reps=3, pin=True):
+    """The reference algorithm (reduce-op.c:226-266, restated in C) as npes
+    forked host processes, PE p pinned to the p-th CPU of this process's
+    affinity mask: (median seconds per call, max over PEs; CPUs used).
+    op/dtype: sum on int (config 1) or double."""
+    cpus = (ctypes.c_int * npes)()
+    t = _load().oracle_cpu_baseline(OPS.index(op), DTYPES.index(dtype), npes, n, warm, reps, 1 if pin else 0, cpus)
+    if t < 0:
+        raise RuntimeError("oracle_cpu_baseline failed")
+    return t, list(cpus)
 
 
 def value_bytes(dtype):

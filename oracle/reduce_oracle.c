@@ -28,6 +28,7 @@
 #define _GNU_SOURCE
 #include <complex.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
@@ -179,12 +180,16 @@ int oracle_reduce_pe (int op, int t, int npes, int me, const void *const *srcs, 
 
 /* ---- CPU baseline: the reference algorithm timed with one process per PE -- */
 /* Shared-memory transport: shmem_getmem = memcpy from the peer's source in a
- * MAP_SHARED region, shmem_barrier = process-shared pthread barrier. Returns
- * the median seconds per call over `reps` timed calls after `warm` untimed,
- * max over PEs, or -1 on error. double sum only (the headline metric). */
+ * MAP_SHARED region (the 64-element pWrk copies inside the fold),
+ * shmem_barrier = process-shared pthread barrier. Each call is
+ * reduce-op.c:226-266: the copy loop, a barrier, the chunked fold of every
+ * other PE's source in ascending order (one indirect operator call per
+ * element), a barrier. Returns the median seconds per call over `reps` timed
+ * calls after `warm` untimed ones, max over PEs, or -1 on error. */
 struct bench_shared {
     pthread_barrier_t bar;
     double t[1024];
+    int cpu[1024];
 };
 
 static double mono (void)
@@ -209,12 +214,46 @@ static void fill_double (double *p, size_t n, unsigned seed)
     }
 }
 
-double oracle_cpu_baseline_double_sum (int npes, size_t n, int warm, int reps)
+/* SURVEY.md 8(d) inputs: config 1's ints src_p[i] = i*7 + p*1000003 (wrapping);
+ * full-mantissa doubles otherwise */
+static void fill_src (int t, void *p, size_t n, int pe)
 {
-    if (npes < 1 || npes > 1024 || reps < 1 || reps > 100000)
+    if (t == T_INT) {
+        int *q = (int *) p;
+        for (size_t i = 0; i < n; ++i)
+            q[i] = (int) ((unsigned) i * 7u + (unsigned) pe * 1000003u);
+    } else {
+        fill_double ((double *) p, n, 1234u + (unsigned) pe);
+    }
+}
+
+/* The `k`-th CPU of this process's affinity mask (wrapping), or -1. */
+static int nth_allowed_cpu (int k)
+{
+    cpu_set_t set;
+    if (sched_getaffinity (0, sizeof set, &set) != 0)
+        return -1;
+    const int cnt = CPU_COUNT (&set);
+    if (cnt <= 0)
+        return -1;
+    k %= cnt;
+    for (int c = 0; c < CPU_SETSIZE; ++c)
+        if (CPU_ISSET (c, &set) && k-- == 0)
+            return c;
+    return -1;
+}
+
+/* op/t: OP_SUM with T_INT (config 1) or T_DOUBLE (configs 2, 3, 5). pin: PE p
+ * runs pinned to the p-th CPU of the caller's affinity mask; cpus_out (npes
+ * entries, or NULL) receives the CPU each PE ran on. */
+double oracle_cpu_baseline (int op, int t, int npes, size_t n, int warm, int reps, int pin, int *cpus_out)
+{
+    if (npes < 1 || npes > 1024 || reps < 1 || reps > 1000000 || (t != T_INT && t != T_DOUBLE))
         return -1.0;
-    const size_t bytes = n * sizeof (double);
-    size_t total = sizeof (struct bench_shared) + 2 * (size_t) npes * bytes + 4096;
+    const size_t es = esize (t);
+    const size_t bytes = n * es;
+    const size_t slot = (bytes + 4095) / 4096 * 4096;
+    size_t total = 4096 * ((sizeof (struct bench_shared) + 4095) / 4096) + 2 * (size_t) npes * slot;
     char *mem = mmap (NULL, total, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_ANONYMOUS, -1, 0);
     if (mem == MAP_FAILED)
         return -1.0;
@@ -223,11 +262,13 @@ double oracle_cpu_baseline_double_sum (int npes, size_t n, int warm, int reps)
     pthread_barrierattr_init (&a);
     pthread_barrierattr_setpshared (&a, PTHREAD_PROCESS_SHARED);
     pthread_barrier_init (&sh->bar, &a, (unsigned) npes);
-    double *src = (double *) (mem + 4096 * ((sizeof (struct bench_shared) + 4095) / 4096));
-    double *tgt = src + (size_t) npes * n;
+    char *src = mem + 4096 * ((sizeof (struct bench_shared) + 4095) / 4096);
+    char *tgt = src + (size_t) npes * slot;
     double *times = (double *) malloc (sizeof (double) * (size_t) reps);
     if (times == NULL)
         return -1.0;
+    cpu_set_t saved; /* the caller's mask, restored when PE 0 returns */
+    const int have_saved = sched_getaffinity (0, sizeof saved, &saved) == 0;
     pid_t kids[1024];
     int me = 0;
     for (int p = 1; p < npes; ++p) {
@@ -238,18 +279,34 @@ double oracle_cpu_baseline_double_sum (int npes, size_t n, int warm, int reps)
         }
         kids[p] = k;
     }
-    fill_double (src + (size_t) me * n, n, 1234u + (unsigned) me);
-    double *mysrc = src + (size_t) me * n, *mytgt = tgt + (size_t) me * n;
+    sh->cpu[me] = -1;
+    if (pin) {
+        const int c = nth_allowed_cpu (me);
+        if (c >= 0) {
+            cpu_set_t one;
+            CPU_ZERO (&one);
+            CPU_SET (c, &one);
+            if (sched_setaffinity (0, sizeof one, &one) == 0)
+                sh->cpu[me] = c;
+        }
+    }
+    char *mysrc = src + (size_t) me * slot, *mytgt = tgt + (size_t) me * slot;
+    fill_src (t, mysrc, n, me);
     for (int r = 0; r < warm + reps; ++r) {
         pthread_barrier_wait (&sh->bar);
         double t0 = mono ();
         /* reduce-op.c:226-266 with the shared-memory transport */
-        for (size_t j = 0; j < n; ++j)
-            mytgt[j] = mysrc[j];
+        if (t == T_INT) {
+            for (size_t j = 0; j < n; ++j)
+                ((int *) mytgt)[j] = ((const int *) mysrc)[j];
+        } else {
+            for (size_t j = 0; j < n; ++j)
+                ((double *) mytgt)[j] = ((const double *) mysrc)[j];
+        }
         pthread_barrier_wait (&sh->bar);
         for (int i = 0; i < npes; ++i)
             if (i != me)
-                fold_double (o_sum_double, mytgt, src + (size_t) i * n, n);
+                oracle_fold (op, t, mytgt, src + (size_t) i * slot, n);
         pthread_barrier_wait (&sh->bar);
         if (r >= warm)
             times[r - warm] = mono () - t0;
@@ -262,10 +319,21 @@ double oracle_cpu_baseline_double_sum (int npes, size_t n, int warm, int reps)
     for (int p = 1; p < npes; ++p)
         waitpid (kids[p], NULL, 0);
     double worst = 0.0;
-    for (int p = 0; p < npes; ++p)
+    for (int p = 0; p < npes; ++p) {
         if (sh->t[p] > worst)
             worst = sh->t[p];
+        if (cpus_out != NULL)
+            cpus_out[p] = sh->cpu[p];
+    }
     pthread_barrier_destroy (&sh->bar);
     munmap (mem, total);
+    if (pin && have_saved)
+        sched_setaffinity (0, sizeof saved, &saved);
     return worst;
+}
+
+/* double sum, unpinned (tools/cpu_baseline.py, round 1) */
+double oracle_cpu_baseline_double_sum (int npes, size_t n, int warm, int reps)
+{
+    return oracle_cpu_baseline (OP_SUM, T_DOUBLE, npes, n, warm, reps, 0, NULL);
 }

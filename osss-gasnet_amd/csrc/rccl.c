@@ -162,9 +162,27 @@ int shmemi_rccl_allreduce (int op, int dtype, const void *src, void *dst, size_t
     ncclResult_t r = ncclAllReduce (src, dst, count, t, o, (ncclComm_t) comm, shmemi.stream);
     shmemi_timed_marker (1);
     r = rccl_settle ((ncclComm_t) comm, r, shmemi.barrier_timeout); /* non-blocking communicator */
-    if (r != ncclSuccess)
+    if (r == ncclSuccess) {
+        /* the collective runs on the library stream: wait for it with the same
+         * deadline (a peer whose enqueue failed never joins it) */
+        const double t0 = mono_s ();
+        hipError_t e;
+        while ((e = hipStreamQuery (shmemi.stream)) == hipErrorNotReady) {
+            if (mono_s () - t0 > shmemi.barrier_timeout) {
+                r = ncclInProgress;
+                break;
+            }
+            usleep (20);
+        }
+        if (r == ncclSuccess && e != hipSuccess)
+            shmemi_hip_check (e, "hipStreamQuery after ncclAllReduce");
+    }
+    if (r != ncclSuccess) {
+        /* drop the communicator: its queued work must not write dst later */
+        ncclCommAbort ((ncclComm_t) comm);
+        shmemi.rccl_comm = NULL;
         return -1;
-    SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    }
     return 0;
 }
 

@@ -736,9 +736,6 @@ void *pshmem_malloc (size_t size)
     return p;
 }
 
-/* Device-accessible address of [p, p + nbytes) when it lies inside one
- * page-locked shmem_malloc block (kernels can then read and write it over
- * PCIe directly), else NULL. */
 /* 1 if PE pe runs on this PE's GPU (same PCI bus id): its device heap is
  * this GPU's own memory. */
 int shmemi_pe_same_device (int pe)
@@ -751,6 +748,18 @@ int shmemi_pe_same_device (int pe)
     return mine[0] != '\0' && strcmp (mine, theirs) == 0;
 }
 
+/* MI355X extension (shmemx.h): the same, for callers (bench.py tells an
+ * xGMI run from PEs sharing one GPU by PCI bus id, not by the HIP ordinal,
+ * which is 0 for every rank under a launcher that gives each one GPU). */
+int shmemx_pe_same_device (int pe)
+{
+    shmemi_init_check ("shmemx_pe_same_device");
+    return shmemi_pe_same_device (pe);
+}
+
+/* Device-accessible address of [p, p + nbytes) when it lies inside one
+ * page-locked shmem_malloc block (kernels can then read and write it over
+ * PCIe directly), else NULL. */
 void *shmemi_host_dev_ptr (const void *p, size_t nbytes)
 {
     const char *c = (const char *) p;

@@ -30,17 +30,30 @@ def common(d, n):
     assert d["value"] > 0 and d["ms_per_step"] > 0 and d["higher_is_better"] is True
     assert d["check"].startswith("bit-exact"), d["check"]
     r = d["roofline"]
-    assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] < 1.2 and r["achieved"] > 0
+    if n == 1:
+        assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] < 1.2 and r["achieved"] > 0
+    else:
+        # N > 1: the reduce-scatter fold's remote reads against the links into the GPU
+        assert r["bound"] == "xgmi" and r["peak"] == (n - 1) * 153.0 and r["achieved"] > 0
+        assert r["alg_bytes_per_launch"] == (n - 1) * (d["config"]["bytes_per_pe"] // n)
+        assert r["hbm"]["peak"] == 8000.0 and r["hbm"]["achieved"] > 0
     for name in ("float_max", "longlong_and"):
         assert d["op_coverage"][name]["check"].startswith("bit-exact"), d["op_coverage"]
     assert d["small_call"]["us_per_call"] > 0
 
 
 def test_bench_one_gpu_line():
-    d = run([sys.executable, "bench.py", "--steps", "5", "--warmup", "2", "--cpu-seconds", "0.5"])
+    d = run([sys.executable, "bench.py", "--steps", "5", "--warmup", "2", "--cpu-seconds", "1", "--kernel-reps", "5"])
     common(d, 1)
-    assert d["cpu_baseline"]["kind"] == "port" and d["cpu_baseline"]["cores"] == 1
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["cores"] == 2 and cb["value"] > 0
+    assert cb["one_pe"]["cores"] == 1 and cb["config1"]["us_per_call"] > 0 and cb["host"]["nproc"] >= 1
     assert d["config"]["bytes_per_pe"] == 256 << 20
+    k = d["kernels"]
+    for name in ("fold_k2_double_sum", "fold_k8_double_sum", "rs_shard_n8_double_sum", "fold_k8_float_max",
+                 "fold_k8_longlong_and", "rs_shard_n8_float_max"):
+        assert k[name]["check"].startswith("bit-exact"), (name, k[name])
+        assert 0 < k[name]["frac"] < 1.2 and k[name]["kernel_avg_us"] > 0, (name, k[name])
 
 
 @pytest.mark.multipe
