@@ -166,6 +166,10 @@ typedef struct MI355FusedArgs {
      *    (nmembers - 1 slots), and each member gathers its own version of the other shards there. */
     int ordered;
     void *ver[MI355_FUSED_MAX_MEMBERS];              /* members' version areas (mapped), if ordered */
+    /* Processes that may run these spin-waiting kernels on this GPU at the same time (>= 1; 0 = 1):
+     * the grid is capped at the kernel's resident blocks per CU (one fewer, as a margin) x CUs / share,
+     * so every such grid can be resident at once and no spinning block keeps a peer's from starting. */
+    int share;
 } MI355FusedArgs;
 
 /* Reduce-scatter + all-gather of n elements over the members in ONE launch:

@@ -87,11 +87,11 @@ struct CombineParams {
 };
 
 // Cache policy (tools/hbm_sweep.hip, MI355X, 256 MiB per buffer):
-//   stores: `global_store_dwordx4 ... nt sc1` -- non-temporal AND write-through
-//     to memory at agent scope. As fast as plain non-temporal stores for the
-//     copy (6.82 TB/s) and within ~5 % for folds, and it makes the completion
+//   stores: write-through to memory at agent scope, which makes the completion
 //     signal cheap: no per-block L2 write-back (that cost 60 us on a 256 MiB
-//     copy with 2048 blocks).
+//     copy with 2048 blocks). The copy: `nt sc1`, as fast as plain
+//     non-temporal stores (6.82 TB/s); the folds: `sc1` (st16_fold), 3-10 %
+//     faster than `nt sc1` beside their non-temporal loads.
 //   loads: plain for the copy (6.8 TB/s vs 6.1 non-temporal), non-temporal
 //     for folds (Shape<NSRC>::policy).
 enum { POL_PLAIN = 0, POL_NT_LOAD = 1 };
@@ -103,6 +103,14 @@ __device__ __forceinline__ u32x4 ld16(const u32x4 *p) {
 }
 __device__ __forceinline__ void st16(u32x4 *p, u32x4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+// The folds' stores: write-through at agent scope WITHOUT the non-temporal
+// hint. Beside non-temporal loads this is the faster form (tools/fold_probe.hip,
+// profiles/r02/fold_probe_copy.txt, 256 MiB per source: k = 2 116.4 vs 127.9 us,
+// k = 3 158.7 vs 177.1, k = 8 393.5 vs 422); the copy keeps `nt sc1` (with
+// its plain loads `sc1` alone is 18 % slower).
+__device__ __forceinline__ void st16_fold(u32x4 *p, u32x4 v) {
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
 // Vector path: every pointer 16-byte aligned. Each lane owns UNROLL vectors
@@ -138,7 +146,7 @@ __global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
 #pragma unroll
                     for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[u][k].e[e]);
                 }
-                st16(d + i, acc.v);
+                st16_fold(d + i, acc.v);
             }
         }
     }
@@ -245,7 +253,7 @@ __global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
 #pragma unroll
                     for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[u][k].e[e]);
                 }
-                st16((u32x4 *)p.dst[q] + i, acc.v);
+                st16_fold((u32x4 *)p.dst[q] + i, acc.v);
             }
         }
     }

@@ -36,7 +36,9 @@
 // state is involved, which is what lets a captured HIP graph replay the call.
 //
 // All blocks of the grid must be co-resident (they wait on each other's last
-// block): the grid is at most kFusedMaxBlocks, far below one block per CU.
+// block), also beside the grids of other PEs sharing this GPU: the grid is
+// capped by the kernel's occupancy and the number of such PEs
+// (coresident_grid; at most MI355_FUSED_MAX_BLOCKS, one block per CU).
 // Every wait is bounded by p.timeout_ticks of the 100 MHz real-time counter.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -461,13 +463,58 @@ __global__ __launch_bounds__(64) void device_barrier(MI355FusedArgs a) {
     finish(a, mine, cnt, ok);
 }
 
+// Co-residency: every block of these grids waits for the grid's last block
+// and for the other members, so all blocks of every such grid running on this
+// GPU at once must be resident together. A launch is capped at the kernel's
+// resident blocks per CU x CUs, divided among the `share` processes that may
+// run such grids here at the same time. Resident blocks per CU: the occupancy
+// query, but at most 6 -- 256-thread blocks are admitted per CU up to
+// floor(800 / (ceil(sgpr / 16) * 16 + 16)) (MI355X_MICROARCH.md "Residency"),
+// which the query ignores, and these kernels use 103-106 SGPRs (6 per CU,
+// where the query says 8: 9 PEs x 174 blocks on one GPU never all started) --
+// and one fewer as a margin.
+struct OccEntry {
+    const void *fn;
+    int blocks_per_cu;
+};
+OccEntry g_occ[256];
+int g_nocc = 0;
+int g_cus = 0;
+
+unsigned coresident_grid(const void *fn, uint64_t want, int share) {
+    if (g_cus == 0) {
+        int dev = 0, cus = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+            cus = 256;
+        g_cus = cus;
+    }
+    int per_cu = -1;
+    for (int i = 0; i < g_nocc; ++i)
+        if (g_occ[i].fn == fn) per_cu = g_occ[i].blocks_per_cu;
+    if (per_cu < 0) {
+        int n = 0;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBlock, 0) != hipSuccess || n < 1) n = 1;
+        (void)hipGetLastError();
+        if (n > 6) n = 6;
+        per_cu = n > 1 ? n - 1 : 1;
+        if (g_nocc < 256) g_occ[g_nocc++] = OccEntry{fn, per_cu};
+    }
+    uint64_t cap = (uint64_t)per_cu * (uint64_t)g_cus / (uint64_t)(share > 1 ? share : 1);
+    if (cap < 1) cap = 1;
+    if (want > cap) want = cap;
+    return (unsigned)(want < 1 ? 1 : want);
+}
+
 template <typename T>
 int launch_op(const MI355FusedArgs &a, unsigned grid, hipStream_t st) {
     switch (a.op) {
 #define CASE(O)                                                                        \
     case O:                                                                            \
         if constexpr (valid_pair<O, T>()) {                                           \
-            hipLaunchKernelGGL((fused_allreduce<O, T>), dim3(grid), dim3(kBlock), 0, st, a); \
+            auto k = fused_allreduce<O, T>;                                            \
+            hipLaunchKernelGGL(k, dim3(coresident_grid((const void *)k, grid, a.share)), \
+                               dim3(kBlock), 0, st, a);                                \
             break;                                                                     \
         } else {                                                                       \
             return MI355_E_UNSUP;                                                      \
@@ -580,7 +627,8 @@ extern "C" int mi355_fused_pull(const MI355PullArgs *p, void *stream) {
     uint64_t grid = (total + 16 * kBlock - 1) / (16 * kBlock);
     if (grid < 1) grid = 1;
     if (grid > MI355_FUSED_MAX_BLOCKS) grid = MI355_FUSED_MAX_BLOCKS;
-    hipLaunchKernelGGL(fused_pull, dim3((unsigned)grid), dim3(kBlock), 0, (hipStream_t)stream, *p);
+    hipLaunchKernelGGL(fused_pull, dim3(coresident_grid((const void *)fused_pull, grid, a->share)), dim3(kBlock), 0,
+                       (hipStream_t)stream, *p);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }

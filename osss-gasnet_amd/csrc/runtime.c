@@ -488,6 +488,8 @@ static void heap_exchange (void)
         }
         if (peer_dev != shmemi.device)
             shmemi.peer_acquire = 1; /* a peer on another GPU (or one this process cannot see) */
+        if (me->pci_bus_id[0] != '\0' && strcmp (me->pci_bus_id, pi->pci_bus_id) == 0)
+            ++shmemi.local_pes; /* shares this GPU: the fused kernels' grids must fit beside each other */
         /* A mapping that cannot be opened is not fatal here: the pointer stays
          * NULL, the self-test below fails for every PE alike and the job falls
          * back (no signal region: host barriers, no fused path; no peer heap:
@@ -859,6 +861,7 @@ void pshmem_init (void)
         SHMEMI_HIP (hipEventCreateWithFlags (&shmemi.ev_in[i], hipEventDisableTiming));
         SHMEMI_HIP (hipEventCreateWithFlags (&shmemi.ev_out[i], hipEventDisableTiming));
     }
+    shmemi.local_pes = 1;
     heap_init ();
     signal_init ();
     sigmem_init ();
@@ -871,6 +874,11 @@ void pshmem_init (void)
         /* SHMEM_PEER_ACQUIRE=0|1 overrides the choice made from the peers' devices */
         static const char *pa_env[] = {"SHMEM_PEER_ACQUIRE", NULL};
         shmemi.peer_acquire = (int) env_long (pa_env, shmemi.peer_acquire) != 0;
+        /* SHMEM_FUSED_GRID_SHARE=k: size the spin-waiting grids as if k PEs shared this GPU */
+        static const char *gs_env[] = {"SHMEM_FUSED_GRID_SHARE", NULL};
+        shmemi.local_pes = (int) env_long (gs_env, shmemi.local_pes);
+        if (shmemi.local_pes < 1)
+            shmemi.local_pes = 1;
         interconnect_selftest ();
         if (shmemi.mype == 0 && !shmemi.seg_unlinked) {
             shm_unlink (shmemi.seg_name); /* every PE is attached: drop the name */

@@ -73,6 +73,7 @@ struct shmemi_state {
     int entry_sync;             /* SHMEM_ENTRY_SYNC: hipDeviceSynchronize on entry */
     int p2p_broken;             /* init self-test: peer heap reads failed */
     int peer_acquire;           /* queue mi355_acquire_system before reads of peers' buffers */
+    int local_pes;              /* PEs on this GPU (this one included): co-residency share of the fused grids */
 
     /* bootstrap */
     struct shmemi_seg *seg;

@@ -281,10 +281,29 @@ def main():
                 shm.put(src, x)
         shm.set_algorithm(c.get("algorithm", "auto"))
         shm.set_order(c.get("order", "reference"))
+        busy_t0 = None
+        if c.get("busy_ms") and me == 0:
+            # another kernel holds every CU of the GPU while this PE enters the
+            # collective (tests/native/busy_kernel.hip, its own non-blocking stream)
+            import time
+            busy = ctypes.CDLL(os.path.join(ROOT, "osss-gasnet_amd", "lib", "libtestbusy.so"))
+            busy.test_busy_launch.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_void_p]
+            st = ctypes.c_void_p()
+            assert hip.hipStreamCreateWithFlags(ctypes.byref(st), 1) == 0
+            shm.barrier_all()
+            assert busy.test_busy_launch(float(c["busy_ms"]), 8, st) == 0
+            busy_t0 = time.perf_counter()
+        elif c.get("busy_ms"):
+            shm.barrier_all()
         if c.get("api") == "fortran":
             fortran_to_all(shm, op, dtype, dst, src, n, *mine)
         else:
             shm.to_all(op, dtype, dst, src, n, *mine)
+        if busy_t0 is not None:
+            import time
+            results[str(c["id"]) + "_seconds"] = np.array([time.perf_counter() - busy_t0])
+            assert hip.hipStreamSynchronize(st) == 0
+            hip.hipStreamDestroy(st)
         if mode.startswith("host"):
             out = np.empty(n, dtype=shmem_reduce.NP[dtype])
             if n:

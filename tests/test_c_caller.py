@@ -56,10 +56,35 @@ def test_c_program_compiles_and_links(tmp_path):
     assert "shmem_int_sum_to_all" in out and "shmem_double_max_to_all" in out
 
 
+def oshrun_module():
+    import importlib.machinery
+    import importlib.util
+    loader = importlib.machinery.SourceFileLoader("oshrun", os.path.join(ROOT, "tools", "oshrun"))
+    spec = importlib.util.spec_from_loader("oshrun", loader)
+    mod = importlib.util.module_from_spec(spec)
+    loader.exec_module(mod)
+    return mod
+
+
+def test_oshrun_hardware_queue_policy():
+    """More than 4 PEs on one GPU: at most 16 hardware queues for the job,
+    also over the box's preset GPU_MAX_HW_QUEUES=4; opt-out kept."""
+    q = oshrun_module().hw_queue_env
+    assert q(8, True, {"GPU_MAX_HW_QUEUES": "4"}) == {"GPU_MAX_HW_QUEUES": "2"}
+    assert q(8, True, {}) == {"GPU_MAX_HW_QUEUES": "2"}
+    assert q(12, True, {}) == {"GPU_MAX_HW_QUEUES": "1"}
+    assert q(12, True, {"GPU_MAX_HW_QUEUES": "1"}) == {}
+    assert q(4, True, {"GPU_MAX_HW_QUEUES": "4"}) == {}
+    assert q(8, False, {"GPU_MAX_HW_QUEUES": "4"}) == {}          # one GPU per PE
+    assert q(8, True, {"GPU_MAX_HW_QUEUES": "4", "SHMEM_KEEP_HW_QUEUES": "1"}) == {}
+
+
 @pytest.mark.gpu
 @pytest.mark.multipe
-@pytest.mark.parametrize("npes", [1, 3])
+@pytest.mark.parametrize("npes", [1, 3, 8])
 def test_c_program_runs(tmp_path, npes):
+    """1, 3 and 8 PEs (8: tools/oshrun's hardware-queue cap for PEs sharing the
+    one test GPU, over the box's preset GPU_MAX_HW_QUEUES)."""
     exe = build(tmp_path)
     env = dict(os.environ, SHMEM_DEVICE_HEAP_SIZE="16M", SHMEM_DEVICE_SCRATCH_SIZE="3M")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "oshrun"), "-np", str(npes), "--same-device",

@@ -31,6 +31,18 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 pytestmark = [pytest.mark.gpu, pytest.mark.multipe]
 
 
+def oshrun_queues(npes, env):
+    """tools/oshrun's hardware-queue policy for PEs sharing one GPU."""
+    import importlib.machinery
+    import importlib.util
+    path = os.path.join(os.path.dirname(HERE), "tools", "oshrun")
+    loader = importlib.machinery.SourceFileLoader("oshrun", path)
+    spec = importlib.util.spec_from_loader("oshrun", loader)
+    mod = importlib.util.module_from_spec(spec)
+    loader.exec_module(mod)
+    return mod.hw_queue_env(npes, True, env)
+
+
 def run_pes(npes, cases, tmp_path, extra_env=None, timeout=600):
     spec = tmp_path / "spec.json"
     spec.write_text(json.dumps({"cases": cases}))
@@ -41,11 +53,11 @@ def run_pes(npes, cases, tmp_path, extra_env=None, timeout=600):
                 # the multi-GPU layout queues a system-scope acquire before every read of peers'
                 # buffers (peers on other GPUs); the PEs here share one GPU, so force it on
                 "SHMEM_PEER_ACQUIRE": "1"})
-    if npes > 4:
-        # PEs sharing the one test GPU: keep the job's hardware queues at 16
-        # (8 processes x the default 4 oversubscribe the GPU's queue slots and
-        # every call then waits ~34 ms for a time slice)
-        env["GPU_MAX_HW_QUEUES"] = str(max(1, 16 // npes))
+    # PEs sharing the one test GPU: the job's hardware queues kept at 16, the
+    # same policy as tools/oshrun (8 processes x the default 4 oversubscribe
+    # the GPU's queue slots and every call then waits ~34 ms for a time slice;
+    # DESIGN.md section 5)
+    env.update(oshrun_queues(npes, env))
     env.update(extra_env or {})
     procs = []
     for pe in range(npes):
@@ -209,6 +221,42 @@ def test_two_and_three_pes(tmp_path, npes):
     cases += make_cases(SOME, 333, [[0, 0, npes]], "inplace", "exact", 100)
     results = run_pes(npes, cases, tmp_path)
     check(results, cases)
+
+
+@pytest.mark.parametrize("npes", [9, 12])
+def test_more_than_eight_pes_one_gpu(tmp_path, npes):
+    """9-12 PEs: the fused kernel's batched fold goes past its first batch of
+    8 members' vectors (one-shot and reduce-scatter, element tails), the
+    every-member-order fold of more than 8 sources runs one fold per member,
+    and 9-12 spin-waiting grids share the GPU (co-residency cap)."""
+    pairs = [("sum", "double"), ("max", "float"), ("xor", "int"), ("prod", "complexf")]
+    cases = make_cases(pairs, 1001, [[0, 0, npes]], "dev", "p2p", 0)            # fused one-shot (< 64 KiB)
+    cases += make_cases(pairs, 20003, [[0, 0, npes]], "dev", "p2p", 100)        # fused two-shot
+    cases += make_cases(pairs, 20003, [[0, 0, npes]], "inplace", "p2p", 200)    # two-shot in place
+    cases += make_cases(pairs[:2], 200001, [[0, 0, npes]], "dev", "p2p", 300)   # multi-launch
+    cases += make_cases(pairs[:2], 20003, [[0, 0, npes]], "dev", "p2p", 400, order="pe_start")
+    results = run_pes(npes, cases, tmp_path, extra_env={"SHMEM_DEVICE_HEAP_SIZE": "32M",
+                                                        "SHMEM_DEVICE_ORDER_SIZE": "16M"})
+    check(results, cases)
+
+
+def test_reduction_while_another_kernel_holds_every_cu(tmp_path):
+    """PE 0 enters each collective right after queueing, on a stream of its
+    own, a kernel that fills every CU for 300 ms: its spin-waiting grid (fused
+    one-launch, or the device barriers of the multi-launch schedule) can only
+    start block by block as that kernel drains, while its peers already wait
+    in theirs. Every call must complete with the right result, well inside
+    the barrier timeout."""
+    cases = make_cases([("sum", "double")], 8000, [[0, 0, 3]], "dev", "p2p", 0)        # fused one-shot
+    cases += make_cases([("max", "float")], 100000, [[0, 0, 3]], "dev", "p2p", 100)   # fused two-shot
+    cases += make_cases([("sum", "double")], 300000, [[0, 0, 3]], "dev", "p2p", 200)  # multi-launch
+    for c in cases:
+        c["busy_ms"] = 300
+    results = run_pes(3, cases, tmp_path, extra_env={"SHMEM_BARRIER_TIMEOUT": "60"})
+    check(results, cases)
+    for c in cases:
+        t = float(results[0][str(c["id"]) + "_seconds"][0])
+        assert 0.2 < t < 10.0, f"case {c['id']}: {t:.3f} s from the busy launch to the call's return"
 
 
 def test_eight_pes_one_gpu(tmp_path):

@@ -1,0 +1,270 @@
+// fold_probe.hip -- what bounds the k-source fold (combine_vec, reduce-scatter
+// kernel) on MI355X: source placement, store and load cache policy, launch
+// shape, and the read-only ceiling of k concurrent streams (tuning tool, not
+// part of the library). 256 MiB per source, double sum, HIP events, median of
+// 7 launches.
+//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/fold_probe.hip -o tools/fold_probe
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <vector>
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
+    fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+union P2 {
+    u32x4 v;
+    double e[2];
+};
+
+struct Srcs {
+    const u32x4 *s[8];
+};
+
+enum { ST_NT_SC1 = 0, ST_NT = 1, ST_PLAIN = 2, ST_NONE = 3, ST_SC1 = 4 };
+
+template <int ST>
+__device__ __forceinline__ void store(u32x4 *p, u32x4 v) {
+    if constexpr (ST == ST_NT_SC1)
+        asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (ST == ST_SC1)
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (ST == ST_NT)
+        __builtin_nontemporal_store(v, p);
+    else if constexpr (ST == ST_PLAIN)
+        *p = v;
+    else if (v.x == 0x7ff80123u && v.y == 0x5u)  // never: keeps the loads alive
+        *p = v;
+}
+
+template <int NT>
+__device__ __forceinline__ u32x4 load(const u32x4 *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+// grid-stride, U vectors per lane, all K*U loads before the adds (the library's combine_vec)
+template <int K, int U, int ST, int NT>
+__global__ __launch_bounds__(256) void fold_gs(Srcs in, u32x4 *d, size_t nvec) {
+    const size_t step = (size_t)gridDim.x * 256 * U;
+    for (size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x; base < nvec; base += step) {
+        P2 x[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            size_t i = base + (size_t)u * 256;
+            if (i < nvec) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) x[u][k].v = load<NT>(in.s[k] + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            size_t i = base + (size_t)u * 256;
+            if (i < nvec) {
+                P2 a = x[u][0];
+#pragma unroll
+                for (int k = 1; k < K; ++k) {
+                    a.e[0] = a.e[0] + x[u][k].e[0];
+                    a.e[1] = a.e[1] + x[u][k].e[1];
+                }
+                store<ST>(d + i, a.v);
+            }
+        }
+    }
+}
+
+// each block owns one contiguous range (chunk of `per` vectors), U vectors per lane per step
+template <int K, int U, int ST, int NT>
+__global__ __launch_bounds__(256) void fold_part(Srcs in, u32x4 *d, size_t nvec) {
+    const size_t per = (nvec + gridDim.x - 1) / gridDim.x;
+    const size_t lo = (size_t)blockIdx.x * per, hi = lo + per < nvec ? lo + per : nvec;
+    for (size_t base = lo + threadIdx.x; base < hi; base += 256 * U) {
+        P2 x[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            size_t i = base + (size_t)u * 256;
+            if (i < hi) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) x[u][k].v = load<NT>(in.s[k] + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            size_t i = base + (size_t)u * 256;
+            if (i < hi) {
+                P2 a = x[u][0];
+#pragma unroll
+                for (int k = 1; k < K; ++k) {
+                    a.e[0] = a.e[0] + x[u][k].e[0];
+                    a.e[1] = a.e[1] + x[u][k].e[1];
+                }
+                store<ST>(d + i, a.v);
+            }
+        }
+    }
+}
+
+template <typename F>
+double time_us(F launch) {
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    launch();
+    launch();
+    CHECK(hipDeviceSynchronize());
+    std::vector<double> ts;
+    for (int r = 0; r < 7; ++r) {
+        CHECK(hipEventRecord(a, 0));
+        launch();
+        CHECK(hipEventRecord(b, 0));
+        CHECK(hipEventSynchronize(b));
+        float ms = 0;
+        CHECK(hipEventElapsedTime(&ms, a, b));
+        ts.push_back(ms * 1e3);
+    }
+    std::sort(ts.begin(), ts.end());
+    CHECK(hipEventDestroy(a));
+    CHECK(hipEventDestroy(b));
+    return ts[ts.size() / 2];
+}
+
+int main(int argc, char **argv) {
+    const size_t bytes = 256ull << 20, nvec = bytes / 16;
+    int cus = 256;
+    CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    // placement A: 8 separate allocations; B: one allocation, source k at k * (bytes + stagger)
+    std::vector<void *> sep(8);
+    for (int k = 0; k < 8; ++k) {
+        CHECK(hipMalloc(&sep[k], bytes));
+        CHECK(hipMemset(sep[k], 0x11 * (k + 1), bytes));
+    }
+    const size_t max_stagger = 8ull << 20;
+    char *big;
+    CHECK(hipMalloc(&big, 8 * (bytes + max_stagger)));
+    CHECK(hipMemset(big, 0x22, 8 * (bytes + max_stagger)));
+    u32x4 *d;
+    CHECK(hipMalloc(&d, bytes + max_stagger));
+    CHECK(hipMemset(d, 0, bytes + max_stagger));
+    CHECK(hipDeviceSynchronize());
+    printf("separate allocations at:");
+    for (int k = 0; k < 8; ++k) printf(" %p", sep[k]);
+    printf("\n");
+
+    auto srcs_sep = [&]() { Srcs s{}; for (int k = 0; k < 8; ++k) s.s[k] = (const u32x4 *)sep[k]; return s; };
+    auto srcs_stag = [&](size_t st) {
+        Srcs s{};
+        for (int k = 0; k < 8; ++k) s.s[k] = (const u32x4 *)(big + k * (bytes + st));
+        return s;
+    };
+    auto rep = [&](const char *what, int k, double us) {
+        printf("%-58s k=%d %8.2f us %6.0f GB/s (k+1)S  %6.0f GB/s reads\n", what, k, us,
+               (k + 1.0) * bytes / us / 1e3, (double)k * bytes / us / 1e3);
+        fflush(stdout);
+    };
+    char name[128];
+#define RUN(KERNEL, K, U, ST, NT, BPC, SRCS, LABEL) do {                                            \
+        Srcs s_ = (SRCS);                                                                           \
+        snprintf(name, sizeof name, "%s<U%d,%s,%s> %d/CU %s", #KERNEL, U, #ST, NT ? "nt-ld" : "ld",  \
+                 BPC, LABEL);                                                                       \
+        rep(name, K, time_us([&] { hipLaunchKernelGGL((KERNEL<K, U, ST, NT>), dim3(cus * BPC), dim3(256), 0, 0, \
+                                                        s_, d, nvec); }));                          \
+    } while (0)
+
+    if (argc > 1 && argv[1][0] == 'c') {  // store policy of the copy and of the k = 2 / 4 / 8 folds
+        for (int r = 0; r < 2; ++r) {
+            RUN(fold_gs, 1, 4, ST_NT_SC1, 0, 1, srcs_sep(), "copy");
+            RUN(fold_gs, 1, 4, ST_SC1, 0, 1, srcs_sep(), "copy");
+            RUN(fold_gs, 1, 4, ST_NT, 0, 1, srcs_sep(), "copy");
+            RUN(fold_gs, 1, 4, ST_SC1, 0, 2, srcs_sep(), "copy");
+            RUN(fold_gs, 1, 4, ST_SC1, 1, 1, srcs_sep(), "copy");
+            RUN(fold_gs, 2, 1, ST_SC1, 1, 2, srcs_sep(), "");
+            RUN(fold_gs, 2, 2, ST_SC1, 1, 2, srcs_sep(), "");
+            RUN(fold_gs, 2, 1, ST_SC1, 1, 4, srcs_sep(), "");
+            RUN(fold_gs, 3, 2, ST_SC1, 1, 1, srcs_sep(), "");
+            RUN(fold_gs, 3, 2, ST_NT_SC1, 1, 1, srcs_sep(), "");
+            RUN(fold_gs, 4, 1, ST_SC1, 1, 1, srcs_sep(), "");
+            RUN(fold_gs, 4, 1, ST_NT_SC1, 1, 1, srcs_sep(), "");
+            RUN(fold_gs, 4, 2, ST_SC1, 1, 2, srcs_sep(), "");
+            RUN(fold_gs, 8, 4, ST_SC1, 1, 8, srcs_sep(), "");
+            RUN(fold_gs, 8, 4, ST_SC1, 1, 4, srcs_sep(), "");
+        }
+        return 0;
+    }
+    if (argc > 1) {  // placement/content study only
+        std::vector<void *> sepg(8);
+        for (int k = 0; k < 8; ++k) {
+            CHECK(hipMalloc(&sepg[k], 1ull << 30));
+            CHECK(hipMemset(sepg[k], 0x11 * (k + 1), 1ull << 30));
+        }
+        auto srcs_g = [&]() { Srcs s{}; for (int k = 0; k < 8; ++k) s.s[k] = (const u32x4 *)sepg[k]; return s; };
+        auto srcs_stag_mixed = [&]() {
+            Srcs s{};
+            for (int k = 0; k < 8; ++k) {
+                s.s[k] = (const u32x4 *)(big + k * bytes);
+                CHECK(hipMemset(big + k * bytes, 0x11 * (k + 1), bytes));
+            }
+            return s;
+        };
+        for (int r = 0; r < 2; ++r) {
+            RUN(fold_gs, 8, 4, ST_NT_SC1, 1, 8, srcs_sep(), "separate 256 MiB allocations");
+            RUN(fold_gs, 8, 4, ST_NONE, 1, 8, srcs_sep(), "separate 256 MiB allocations (no store)");
+            RUN(fold_gs, 8, 4, ST_NT_SC1, 1, 8, srcs_g(), "separate 1 GiB allocations");
+            RUN(fold_gs, 8, 4, ST_NONE, 1, 8, srcs_g(), "separate 1 GiB allocations (no store)");
+            RUN(fold_gs, 8, 4, ST_NT_SC1, 1, 8, srcs_stag_mixed(), "one allocation, per-source content");
+            RUN(fold_gs, 8, 4, ST_NONE, 1, 8, srcs_stag_mixed(), "one allocation, per-source content (no store)");
+            RUN(fold_gs, 8, 4, ST_SC1, 1, 8, srcs_stag_mixed(), "one allocation, per-source content");
+            RUN(fold_gs, 8, 2, ST_SC1, 1, 8, srcs_stag_mixed(), "one allocation, per-source content");
+            RUN(fold_gs, 8, 2, ST_SC1, 1, 4, srcs_stag_mixed(), "one allocation, per-source content");
+            RUN(fold_gs, 8, 4, ST_SC1, 1, 4, srcs_stag_mixed(), "one allocation, per-source content");
+            RUN(fold_gs, 8, 4, ST_NT_SC1, 0, 8, srcs_stag_mixed(), "one allocation, per-source content");
+            RUN(fold_gs, 8, 4, ST_SC1, 0, 8, srcs_stag_mixed(), "one allocation, per-source content");
+            RUN(fold_gs, 2, 1, ST_SC1, 1, 2, srcs_stag_mixed(), "one allocation, per-source content");
+            RUN(fold_gs, 2, 1, ST_NT_SC1, 1, 2, srcs_stag_mixed(), "one allocation, per-source content");
+            RUN(fold_gs, 2, 1, ST_NT, 1, 2, srcs_stag_mixed(), "one allocation, per-source content");
+        }
+        return 0;
+    }
+    for (int r = 0; r < 2; ++r) {
+        printf("--- pass %d\n", r);
+        // the library's k=8 shape on separate allocations, then read-only ceilings
+        RUN(fold_gs, 8, 4, ST_NT_SC1, 1, 8, srcs_sep(), "separate");
+        RUN(fold_gs, 8, 4, ST_NONE, 1, 8, srcs_sep(), "separate (no store: read ceiling)");
+        RUN(fold_gs, 1, 4, ST_NONE, 1, 8, srcs_sep(), "separate (no store: read ceiling)");
+        RUN(fold_gs, 2, 4, ST_NONE, 1, 8, srcs_sep(), "separate (no store: read ceiling)");
+        RUN(fold_gs, 4, 4, ST_NONE, 1, 8, srcs_sep(), "separate (no store: read ceiling)");
+        // placement
+        for (size_t st : {(size_t)0, (size_t)4096, (size_t)(68 << 10), (size_t)(1 << 20) + 4096,
+                          (size_t)(4 << 20) + 12288}) {
+            char lab[64];
+            snprintf(lab, sizeof lab, "stagger %zu B", st);
+            RUN(fold_gs, 8, 4, ST_NT_SC1, 1, 8, srcs_stag(st), lab);
+            RUN(fold_gs, 8, 4, ST_NONE, 1, 8, srcs_stag(st), lab);
+        }
+        // store policy
+        RUN(fold_gs, 8, 4, ST_NT, 1, 8, srcs_sep(), "separate");
+        RUN(fold_gs, 8, 4, ST_PLAIN, 1, 8, srcs_sep(), "separate");
+        RUN(fold_gs, 8, 4, ST_SC1, 1, 8, srcs_sep(), "separate");
+        // load policy
+        RUN(fold_gs, 8, 4, ST_NT_SC1, 0, 8, srcs_sep(), "separate");
+        // shapes
+        RUN(fold_gs, 8, 2, ST_NT_SC1, 1, 4, srcs_sep(), "separate");
+        RUN(fold_gs, 8, 2, ST_NT_SC1, 1, 8, srcs_sep(), "separate");
+        RUN(fold_gs, 8, 1, ST_NT_SC1, 1, 8, srcs_sep(), "separate");
+        RUN(fold_gs, 8, 1, ST_NT_SC1, 1, 4, srcs_sep(), "separate");
+        RUN(fold_part, 8, 1, ST_NT_SC1, 1, 2, srcs_sep(), "separate");
+        RUN(fold_part, 8, 2, ST_NT_SC1, 1, 2, srcs_sep(), "separate");
+        RUN(fold_part, 8, 1, ST_NT_SC1, 1, 4, srcs_sep(), "separate");
+        RUN(fold_part, 8, 2, ST_NT_SC1, 1, 4, srcs_sep(), "separate");
+        RUN(fold_part, 8, 4, ST_NT_SC1, 1, 4, srcs_sep(), "separate");
+        // k = 2 for reference
+        RUN(fold_gs, 2, 1, ST_NT_SC1, 1, 2, srcs_sep(), "separate");
+        RUN(fold_gs, 2, 1, ST_NT, 1, 2, srcs_sep(), "separate");
+        RUN(fold_gs, 2, 1, ST_NONE, 1, 2, srcs_sep(), "separate (no store)");
+        RUN(fold_part, 2, 2, ST_NT_SC1, 1, 2, srcs_sep(), "separate");
+        RUN(fold_part, 2, 4, ST_NT_SC1, 1, 1, srcs_sep(), "separate");
+    }
+    return 0;
+}
