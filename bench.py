@@ -422,6 +422,18 @@ def main():
     kernels = None
     if npes == 1 and not args.no_kernels and not args.host:
         kernels = kernel_legs(shm, args.kernel_reps, not args.no_check)
+        traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(traffic_file):
+            try:
+                pmc = json.load(open(traffic_file))
+            except ValueError:
+                pmc = {}
+            for name, leg in kernels.items():
+                tr = pmc.get(f"kernel_{name}") if isinstance(leg, dict) else None
+                if tr:
+                    leg["traffic"] = tr["hbm_bytes_per_launch"]
+                    leg["traffic_over_alg"] = round(tr["hbm_bytes_per_launch"] / leg["alg_bytes_per_launch"], 4)
+                    leg["traffic_source"] = tr["source"]
 
     # BASELINE config 4 (op coverage): shmem_float_max_to_all and
     # shmem_longlong_and_to_all on 64 MiB per PE, timed like the headline
