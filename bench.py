@@ -112,6 +112,43 @@ def cpu_baseline(S, n_gpus, budget_s):
             "host": {"nproc": os.cpu_count(), "allowed_cpus": allowed, "cpu_model": cpu_model()}}
 
 
+def fused_same_gpu(npes, calls):
+    """The fused one-launch schedule (fused.hip), which every call up to 1 MiB
+    per PE takes at N > 1, measured on this box's one GPU: `npes` PE processes
+    of tools/fused_bench.py sharing it (started from this process before it
+    touches the GPU). Per-call time for BASELINE config 5's 64 KiB calls
+    (one-shot fold) and 1 MiB (reduce-scatter + all-gather in one launch), the
+    fused kernel's own duration (HIP event stamps), and a bit-exact check of
+    every PE's result. Same-GPU figures: the 'remote' reads are this GPU's HBM,
+    not xGMI."""
+    import subprocess
+    import uuid
+    env = dict(os.environ, SHMEM_NPES=str(npes), SHMEM_JOB_ID="fb" + uuid.uuid4().hex[:10], SHMEM_DEVICE="0")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    script = os.path.join(ROOT, "tools", "fused_bench.py")
+    procs = [subprocess.Popen([sys.executable, script, str(calls)], env=dict(env, SHMEM_PE=str(pe)),
+                              stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for pe in range(npes)]
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=180))
+    except subprocess.TimeoutExpired:
+        for p in procs:
+            p.kill()
+        return {"error": "timed out"}
+    if any(p.returncode != 0 for p in procs):
+        return {"error": "; ".join(f"PE {i} rc {p.returncode}: {o[1][-300:]}" for i, (p, o) in enumerate(zip(procs, outs))
+                                   if p.returncode != 0)}
+    lines = [ln for ln in outs[0][0].splitlines() if ln.startswith("{")]
+    if not lines:
+        return {"error": "no result line from PE 0"}
+    d = json.loads(lines[-1])
+    d["note"] = ("fused_allreduce (one launch per call: device-side arrival/done flags) with the PEs sharing this one "
+                 "GPU; us_per_call is entry-to-return, max over PEs; kernel_avg_us the fused kernel's duration")
+    return d
+
+
 # ---------------------------------------------------------------------------
 # kernel legs (N = 1): the fold kernels themselves, timed on one GPU
 # ---------------------------------------------------------------------------
@@ -242,6 +279,8 @@ def main():
                     help="N = 1: skip the kernel legs (the fold kernels timed alone: k = 2 / 8 sources of "
                          "256 MiB, config 3 / 4's per-GPU reduce-scatter shapes)")
     ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--no-fused", action="store_true",
+                    help="N = 1: skip the fused-kernel leg (2 PE processes sharing this GPU, 64 KiB and 1 MiB calls)")
     ap.add_argument("--host", action="store_true",
                     help="source/target in host memory (shmem_malloc, page-locked): the rate includes the "
                          "H2D/D2H staging copies (DESIGN.md); not the headline metric")
@@ -258,6 +297,11 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(S, args.gpus, args.cpu_seconds)
+    # the fused kernel on 2 PE processes sharing this GPU (children; this
+    # process has not touched the GPU yet)
+    fused = None
+    if world == 1 and not args.no_fused and not args.host:
+        fused = fused_same_gpu(2, 4096 if args.no_small is False else 512)
 
     os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(2 * S + (64 << 20)))
     os.environ.setdefault("SHMEM_DEVICE_SCRATCH_SIZE", str(96 << 20))
@@ -575,6 +619,7 @@ def main():
             "check": check,
             "op_coverage": ops,
             "kernels": kernels,
+            "fused_same_gpu": fused,
         }
         print(json.dumps(out), flush=True)
     if args.host:

@@ -874,6 +874,14 @@ extern "C" void mi355_time_next_launch(void *start_event, void *stop_event) {
     t_ev_stop = (hipEvent_t)stop_event;
 }
 
+// For fused.hip (same library): take the event pair armed for the next
+// launch, if any, so its kernels carry the stamps too.
+extern "C" void mi355i_take_launch_events(void **start_event, void **stop_event) {
+    *start_event = t_ev_start;
+    *stop_event = t_ev_stop;
+    t_ev_start = t_ev_stop = nullptr;
+}
+
 // short <-> int32 for the RCCL schedule (RCCL has no 16-bit integer type):
 // sum/prod wrap mod 2^32 in int32, and truncating to 16 bits afterwards gives
 // the same bits as the reference's per-step promote-and-truncate (truncation

@@ -40,6 +40,7 @@
 // capped by the kernel's occupancy and the number of such PEs
 // (coresident_grid; at most MI355_FUSED_MAX_BLOCKS, one block per CU).
 // Every wait is bounded by p.timeout_ticks of the 100 MHz real-time counter.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <type_traits>
@@ -463,6 +464,20 @@ __global__ __launch_bounds__(64) void device_barrier(MI355FusedArgs a) {
     finish(a, mine, cnt, ok);
 }
 
+extern "C" void mi355i_take_launch_events(void **start_event, void **stop_event);  // combine.hip
+
+// Launch, carrying the event pair armed by mi355_time_next_launch (if any)
+// as hipExtLaunchKernel stamps: no marker packets on the stream.
+template <typename K, typename P>
+void launch_stamped(K kernel, unsigned grid, unsigned block, hipStream_t st, const P &p) {
+    void *e0 = nullptr, *e1 = nullptr;
+    mi355i_take_launch_events(&e0, &e1);
+    if (e0 != nullptr || e1 != nullptr)
+        hipExtLaunchKernelGGL(kernel, dim3(grid), dim3(block), 0, st, (hipEvent_t)e0, (hipEvent_t)e1, 0, p);
+    else
+        hipLaunchKernelGGL(kernel, dim3(grid), dim3(block), 0, st, p);
+}
+
 // Co-residency: every block of these grids waits for the grid's last block
 // and for the other members, so all blocks of every such grid running on this
 // GPU at once must be resident together. A launch is capped at the kernel's
@@ -513,8 +528,7 @@ int launch_op(const MI355FusedArgs &a, unsigned grid, hipStream_t st) {
     case O:                                                                            \
         if constexpr (valid_pair<O, T>()) {                                           \
             auto k = fused_allreduce<O, T>;                                            \
-            hipLaunchKernelGGL(k, dim3(coresident_grid((const void *)k, grid, a.share)), \
-                               dim3(kBlock), 0, st, a);                                \
+            launch_stamped(k, coresident_grid((const void *)k, grid, a.share), kBlock, st, a); \
             break;                                                                     \
         } else {                                                                       \
             return MI355_E_UNSUP;                                                      \
@@ -627,8 +641,8 @@ extern "C" int mi355_fused_pull(const MI355PullArgs *p, void *stream) {
     uint64_t grid = (total + 16 * kBlock - 1) / (16 * kBlock);
     if (grid < 1) grid = 1;
     if (grid > MI355_FUSED_MAX_BLOCKS) grid = MI355_FUSED_MAX_BLOCKS;
-    hipLaunchKernelGGL(fused_pull, dim3(coresident_grid((const void *)fused_pull, grid, a->share)), dim3(kBlock), 0,
-                       (hipStream_t)stream, *p);
+    launch_stamped(fused_pull, coresident_grid((const void *)fused_pull, grid, a->share), kBlock, (hipStream_t)stream,
+                   *p);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }

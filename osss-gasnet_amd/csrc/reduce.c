@@ -465,7 +465,9 @@ static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t sr
     a.share = shmemi.local_pes;
     a.oneshot = n * es <= shmemi.oneshot_max && dst_off != src_off;
     fused_order (&a, s, SHMEMI_CHAN_HOST);
+    shmemi_timed_begin (); /* the call's one (dominant) kernel */
     const int rc = mi355_fused_allreduce (&a, shmemi.stream);
+    shmemi_timed_end ();
     if (rc != 0)
         shmemi_fatal ("fused reduction launch failed (op %d, dtype %d, %d PEs, %zu elements): %d", op, dtype,
                       s->size, n, rc);

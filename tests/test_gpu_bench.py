@@ -54,6 +54,10 @@ def test_bench_one_gpu_line():
                  "fold_k8_longlong_and", "rs_shard_n8_float_max"):
         assert k[name]["check"].startswith("bit-exact"), (name, k[name])
         assert 0 < k[name]["frac"] < 1.2 and k[name]["kernel_avg_us"] > 0, (name, k[name])
+    f = d["fused_same_gpu"]
+    assert "error" not in f, f
+    for leg in f["legs"].values():
+        assert leg["check"].startswith("bit-exact") and leg["us_per_call"] > 0 and leg["kernel_avg_us"] > 0, leg
 
 
 @pytest.mark.multipe

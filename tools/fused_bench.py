@@ -1,0 +1,85 @@
+#!/usr/bin/env python3
+"""One PE of the same-GPU fused-kernel measurement (bench.py's `fused_same_gpu`
+leg, tools/profile_fused.sh). Run as NPES processes with SHMEM_PE / SHMEM_NPES
+/ SHMEM_JOB_ID set and SHMEM_DEVICE=0 (every PE on this GPU).
+
+For each message size, K back-to-back shmem_double_sum_to_all calls from a C
+loop (csrc/bench_loop.c): per-call time (max over PEs), then the same K calls
+with the fused kernel's own HIP event stamps (its average duration), and every
+PE's result checked bit-exact against the oracle's result for that PE (the
+reference's own-source-first order). PE 0 prints one JSON line.
+
+usage: fused_bench.py [calls] [sizes in bytes...]
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, "osss-gasnet_amd"), os.path.join(ROOT, "oracle")]
+import shmem_reduce  # noqa: E402
+
+
+def synth(pe, n):
+    return (np.random.default_rng(1000 + pe).random(n) - 0.5) * np.exp2(np.random.default_rng(pe).integers(0, 8, n))
+
+
+def main():
+    calls = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+    sizes = [int(x) for x in sys.argv[2:]] or [64 << 10, 1 << 20]
+    os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(8 << 20))
+    os.environ.setdefault("SHMEM_DEVICE_SCRATCH_SIZE", "3M")
+    os.environ.setdefault("SHMEM_DEVICE_ORDER_SIZE", "8M")
+    shm = shmem_reduce.Shmem()
+    shm.init()
+    me, npes = shm.my_pe(), shm.n_pes()
+    maxb = max(sizes)
+    src, dst = shm.malloc_device(maxb), shm.malloc_device(maxb)
+    loop = shmem_reduce.bench_loop()
+
+    def max_over_pes(x):
+        a, b = np.array([x], dtype=np.float64), np.zeros(1, dtype=np.float64)
+        shm.to_all("max", "double", b.ctypes.data, a.ctypes.data, 1, 0, 0, npes)
+        return float(b[0])
+
+    out = {}
+    import oracle
+    for nb in sizes:
+        n = nb // 8
+        x = synth(me, n)
+        shm.put(src, x)
+        loop(dst, src, n, 0, 0, npes, None, shm._psync_ptr, 20)
+        shm.barrier_all()
+        shm.sync()
+        t0 = time.perf_counter()
+        loop(dst, src, n, 0, 0, npes, None, shm._psync_ptr, calls)
+        shm.sync()
+        t = max_over_pes(time.perf_counter() - t0) / calls
+        shm.barrier_all()
+        shm.kernel_timing(True)
+        loop(dst, src, n, 0, 0, npes, None, shm._psync_ptr, calls)
+        shm.sync()
+        nk, _, kavg = shm.kernel_timing_stats()
+        shm.kernel_timing(False)
+        got = shm.get(dst, n, "double")
+        want = oracle.reduce_pe("sum", "double", [synth(p, n) for p in range(npes)], me)
+        bad = int(max_over_pes(int((got.view(np.uint64) != want.view(np.uint64)).sum())))
+        kmax = max_over_pes(kavg)
+        out[str(nb)] = {"bytes_per_pe": nb, "calls": calls, "us_per_call": round(t * 1e6, 2),
+                        "kernel_avg_us": round(kmax * 1e3, 2), "kernels_timed": nk,
+                        "schedule": "fused one-shot" if nb <= 64 << 10 else "fused reduce-scatter + all-gather",
+                        "check": f"bit-exact vs the reference's per-PE order on every PE, {n} elements each"
+                        if bad == 0 else f"MISMATCH {bad} elements (worst PE)"}
+        shm.barrier_all()
+    shm.free_device(dst)
+    shm.free_device(src)
+    if me == 0:
+        print(json.dumps({"npes": npes, "same_gpu": True, "legs": out}), flush=True)
+    shm.finalize()
+
+
+if __name__ == "__main__":
+    main()
