@@ -128,6 +128,9 @@ void shmemi_trace_show_info (void)
         {"SHMEM_DEVICE_SCRATCH_SIZE", "staging/temporary scratch per PE (3 buffers)"},
         {"SHMEM_SYMMETRIC_HEAP_KIND", "\"device\": shmem_malloc returns device memory"},
         {"SHMEM_REDUCE_ALGORITHM", "auto | p2p | exact | rccl"},
+        {"SHMEM_REDUCE_ORDER", "reference (each PE gets the reference's result for itself) | pe_start"},
+        {"SHMEM_DEVICE_ORDER_SIZE", "version areas of the per-PE-order schedule (default 512M, 2 channels)"},
+        {"SHMEM_FUSED_GRID_SHARE", "size the spin-waiting grids as if this many PEs shared the GPU"},
         {"SHMEM_FUSED_MAX_BYTES", "largest message for the one-launch fused reduction (default 1M)"},
         {"SHMEM_ONESHOT_MAX_BYTES", "largest fused message folded one-shot, not reduce-scatter + all-gather (default 64K)"},
         {"SHMEM_BARRIER_TIMEOUT", "seconds before a barrier wait aborts the job (default 600)"},
