@@ -76,6 +76,63 @@ __global__ __launch_bounds__(256) void fold_gs(Srcs in, u32x4 *d, size_t nvec) {
     }
 }
 
+// as fold_gs, but the loads issued source-major: src0's U vectors, then src1's, ...
+template <int K, int U, int ST, int NT>
+__global__ __launch_bounds__(256) void fold_sm(Srcs in, u32x4 *d, size_t nvec) {
+    const size_t step = (size_t)gridDim.x * 256 * U;
+    for (size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x; base < nvec; base += step) {
+        P2 x[U][K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                size_t i = base + (size_t)u * 256;
+                if (i < nvec) x[u][k].v = load<NT>(in.s[k] + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            size_t i = base + (size_t)u * 256;
+            if (i < nvec) {
+                P2 a = x[u][0];
+#pragma unroll
+                for (int k = 1; k < K; ++k) {
+                    a.e[0] = a.e[0] + x[u][k].e[0];
+                    a.e[1] = a.e[1] + x[u][k].e[1];
+                }
+                store<ST>(d + i, a.v);
+            }
+        }
+    }
+}
+
+// each lane owns U CONSECUTIVE vectors (64 B per source per lane at U = 4): a wave covers 4 KiB per source
+template <int K, int U, int ST, int NT>
+__global__ __launch_bounds__(256) void fold_lane(Srcs in, u32x4 *d, size_t nvec) {
+    const size_t step = (size_t)gridDim.x * 256 * U;
+    for (size_t base = ((size_t)blockIdx.x * 256 + threadIdx.x) * U; base < nvec; base += step) {
+        P2 x[U][K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+                if (base + u < nvec) x[u][k].v = load<NT>(in.s[k] + base + u);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (base + u < nvec) {
+                P2 a = x[u][0];
+#pragma unroll
+                for (int k = 1; k < K; ++k) {
+                    a.e[0] = a.e[0] + x[u][k].e[0];
+                    a.e[1] = a.e[1] + x[u][k].e[1];
+                }
+                store<ST>(d + base + u, a.v);
+            }
+        }
+    }
+}
+
 // each block owns one contiguous range (chunk of `per` vectors), U vectors per lane per step
 template <int K, int U, int ST, int NT>
 __global__ __launch_bounds__(256) void fold_part(Srcs in, u32x4 *d, size_t nvec) {
@@ -173,6 +230,24 @@ int main(int argc, char **argv) {
                                                         s_, d, nvec); }));                          \
     } while (0)
 
+    if (argc > 1 && argv[1][0] == 'o') {  // load order / lane layout at k = 8 and k = 2
+        for (int r = 0; r < 2; ++r) {
+            RUN(fold_gs, 8, 4, ST_SC1, 1, 8, srcs_sep(), "library shape");
+            RUN(fold_sm, 8, 4, ST_SC1, 1, 8, srcs_sep(), "source-major loads");
+            RUN(fold_sm, 8, 4, ST_SC1, 1, 4, srcs_sep(), "source-major loads");
+            RUN(fold_sm, 8, 2, ST_SC1, 1, 8, srcs_sep(), "source-major loads");
+            RUN(fold_lane, 8, 4, ST_SC1, 1, 4, srcs_sep(), "4 consecutive vectors per lane");
+            RUN(fold_lane, 8, 2, ST_SC1, 1, 8, srcs_sep(), "2 consecutive vectors per lane");
+            RUN(fold_lane, 8, 4, ST_SC1, 1, 8, srcs_sep(), "4 consecutive vectors per lane");
+            RUN(fold_gs, 8, 4, ST_SC1, 1, 8, srcs_stag(0), "one arena");
+            RUN(fold_sm, 8, 4, ST_SC1, 1, 8, srcs_stag(0), "one arena, source-major");
+            RUN(fold_gs, 2, 1, ST_SC1, 1, 2, srcs_sep(), "library shape");
+            RUN(fold_sm, 2, 2, ST_SC1, 1, 2, srcs_sep(), "source-major loads");
+            RUN(fold_lane, 2, 2, ST_SC1, 1, 2, srcs_sep(), "2 consecutive vectors per lane");
+            RUN(fold_lane, 2, 4, ST_SC1, 1, 1, srcs_sep(), "4 consecutive vectors per lane");
+        }
+        return 0;
+    }
     if (argc > 1 && argv[1][0] == 'c') {  // store policy of the copy and of the k = 2 / 4 / 8 folds
         for (int r = 0; r < 2; ++r) {
             RUN(fold_gs, 1, 4, ST_NT_SC1, 0, 1, srcs_sep(), "copy");
