@@ -28,248 +28,11 @@
 #include <stdint.h>
 #include <type_traits>
 
+#include "combine_kernels.h"
 #include "mi355_reduce.h"
 #include "ops.h"
 
-namespace {
-
-using namespace mi355;
-
-constexpr int kBlock = 256;
-constexpr int kMaxSrc = 8;
-
-// ---------------------------------------------------------------------------
-// kernels
-// ---------------------------------------------------------------------------
-// Completion signal (mi355_signal_next_launch): the last block to finish
-// stores `epoch` into a host-visible word, so the host learns the result is
-// in memory ~4 us sooner than through hipStreamSynchronize (tools/latency.hip:
-// 6.9 vs 10.7 us for a launch round trip on MI355X).
-struct Signal {
-    unsigned *count;  // device word, 0 between launches (the last block resets it)
-    unsigned *flag;   // host-coherent word the host spins on; nullptr = no signal
-    unsigned epoch;
-};
-
-// Publish recipe of MI355X_MICROARCH.md (inter-workgroup visibility, valid
-// form "sc1 payload + drained waves + flag"): the bulk stores are
-// write-through (`nt sc1`, st16), so once every wave has drained its stores
-// they are in memory for any agent; a block that also made plain stores (an
-// element tail, an unaligned kernel) first writes its XCD's L2 back with an
-// agent-scope release. One lane per block counts the block in; the last
-// block resets the counter and stores the epoch to the host-coherent flag.
-__device__ __forceinline__ void signal_done(const Signal &sg, bool plain_stores) {
-    if (sg.flag == nullptr) return;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (plain_stores) {
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        const unsigned total = gridDim.x * gridDim.y;
-        const unsigned prev = __hip_atomic_fetch_add(sg.count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (prev + 1 == total) {
-            __hip_atomic_store(sg.count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __hip_atomic_store(sg.flag, sg.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-}
-
-struct CombineParams {
-    void *dst;
-    const void *src[kMaxSrc];
-    uint64_t nvec;   // vector kernel: whole 16-byte vectors; scalar kernel: elements
-    uint32_t tail;   // vector kernel: elements after nvec*V (< V)
-    uint32_t head;   // vector kernel: elements just BEFORE dst/src (pointers advanced to 16-byte alignment)
-    Signal sig;
-};
-
-// Cache policy (tools/hbm_sweep.hip, MI355X, 256 MiB per buffer):
-//   stores: write-through to memory at agent scope, which makes the completion
-//     signal cheap: no per-block L2 write-back (that cost 60 us on a 256 MiB
-//     copy with 2048 blocks). The copy: `nt sc1`, as fast as plain
-//     non-temporal stores (6.82 TB/s); the folds: `sc1` (st16_fold), 3-10 %
-//     faster than `nt sc1` beside their non-temporal loads.
-//   loads: plain for the copy (6.8 TB/s vs 6.1 non-temporal), non-temporal
-//     for folds (Shape<NSRC>::policy).
-enum { POL_PLAIN = 0, POL_NT_LOAD = 1 };
-
-template <int POL>
-__device__ __forceinline__ u32x4 ld16(const u32x4 *p) {
-    if constexpr ((POL & POL_NT_LOAD) != 0) return __builtin_nontemporal_load(p);
-    else return *p;
-}
-__device__ __forceinline__ void st16(u32x4 *p, u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-}
-// The folds' stores: write-through at agent scope WITHOUT the non-temporal
-// hint. Beside non-temporal loads this is the faster form (tools/fold_probe.hip,
-// profiles/r02/fold_probe_copy.txt, 256 MiB per source: k = 2 116.4 vs 127.9 us,
-// k = 3 158.7 vs 177.1, k = 8 393.5 vs 422); the copy keeps `nt sc1` (with
-// its plain loads `sc1` alone is 18 % slower).
-__device__ __forceinline__ void st16_fold(u32x4 *p, u32x4 v) {
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-}
-
-// Vector path: every pointer 16-byte aligned. Each lane owns UNROLL vectors
-// spaced one block apart (so a wave touches contiguous 1 KiB per source per
-// step) and issues all NSRC*UNROLL loads before combining.
-template <int OP, typename T, int NSRC, int UNROLL, int POL>
-__global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
-    constexpr int V = 16 / sizeof(T);
-    const u32x4 *s[NSRC];
-#pragma unroll
-    for (int k = 0; k < NSRC; ++k) s[k] = (const u32x4 *)p.src[k];
-    u32x4 *d = (u32x4 *)p.dst;
-    const uint64_t nvec = p.nvec;
-    const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
-    for (uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x; base < nvec;
-         base += step) {
-        Pack<T> x[UNROLL][NSRC];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            const uint64_t i = base + (uint64_t)u * kBlock;
-            if (i < nvec) {
-#pragma unroll
-                for (int k = 0; k < NSRC; ++k) x[u][k].v = ld16<POL>(s[k] + i);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            const uint64_t i = base + (uint64_t)u * kBlock;
-            if (i < nvec) {
-                Pack<T> acc = x[u][0];
-#pragma unroll
-                for (int k = 1; k < NSRC; ++k) {
-#pragma unroll
-                    for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[u][k].e[e]);
-                }
-                st16_fold(d + i, acc.v);
-            }
-        }
-    }
-    const bool tail_block = V > 1 && p.tail != 0 && blockIdx.x == 0;
-    if (tail_block && threadIdx.x < p.tail) {
-        const uint64_t i = nvec * V + threadIdx.x;
-        T acc = ((const T *)p.src[0])[i];
-#pragma unroll
-        for (int k = 1; k < NSRC; ++k) acc = apply<OP>(acc, ((const T *)p.src[k])[i]);
-        ((T *)p.dst)[i] = acc;
-    }
-    const bool head_block = V > 1 && p.head != 0 && blockIdx.x == 0;
-    if (head_block && threadIdx.x < p.head) {
-        const int64_t i = (int64_t)threadIdx.x - (int64_t)p.head;
-        T acc = ((const T *)p.src[0])[i];
-#pragma unroll
-        for (int k = 1; k < NSRC; ++k) acc = apply<OP>(acc, ((const T *)p.src[k])[i]);
-        ((T *)p.dst)[i] = acc;
-    }
-    signal_done(p.sig, tail_block || head_block);
-}
-
-// Scalar path for pointers that are not 16-byte aligned (user offsets into
-// arrays). Coalesced element loads, grid-stride.
-template <int OP, typename T, int NSRC>
-__global__ __launch_bounds__(kBlock) void combine_scalar(CombineParams p) {
-    const T *s[NSRC];
-#pragma unroll
-    for (int k = 0; k < NSRC; ++k) s[k] = (const T *)p.src[k];
-    T *d = (T *)p.dst;
-    const uint64_t n = p.nvec;
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n;
-         i += (uint64_t)gridDim.x * kBlock) {
-        T v[NSRC];
-#pragma unroll
-        for (int k = 0; k < NSRC; ++k) v[k] = s[k][i];
-        T acc = v[0];
-#pragma unroll
-        for (int k = 1; k < NSRC; ++k) acc = apply<OP>(acc, v[k]);
-        d[i] = acc;
-    }
-    signal_done(p.sig, true);
-}
-
-// Every member's reference order in one pass (mi355_combine_orders). On
-// member q the reference folds its OWN source first and then the others in
-// active-set order (reduce-op.c:226-264), so for order-sensitive operators (FP
-// rounding; the NaN and +-0 selects of min/max) the members' results differ.
-// The owner of a shard loads the NSRC sources once and computes every fold
-// from registers: dst[q] = fold(src[q], src[0], .., src[q-1], src[q+1], ..).
-// A null dst[q] skips fold q (a kernel argument: the branch is uniform).
-struct OrdersParams {
-    void *dst[kMaxSrc];
-    const void *src[kMaxSrc];
-    uint64_t nvec;  // as CombineParams
-    uint32_t tail;
-    uint32_t head;
-    Signal sig;
-};
-
-template <int OP, typename T, int NSRC>
-__device__ __forceinline__ void orders_element(const OrdersParams &p, int64_t i) {
-    T v[NSRC];
-#pragma unroll
-    for (int k = 0; k < NSRC; ++k) v[k] = ((const T *)p.src[k])[i];
-#pragma unroll
-    for (int q = 0; q < NSRC; ++q) {
-        if (p.dst[q] == nullptr) continue;
-        T acc = v[q];
-#pragma unroll
-        for (int k = 0; k < NSRC; ++k)
-            if (k != q) acc = apply<OP>(acc, v[k]);
-        ((T *)p.dst[q])[i] = acc;
-    }
-}
-
-template <int OP, typename T, int NSRC, int UNROLL, int POL>
-__global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
-    constexpr int V = 16 / sizeof(T);
-    const uint64_t nvec = p.nvec;
-    const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
-    for (uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x; base < nvec;
-         base += step) {
-        Pack<T> x[UNROLL][NSRC];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            const uint64_t i = base + (uint64_t)u * kBlock;
-            if (i < nvec) {
-#pragma unroll
-                for (int k = 0; k < NSRC; ++k) x[u][k].v = ld16<POL>((const u32x4 *)p.src[k] + i);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            const uint64_t i = base + (uint64_t)u * kBlock;
-            if (i >= nvec) continue;
-#pragma unroll
-            for (int q = 0; q < NSRC; ++q) {
-                if (p.dst[q] == nullptr) continue;
-                Pack<T> acc = x[u][q];
-#pragma unroll
-                for (int k = 0; k < NSRC; ++k) {
-                    if (k == q) continue;
-#pragma unroll
-                    for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[u][k].e[e]);
-                }
-                st16_fold((u32x4 *)p.dst[q] + i, acc.v);
-            }
-        }
-    }
-    const bool tail_block = V > 1 && p.tail != 0 && blockIdx.x == 0;
-    if (tail_block && threadIdx.x < p.tail) orders_element<OP, T, NSRC>(p, (int64_t)(nvec * V + threadIdx.x));
-    const bool head_block = V > 1 && p.head != 0 && blockIdx.x == 0;
-    if (head_block && threadIdx.x < p.head) orders_element<OP, T, NSRC>(p, (int64_t)threadIdx.x - (int64_t)p.head);
-    signal_done(p.sig, tail_block || head_block);
-}
-
-template <int OP, typename T, int NSRC>
-__global__ __launch_bounds__(kBlock) void combine_orders_scalar(OrdersParams p) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < p.nvec; i += (uint64_t)gridDim.x * kBlock)
-        orders_element<OP, T, NSRC>(p, (int64_t)i);
-    signal_done(p.sig, true);
-}
+namespace mi355k {
 
 // Byte copy of up to NS segments in one launch; blockIdx.y = segment. NS = 1
 // (the 1-PE identity, the bench's call) keeps the kernel arguments at 48
@@ -377,295 +140,9 @@ struct EmptyParams {
 };
 __global__ __launch_bounds__(kBlock) void signal_only(EmptyParams p) { signal_done(p.sig, false); }
 
-// ---------------------------------------------------------------------------
-// launch helpers
-// ---------------------------------------------------------------------------
-int g_cus[64];
+}  // namespace mi355k
 
-// events and completion signal for the next launch (mi355_time_next_launch,
-// mi355_signal_next_launch), consumed by it
-thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
-thread_local Signal t_sig = {nullptr, nullptr, 0};
-
-// A host-visible word the host can also write: an armed signal that no kernel
-// will carry (nothing to launch) is fired right here, in stream order.
-void fire_on_host(hipStream_t st) {
-    if (t_sig.flag == nullptr) return;
-    if (hipStreamSynchronize(st) == hipSuccess)
-        __atomic_store_n(t_sig.flag, t_sig.epoch, __ATOMIC_RELEASE);
-    t_sig = Signal{nullptr, nullptr, 0};
-}
-
-// `final`: the last launch of an API call, the one that carries the signal
-template <typename K, typename P>
-int launch(K kernel, dim3 grid, hipStream_t st, P p, bool final = true) {
-    p.sig = Signal{nullptr, nullptr, 0};
-    if (final) {
-        p.sig = t_sig;
-        t_sig = Signal{nullptr, nullptr, 0};
-    }
-    if (t_ev_start != nullptr || t_ev_stop != nullptr) {
-        hipExtLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, st, t_ev_start, t_ev_stop, 0, p);
-        t_ev_start = t_ev_stop = nullptr;
-    } else {
-        hipLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, st, p);
-    }
-    hipError_t e = hipGetLastError();
-    return e == hipSuccess ? 0 : (int)e;
-}
-
-int device_cus() {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    if (g_cus[dev] == 0) {
-        int cus = 0;
-        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
-            cus <= 0)
-            cus = 256;
-        g_cus[dev] = cus;
-    }
-    return g_cus[dev];
-}
-
-// Blocks for a streaming launch: enough to cover the work once, capped at
-// kBlocksPerCU resident blocks per CU (grid-stride covers the rest).
-constexpr int kBlocksPerCU = 8;
-
-unsigned grid_for(uint64_t units_per_block_pass, uint64_t units, int blocks_per_cu = kBlocksPerCU) {
-    uint64_t want = (units + units_per_block_pass - 1) / units_per_block_pass;
-    uint64_t cap = (uint64_t)device_cus() * blocks_per_cu;
-    if (want < 1) want = 1;
-    return (unsigned)(want < cap ? want : cap);
-}
-
-// Launch shape per source count, from tools/hbm_sweep.hip and
-// tools/fold_bench.py on MI355X (256 MiB per source, double sums,
-// non-temporal loads + `nt sc1` stores; GB/s counts (k+1) x 256 MiB;
-// profiles/r01/hbm_sweep_v5.txt, fold_bench_k_sources.jsonl):
-//   k=2: 1 vector/lane,  2 blocks/CU     6.4 TB/s
-//   k=3: 2 vectors/lane, 1 block/CU      6.5 TB/s
-//   k=4: 1 vector/lane,  1 block/CU      6.2-6.3 TB/s
-//   k=8: 4 vectors/lane, 8 blocks/CU     5.8-5.9 TB/s (k=5..7 take k=8's
-//        depth at half the blocks)
-// Box-to-box spread is +-3 %, so neighbours within that band are ties.
-// Long double is VALU-bound (x87 arithmetic in software): it wants many
-// waves to hide ALU latency, not deep per-lane load queues.
-template <int NSRC, typename T> struct Shape {
-    static constexpr bool alu_heavy = std::is_same<T, x80>::value;
-    static constexpr int unroll =
-        alu_heavy ? 1 : NSRC == 2 ? 1 : NSRC == 3 ? 2 : NSRC == 4 ? 1 : NSRC < 8 ? 2 : 4;
-    static constexpr int blocks_per_cu =
-        alu_heavy ? 8 : NSRC == 2 ? 2 : NSRC == 3 ? 1 : NSRC == 4 ? 1 : NSRC < 8 ? 4 : 8;
-    static constexpr int policy = POL_NT_LOAD;
-};
-
-// mi355_combine_orders: NSRC loads and up to NSRC stores per vector (every
-// member's fold); the loads in flight per lane are those of the fold of the
-// same width. Complex types: one vector per lane (NSRC*(NSRC-1) complex
-// products per vector do not fit the registers of deeper unrolling; the
-// loads in flight come from more blocks instead).
-template <int NSRC, typename T> struct OrdersShape {
-    static constexpr bool cplx = std::is_same<T, cplxf>::value || std::is_same<T, cplxd>::value;
-    using S = Shape<NSRC, T>;
-    static constexpr int unroll = cplx ? 1 : S::unroll;
-    static constexpr int blocks_per_cu = cplx ? (S::blocks_per_cu * S::unroll < 8 ? S::blocks_per_cu * S::unroll : 8)
-                                              : S::blocks_per_cu;
-    static constexpr int policy = POL_NT_LOAD;
-};
-
-// How a launch over these pointers can run as 16-byte vectors: 0 = every
-// pointer aligned; h > 0 = every pointer equally misaligned by whole elements
-// (a user offset into the arrays): fold the first h elements element-wise and
-// the rest as vectors from the advanced pointers (peeled to a 128-byte line
-// when all share the misalignment within the line, else to 16 bytes); -1 =
-// element-wise kernel.
-template <typename T>
-long vector_head(const void *const *ptrs, int np, size_t n) {
-    constexpr int V = 16 / sizeof(T);
-    uintptr_t orbits = 0;
-    for (int k = 0; k < np; ++k) orbits |= (uintptr_t)ptrs[k];
-    if ((orbits & 15) == 0) return 0;
-    if (V == 1) return -1;
-    uintptr_t mis = (uintptr_t)ptrs[0] & 127;
-    bool line = true;
-    for (int k = 1; k < np; ++k) line = line && ((uintptr_t)ptrs[k] & 127) == mis;
-    if (!line) mis &= 15;
-    bool same = mis % sizeof(T) == 0;
-    for (int k = 1; k < np; ++k) same = same && ((uintptr_t)ptrs[k] & (line ? 127 : 15)) == mis;
-    const size_t head = ((line ? 128 : 16) - mis) / sizeof(T);
-    return same && n > head ? (long)head : -1;
-}
-
-template <int OP, typename T, int NSRC>
-int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, bool final) {
-    CombineParams p{};
-    const void *ptrs[kMaxSrc + 1];
-    p.dst = dst;
-    ptrs[0] = dst;
-    for (int k = 0; k < NSRC; ++k) p.src[k] = ptrs[1 + k] = srcs[k];
-    constexpr int V = 16 / sizeof(T);
-    const long head = vector_head<T>(ptrs, NSRC + 1, n);
-    if (head >= 0) {
-        if (head > 0) {
-            p.head = (uint32_t)head;
-            p.dst = (char *)dst + head * sizeof(T);
-            for (int k = 0; k < NSRC; ++k) p.src[k] = (const char *)srcs[k] + head * sizeof(T);
-            n -= (size_t)head;
-        }
-        using S = Shape<NSRC, T>;
-        p.nvec = n / V;
-        p.tail = (uint32_t)(n % V);
-        const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, S::blocks_per_cu);
-        return launch(combine_vec<OP, T, NSRC, S::unroll, S::policy>, dim3(grid), st, p, final);
-    }
-    p.nvec = n;
-    p.tail = 0;
-    const unsigned grid = grid_for((uint64_t)kBlock * 4, n);
-    return launch(combine_scalar<OP, T, NSRC>, dim3(grid), st, p, final);
-}
-
-// mi355_combine_orders for NSRC <= kMaxSrc sources: one launch
-template <int OP, typename T, int NSRC>
-int launch_orders_fixed(void *const *dsts, const void *const *srcs, size_t n, hipStream_t st) {
-    OrdersParams p{};
-    const void *ptrs[2 * kMaxSrc];
-    int np = 0;
-    for (int k = 0; k < NSRC; ++k) {
-        p.src[k] = ptrs[np++] = srcs[k];
-        p.dst[k] = dsts[k];
-        if (dsts[k] != nullptr) ptrs[np++] = dsts[k];
-    }
-    constexpr int V = 16 / sizeof(T);
-    const long head = vector_head<T>(ptrs, np, n);
-    if (head >= 0) {
-        if (head > 0) {
-            p.head = (uint32_t)head;
-            for (int k = 0; k < NSRC; ++k) {
-                p.src[k] = (const char *)srcs[k] + head * sizeof(T);
-                if (dsts[k] != nullptr) p.dst[k] = (char *)dsts[k] + head * sizeof(T);
-            }
-            n -= (size_t)head;
-        }
-        using S = OrdersShape<NSRC, T>;
-        p.nvec = n / V;
-        p.tail = (uint32_t)(n % V);
-        const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, S::blocks_per_cu);
-        return launch(combine_orders_vec<OP, T, NSRC, S::unroll, S::policy>, dim3(grid), st, p);
-    }
-    p.nvec = n;
-    p.tail = 0;
-    const unsigned grid = grid_for((uint64_t)kBlock * 4, n);
-    return launch(combine_orders_scalar<OP, T, NSRC>, dim3(grid), st, p);
-}
-
-template <int OP, typename T>
-int launch_n(int nsrc, void *dst, const void *const *srcs, size_t n, hipStream_t st, bool final) {
-    switch (nsrc) {
-    case 1: return launch_fixed<OP, T, 1>(dst, srcs, n, st, final);
-    case 2: return launch_fixed<OP, T, 2>(dst, srcs, n, st, final);
-    case 3: return launch_fixed<OP, T, 3>(dst, srcs, n, st, final);
-    case 4: return launch_fixed<OP, T, 4>(dst, srcs, n, st, final);
-    case 5: return launch_fixed<OP, T, 5>(dst, srcs, n, st, final);
-    case 6: return launch_fixed<OP, T, 6>(dst, srcs, n, st, final);
-    case 7: return launch_fixed<OP, T, 7>(dst, srcs, n, st, final);
-    case 8: return launch_fixed<OP, T, 8>(dst, srcs, n, st, final);
-    default: return MI355_E_INVAL;
-    }
-}
-
-// Left fold of any number of sources: first kMaxSrc into dst, then dst
-// stays the accumulator (first operand) of every following launch. `final`:
-// the last launch carries the armed completion signal.
-template <int OP, typename T>
-int launch_fold(void *dst, const void *const *srcs, int nsrc, size_t n, hipStream_t st, bool final = true) {
-    if constexpr (!valid_pair<OP, T>()) {
-        return MI355_E_UNSUP;
-    } else {
-        int first = nsrc < kMaxSrc ? nsrc : kMaxSrc;
-        int rc = launch_n<OP, T>(first, dst, srcs, n, st, final && first == nsrc);
-        int done = first;
-        while (rc == 0 && done < nsrc) {
-            const void *chunk[kMaxSrc];
-            chunk[0] = dst;
-            int take = nsrc - done < kMaxSrc - 1 ? nsrc - done : kMaxSrc - 1;
-            for (int k = 0; k < take; ++k) chunk[1 + k] = srcs[done + k];
-            done += take;
-            rc = launch_n<OP, T>(1 + take, dst, chunk, n, st, final && done == nsrc);
-        }
-        return rc;
-    }
-}
-
-template <typename T>
-int dispatch_op(int op, void *dst, const void *const *srcs, int nsrc, size_t n, hipStream_t st) {
-    switch (op) {
-    case MI355_OP_SUM: return launch_fold<MI355_OP_SUM, T>(dst, srcs, nsrc, n, st);
-    case MI355_OP_PROD: return launch_fold<MI355_OP_PROD, T>(dst, srcs, nsrc, n, st);
-    case MI355_OP_AND: return launch_fold<MI355_OP_AND, T>(dst, srcs, nsrc, n, st);
-    case MI355_OP_OR: return launch_fold<MI355_OP_OR, T>(dst, srcs, nsrc, n, st);
-    case MI355_OP_XOR: return launch_fold<MI355_OP_XOR, T>(dst, srcs, nsrc, n, st);
-    case MI355_OP_MIN: return launch_fold<MI355_OP_MIN, T>(dst, srcs, nsrc, n, st);
-    case MI355_OP_MAX: return launch_fold<MI355_OP_MAX, T>(dst, srcs, nsrc, n, st);
-    default: return MI355_E_INVAL;
-    }
-}
-
-// Every member's order (mi355_combine_orders): one launch up to kMaxSrc
-// sources. Beyond that, each member's fold is its own multi-launch left fold
-// in that member's order; a fold whose target is its own source (in place)
-// runs last, since the other folds still read that source.
-template <int OP, typename T>
-int launch_orders(void *const *dsts, const void *const *srcs, int nsrc, size_t n, hipStream_t st) {
-    if constexpr (!valid_pair<OP, T>()) {
-        return MI355_E_UNSUP;
-    } else {
-        switch (nsrc) {
-        case 2: return launch_orders_fixed<OP, T, 2>(dsts, srcs, n, st);
-        case 3: return launch_orders_fixed<OP, T, 3>(dsts, srcs, n, st);
-        case 4: return launch_orders_fixed<OP, T, 4>(dsts, srcs, n, st);
-        case 5: return launch_orders_fixed<OP, T, 5>(dsts, srcs, n, st);
-        case 6: return launch_orders_fixed<OP, T, 6>(dsts, srcs, n, st);
-        case 7: return launch_orders_fixed<OP, T, 7>(dsts, srcs, n, st);
-        case 8: return launch_orders_fixed<OP, T, 8>(dsts, srcs, n, st);
-        default: break;
-        }
-        int alias = -1, last = -1;
-        for (int q = 0; q < nsrc; ++q) {
-            if (dsts[q] == nullptr) continue;
-            if (dsts[q] == srcs[q]) alias = q;
-            else last = q;
-        }
-        const int final_q = alias >= 0 ? alias : last;
-        const void *order[MI355_ORDERS_MAX_SOURCES];
-        int rc = 0;
-        for (int j = 0; j <= nsrc && rc == 0; ++j) {
-            const int q = j < nsrc ? j : alias;  // the in-place fold, if any, after all others
-            if (q < 0 || dsts[q] == nullptr || (j < nsrc && q == alias)) continue;
-            order[0] = srcs[q];
-            int m = 1;
-            for (int k = 0; k < nsrc; ++k)
-                if (k != q) order[m++] = srcs[k];
-            rc = launch_fold<OP, T>(dsts[q], order, nsrc, n, st, q == final_q);
-        }
-        return rc;
-    }
-}
-
-template <typename T>
-int dispatch_orders(int op, void *const *dsts, const void *const *srcs, int nsrc, size_t n, hipStream_t st) {
-    switch (op) {
-    case MI355_OP_SUM: return launch_orders<MI355_OP_SUM, T>(dsts, srcs, nsrc, n, st);
-    case MI355_OP_PROD: return launch_orders<MI355_OP_PROD, T>(dsts, srcs, nsrc, n, st);
-    case MI355_OP_AND: return launch_orders<MI355_OP_AND, T>(dsts, srcs, nsrc, n, st);
-    case MI355_OP_OR: return launch_orders<MI355_OP_OR, T>(dsts, srcs, nsrc, n, st);
-    case MI355_OP_XOR: return launch_orders<MI355_OP_XOR, T>(dsts, srcs, nsrc, n, st);
-    case MI355_OP_MIN: return launch_orders<MI355_OP_MIN, T>(dsts, srcs, nsrc, n, st);
-    case MI355_OP_MAX: return launch_orders<MI355_OP_MAX, T>(dsts, srcs, nsrc, n, st);
-    default: return MI355_E_INVAL;
-    }
-}
-
-}  // namespace
+using namespace mi355k;
 
 extern "C" size_t mi355_dtype_size(int dtype) {
     switch (dtype) {
@@ -747,15 +224,15 @@ static int combine_impl(int op, int dtype, void *dst, const void *const *srcs, i
         return mi355_copy_segments(d, srcs, nb, 1, stream);
     }
     switch (dtype) {
-    case MI355_SHORT: return dispatch_op<int16_t>(op, dst, srcs, nsrc, n, st);
-    case MI355_INT: return dispatch_op<int32_t>(op, dst, srcs, nsrc, n, st);
+    case MI355_SHORT: return combine_short(op, dst, srcs, nsrc, n, st);
+    case MI355_INT: return combine_int(op, dst, srcs, nsrc, n, st);
     case MI355_LONG:
-    case MI355_LONGLONG: return dispatch_op<int64_t>(op, dst, srcs, nsrc, n, st);
-    case MI355_FLOAT: return dispatch_op<float>(op, dst, srcs, nsrc, n, st);
-    case MI355_DOUBLE: return dispatch_op<double>(op, dst, srcs, nsrc, n, st);
-    case MI355_LONGDOUBLE: return dispatch_op<x80>(op, dst, srcs, nsrc, n, st);
-    case MI355_COMPLEXF: return dispatch_op<cplxf>(op, dst, srcs, nsrc, n, st);
-    case MI355_COMPLEXD: return dispatch_op<cplxd>(op, dst, srcs, nsrc, n, st);
+    case MI355_LONGLONG: return combine_long(op, dst, srcs, nsrc, n, st);
+    case MI355_FLOAT: return combine_float(op, dst, srcs, nsrc, n, st);
+    case MI355_DOUBLE: return combine_double(op, dst, srcs, nsrc, n, st);
+    case MI355_LONGDOUBLE: return combine_longdouble(op, dst, srcs, nsrc, n, st);
+    case MI355_COMPLEXF: return combine_complexf(op, dst, srcs, nsrc, n, st);
+    case MI355_COMPLEXD: return combine_complexd(op, dst, srcs, nsrc, n, st);
     default: return MI355_E_INVAL;
     }
 }
@@ -781,15 +258,15 @@ static int combine_orders_impl(int op, int dtype, void *const *dsts, const void 
     }
     if (nsrc == 1) return combine_impl(op, dtype, dsts[0], srcs, 1, n, stream);
     switch (dtype) {
-    case MI355_SHORT: return dispatch_orders<int16_t>(op, dsts, srcs, nsrc, n, st);
-    case MI355_INT: return dispatch_orders<int32_t>(op, dsts, srcs, nsrc, n, st);
+    case MI355_SHORT: return orders_short(op, dsts, srcs, nsrc, n, st);
+    case MI355_INT: return orders_int(op, dsts, srcs, nsrc, n, st);
     case MI355_LONG:
-    case MI355_LONGLONG: return dispatch_orders<int64_t>(op, dsts, srcs, nsrc, n, st);
-    case MI355_FLOAT: return dispatch_orders<float>(op, dsts, srcs, nsrc, n, st);
-    case MI355_DOUBLE: return dispatch_orders<double>(op, dsts, srcs, nsrc, n, st);
-    case MI355_LONGDOUBLE: return dispatch_orders<x80>(op, dsts, srcs, nsrc, n, st);
-    case MI355_COMPLEXF: return dispatch_orders<cplxf>(op, dsts, srcs, nsrc, n, st);
-    case MI355_COMPLEXD: return dispatch_orders<cplxd>(op, dsts, srcs, nsrc, n, st);
+    case MI355_LONGLONG: return orders_long(op, dsts, srcs, nsrc, n, st);
+    case MI355_FLOAT: return orders_float(op, dsts, srcs, nsrc, n, st);
+    case MI355_DOUBLE: return orders_double(op, dsts, srcs, nsrc, n, st);
+    case MI355_LONGDOUBLE: return orders_longdouble(op, dsts, srcs, nsrc, n, st);
+    case MI355_COMPLEXF: return orders_complexf(op, dsts, srcs, nsrc, n, st);
+    case MI355_COMPLEXD: return orders_complexd(op, dsts, srcs, nsrc, n, st);
     default: return MI355_E_INVAL;
     }
 }
