@@ -185,6 +185,47 @@ def run_config(shm, c, me, results):
     shm.free_device(src)
 
 
+def big_source(c, pe):
+    """Inputs of a "big" case, cheap to generate at GiB sizes: config 1's
+    int pattern for integers; for floats random values with NaN / +0 / -0
+    planted on some PEs (the selects of min/max then depend on the order)."""
+    n, dtype = c["n"], c["dtype"]
+    if dtype in ("short", "int", "long", "longlong"):
+        i = np.arange(n, dtype=np.int64)
+        return (i * 7 + pe * 1000003).astype(shmem_reduce.NP[dtype])
+    x = np.random.default_rng(c["seed"] + pe).random(n, dtype=np.float32).astype(shmem_reduce.NP[dtype]) - 0.5
+    x[pe::97 + pe] = np.nan if pe % 2 == 0 else 0.0
+    x[3::89] = -0.0 if pe % 2 else 0.0
+    return x
+
+
+def run_big(shm, c, me, results):
+    """kind "big": one reduction of c["n"] elements (GiB-scale, up to nreduce =
+    INT_MAX) on device-heap buffers allocated for it; checked here, on every
+    PE: the whole target at one PE (the identity), else a million sampled
+    elements against the oracle's result for this PE."""
+    import oracle
+    op, dtype, n = c["op"], c["dtype"], c["n"]
+    es = np.dtype(shmem_reduce.NP[dtype]).itemsize
+    start, logstride, size = c["sets"][0]
+    src, dst = shm.malloc_device(n * es), shm.malloc_device(n * es)
+    x = big_source(c, me)
+    shm.put(src, x)
+    shm.to_all(op, dtype, dst, src, n, start, logstride, size)
+    got = shm.get(dst, n, dtype)
+    if size == 1:
+        bad = int((got.view(np.uint8) != x.view(np.uint8)).sum())
+    else:
+        idx = np.unique(np.random.default_rng(7).integers(0, n, 1 << 20))
+        idx = np.concatenate([idx, [0, n - 1]])
+        srcs = [big_source(c, p)[idx] for p in range(size)]
+        want = oracle.reduce_pe(op, dtype, srcs, me)
+        bad = int((got[idx].view(np.uint8) != want.view(np.uint8)).sum())
+    results[str(c["id"]) + "_bad"] = np.array([bad])
+    shm.free_device(dst)
+    shm.free_device(src)
+
+
 FORTRAN_KIND = {"short": "int2", "int": "int4", "long": "int8", "float": "real4", "double": "real8",
                 "longdouble": "real16", "complexf": "comp4", "complexd": "comp8"}
 
@@ -209,7 +250,7 @@ def main():
     shm = shmem_reduce.Shmem()
     shm.init()
     me = shm.my_pe()
-    maxb = max(max(c["n"] + 16, c.get("cap", 0)) * 16 if c.get("kind") != "config" else 4096
+    maxb = max(max(c["n"] + 16, c.get("cap", 0)) * 16 if c.get("kind") not in ("config", "big") else 4096
                for c in spec["cases"])
     da, db = shm.malloc_device(maxb), shm.malloc_device(maxb)
     ha, hb = shm.malloc(maxb), shm.malloc(maxb)
@@ -222,6 +263,9 @@ def main():
     for c in spec["cases"]:
         if c.get("kind") == "config":
             run_config(shm, c, me, results)
+            continue
+        if c.get("kind") == "big":
+            run_big(shm, c, me, results)
             continue
         if c.get("kind") == "stream":
             run_stream(shm, c, me, da, db, results)

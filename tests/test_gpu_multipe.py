@@ -259,6 +259,26 @@ def test_reduction_while_another_kernel_holds_every_cu(tmp_path):
         assert 0.2 < t < 10.0, f"case {c['id']}: {t:.3f} s from the busy launch to the call's return"
 
 
+def test_largest_messages(tmp_path):
+    """nreduce up to INT_MAX (the `int nreduce` of shmem.h:1507-1743): 2^31-1
+    shorts (4 GiB) on one PE, the identity checked whole; and 2^29 floats
+    (2 GiB per PE) on 2 PEs through max_to_all, whose every-member order needs
+    several rounds of the default 256 MiB version area, NaN and +-0 planted,
+    checked on a million samples per PE against the oracle's result for that
+    PE. (The reference's own byte count `int snred = sizeof(Type)*nreduce`,
+    reduce-op.c:190, overflows above 2 GiB; this build counts in size_t.)"""
+    one = [{"id": 0, "kind": "big", "op": "sum", "dtype": "short", "n": (1 << 31) - 1, "sets": [[0, 0, 1]],
+            "seed": 3}]
+    res = run_pes(1, one, tmp_path, extra_env={"SHMEM_DEVICE_HEAP_SIZE": "8400M"}, timeout=900)
+    assert int(res[0]["0_bad"][0]) == 0
+    two = [{"id": 1, "kind": "big", "op": "max", "dtype": "float", "n": 1 << 29, "sets": [[0, 0, 2]], "seed": 5},
+           {"id": 2, "kind": "big", "op": "sum", "dtype": "int", "n": (1 << 29) + 3, "sets": [[0, 0, 2]], "seed": 6}]
+    res = run_pes(2, two, tmp_path, extra_env={"SHMEM_DEVICE_HEAP_SIZE": "4200M"}, timeout=900)
+    for pe in range(2):
+        for c in two:
+            assert int(res[pe][f"{c['id']}_bad"][0]) == 0, (pe, c["id"])
+
+
 def test_eight_pes_one_gpu(tmp_path):
     cases = make_cases([("sum", "double"), ("and", "longlong"), ("max", "float")], 20000, [[0, 0, 8]],
                        "dev", "p2p", 0)
