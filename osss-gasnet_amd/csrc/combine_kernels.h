@@ -206,7 +206,13 @@ __device__ __forceinline__ void orders_element(const OrdersParams &p, int64_t i)
     }
 }
 
-template <int OP, typename T, int NSRC, int UNROLL, int POL>
+// ALL: every dst[q] is set (the P2P schedule's case). Without the per-output
+// null tests the compiler keeps the next pass's loads ahead of this pass's
+// stores; with them it placed `s_waitcnt vmcnt` on the previous pass's stores
+// before the loads (the stores' data registers are reused as load addresses
+// across the branches), which halved the kernel's rate at 2-4 sources
+// (tools/orders_probe.hip; rocprofv3 160 vs 82 us at 4 x 64 MiB).
+template <int OP, typename T, int NSRC, int UNROLL, int POL, bool ALL>
 __global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
     constexpr int V = 16 / sizeof(T);
     const uint64_t nvec = p.nvec;
@@ -228,7 +234,7 @@ __global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
             if (i >= nvec) continue;
 #pragma unroll
             for (int q = 0; q < NSRC; ++q) {
-                if (p.dst[q] == nullptr) continue;
+                if (!ALL && p.dst[q] == nullptr) continue;
                 Pack<T> acc = x[u][q];
 #pragma unroll
                 for (int k = 0; k < NSRC; ++k) {
@@ -427,7 +433,10 @@ int launch_orders_fixed(void *const *dsts, const void *const *srcs, size_t n, hi
         p.nvec = n / V;
         p.tail = (uint32_t)(n % V);
         const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, S::blocks_per_cu);
-        return launch(combine_orders_vec<OP, T, NSRC, S::unroll, S::policy>, dim3(grid), st, p);
+        bool all = true;
+        for (int k = 0; k < NSRC; ++k) all = all && dsts[k] != nullptr;
+        if (all) return launch(combine_orders_vec<OP, T, NSRC, S::unroll, S::policy, true>, dim3(grid), st, p);
+        return launch(combine_orders_vec<OP, T, NSRC, S::unroll, S::policy, false>, dim3(grid), st, p);
     }
     p.nvec = n;
     p.tail = 0;
