@@ -76,6 +76,46 @@ __global__ __launch_bounds__(256) void fold_gs(Srcs in, u32x4 *d, size_t nvec) {
     }
 }
 
+// as fold_gs, but full passes (all U vectors in range) run without per-vector
+// range tests; only the last, partial pass is guarded
+template <int K, int U, int ST, int NT>
+__global__ __launch_bounds__(256) void fold_nog(Srcs in, u32x4 *d, size_t nvec) {
+    const size_t step = (size_t)gridDim.x * 256 * U;
+    size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+    for (; base + (size_t)(U - 1) * 256 < nvec; base += step) {
+        P2 x[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) x[u][k].v = load<NT>(in.s[k] + base + (size_t)u * 256);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            P2 a = x[u][0];
+#pragma unroll
+            for (int k = 1; k < K; ++k) {
+                a.e[0] = a.e[0] + x[u][k].e[0];
+                a.e[1] = a.e[1] + x[u][k].e[1];
+            }
+            store<ST>(d + base + (size_t)u * 256, a.v);
+        }
+    }
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * 256;
+        if (i < nvec) {
+            P2 a;
+            a.v = load<NT>(in.s[0] + i);
+            for (int k = 1; k < K; ++k) {
+                P2 b;
+                b.v = load<NT>(in.s[k] + i);
+                a.e[0] = a.e[0] + b.e[0];
+                a.e[1] = a.e[1] + b.e[1];
+            }
+            store<ST>(d + i, a.v);
+        }
+    }
+}
+
 // as fold_gs, but the loads issued source-major: src0's U vectors, then src1's, ...
 template <int K, int U, int ST, int NT>
 __global__ __launch_bounds__(256) void fold_sm(Srcs in, u32x4 *d, size_t nvec) {
@@ -230,6 +270,26 @@ int main(int argc, char **argv) {
                                                         s_, d, nvec); }));                          \
     } while (0)
 
+    if (argc > 1 && argv[1][0] == 'g') {  // unguarded full passes
+        for (int r = 0; r < 2; ++r) {
+            RUN(fold_gs, 8, 4, ST_SC1, 1, 8, srcs_sep(), "library shape");
+            RUN(fold_nog, 8, 4, ST_SC1, 1, 8, srcs_sep(), "unguarded full passes");
+            RUN(fold_nog, 8, 4, ST_SC1, 1, 4, srcs_sep(), "unguarded full passes");
+            RUN(fold_nog, 8, 2, ST_SC1, 1, 8, srcs_sep(), "unguarded full passes");
+            RUN(fold_gs, 3, 2, ST_SC1, 1, 1, srcs_sep(), "library shape");
+            RUN(fold_nog, 3, 2, ST_SC1, 1, 1, srcs_sep(), "unguarded full passes");
+            RUN(fold_nog, 3, 2, ST_SC1, 1, 2, srcs_sep(), "unguarded full passes");
+            RUN(fold_gs, 2, 1, ST_SC1, 1, 2, srcs_sep(), "library shape");
+            RUN(fold_nog, 2, 2, ST_SC1, 1, 2, srcs_sep(), "unguarded full passes");
+            RUN(fold_nog, 2, 4, ST_SC1, 1, 1, srcs_sep(), "unguarded full passes");
+            RUN(fold_nog, 2, 4, ST_SC1, 1, 2, srcs_sep(), "unguarded full passes");
+            RUN(fold_gs, 1, 4, ST_NT_SC1, 0, 1, srcs_sep(), "copy, library-like");
+            RUN(fold_nog, 1, 4, ST_NT_SC1, 0, 1, srcs_sep(), "copy, unguarded");
+            RUN(fold_nog, 1, 4, ST_SC1, 1, 1, srcs_sep(), "copy, unguarded");
+            RUN(fold_nog, 1, 8, ST_SC1, 1, 1, srcs_sep(), "copy, unguarded");
+        }
+        return 0;
+    }
     if (argc > 1 && argv[1][0] == 'o') {  // load order / lane layout at k = 8 and k = 2
         for (int r = 0; r < 2; ++r) {
             RUN(fold_gs, 8, 4, ST_SC1, 1, 8, srcs_sep(), "library shape");
