@@ -76,8 +76,8 @@ def cpu_baseline(S, n_gpus, budget_s):
     oracle/reduce_oracle.c: copy loop, barrier, 64-element pWrk chunks folded
     with one indirect operator call per element, barrier) on this box's host
     cores, in this run, before the GPU is touched: N = max(2, n_gpus) forked
-    PE processes, PE p pinned to the p-th CPU of this process's affinity mask,
-    shared-memory transport. Bounded sample: as many calls as fit in about
+    PE processes, each pinned to a CPU of its own (the third allowed CPU on:
+    CPU 0 takes most interrupts), shared-memory transport. Bounded sample: as many calls as fit in about
     budget_s. Also the 1-PE call (the N = 1 headline's workload) and BASELINE
     config 1 (int sum, 2 PEs, 4 KiB)."""
     import oracle

@@ -244,8 +244,9 @@ static int nth_allowed_cpu (int k)
 }
 
 /* op/t: OP_SUM with T_INT (config 1) or T_DOUBLE (configs 2, 3, 5). pin: PE p
- * runs pinned to the p-th CPU of the caller's affinity mask; cpus_out (npes
- * entries, or NULL) receives the CPU each PE ran on. */
+ * runs pinned to the (p+2)-th CPU of the caller's affinity mask (the p-th when
+ * fewer than npes + 2 are allowed); cpus_out (npes entries, or NULL) receives
+ * the CPU each PE ran on. */
 double oracle_cpu_baseline (int op, int t, int npes, size_t n, int warm, int reps, int pin, int *cpus_out)
 {
     if (npes < 1 || npes > 1024 || reps < 1 || reps > 1000000 || (t != T_INT && t != T_DOUBLE))
@@ -281,7 +282,11 @@ double oracle_cpu_baseline (int op, int t, int npes, size_t n, int warm, int rep
     }
     sh->cpu[me] = -1;
     if (pin) {
-        const int c = nth_allowed_cpu (me);
+        /* skip the first two allowed CPUs when there are spare ones: CPU 0
+         * takes most of the host's interrupts */
+        cpu_set_t set;
+        const int skip = sched_getaffinity (0, sizeof set, &set) == 0 && CPU_COUNT (&set) >= npes + 2 ? 2 : 0;
+        const int c = nth_allowed_cpu (me + skip);
         if (c >= 0) {
             cpu_set_t one;
             CPU_ZERO (&one);
