@@ -7,6 +7,8 @@
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
+#include <stdint.h>
 
 #include <algorithm>
 #include <vector>
@@ -24,7 +26,7 @@ struct Srcs {
     const u32x4 *s[8];
 };
 
-enum { ST_NT_SC1 = 0, ST_NT = 1, ST_PLAIN = 2, ST_NONE = 3, ST_SC1 = 4 };
+enum { ST_NT_SC1 = 0, ST_NT = 1, ST_PLAIN = 2, ST_NONE = 3, ST_SC1 = 4, ST_BSC1 = 5 };
 
 template <int ST>
 __device__ __forceinline__ void store(u32x4 *p, u32x4 v) {
@@ -204,6 +206,271 @@ __global__ __launch_bounds__(256) void fold_part(Srcs in, u32x4 *d, size_t nvec)
     }
 }
 
+// software-pipelined: the next pass's K*U loads are issued BEFORE this pass's
+// stores, so the wait for them (vmcnt counts loads and stores in issue order
+// on gfx9) does not include the store acknowledgements
+template <int K, int U, int ST, int NT>
+__global__ __launch_bounds__(256) void fold_pipe(Srcs in, u32x4 *d, size_t nvec) {
+    const size_t step = (size_t)gridDim.x * 256 * U;
+    size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x;
+    if (base >= nvec) return;
+    P2 x[U][K];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        size_t i = base + (size_t)u * 256;
+        if (i < nvec) {
+#pragma unroll
+            for (int k = 0; k < K; ++k) x[u][k].v = load<NT>(in.s[k] + i);
+        }
+    }
+    for (;;) {
+        const size_t next = base + step;
+        P2 y[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            size_t i = next + (size_t)u * 256;
+            if (i < nvec) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) y[u][k].v = load<NT>(in.s[k] + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            size_t i = base + (size_t)u * 256;
+            if (i < nvec) {
+                P2 a = x[u][0];
+#pragma unroll
+                for (int k = 1; k < K; ++k) {
+                    a.e[0] = a.e[0] + x[u][k].e[0];
+                    a.e[1] = a.e[1] + x[u][k].e[1];
+                }
+                store<ST>(d + i, a.v);
+            }
+        }
+        if (next >= nvec) break;
+        base = next;
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < K; ++k) x[u][k] = y[u][k];
+    }
+}
+
+// fold_pipe with block-uniform full passes: every load of a full pass is
+// unconditional (no per-lane guards), the prefetch of pass i+1 is issued
+// before the stores of pass i, and the last (partial) pass is guarded
+template <int K, int U, int ST, int NT>
+__device__ __forceinline__ void fold_store(const P2 (&x)[U][K], u32x4 *d, size_t base) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        P2 a = x[u][0];
+#pragma unroll
+        for (int k = 1; k < K; ++k) {
+            a.e[0] = a.e[0] + x[u][k].e[0];
+            a.e[1] = a.e[1] + x[u][k].e[1];
+        }
+        store<ST>(d + base + (size_t)u * 256, a.v);
+    }
+}
+template <int K, int U, int ST, int NT>
+__global__ __launch_bounds__(256) void fold_pipe2(Srcs in, u32x4 *d, size_t nvec) {
+    const size_t step = (size_t)gridDim.x * 256 * U;
+    size_t bb = (size_t)blockIdx.x * 256 * U;  // block-uniform
+    const size_t t = threadIdx.x;
+    if (bb + 256 * U <= nvec) {
+        P2 x[U][K];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < K; ++k) x[u][k].v = load<NT>(in.s[k] + bb + t + (size_t)u * 256);
+        while (bb + step + 256 * U <= nvec) {
+            P2 y[U][K];
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int k = 0; k < K; ++k) y[u][k].v = load<NT>(in.s[k] + bb + step + t + (size_t)u * 256);
+            fold_store<K, U, ST, NT>(x, d, bb + t);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int k = 0; k < K; ++k) x[u][k] = y[u][k];
+            bb += step;
+        }
+        fold_store<K, U, ST, NT>(x, d, bb + t);
+        bb += step;
+    }
+    // the partial pass (at most one per block)
+    for (int u = 0; u < U; ++u) {
+        const size_t i = bb + t + (size_t)u * 256;
+        if (i < nvec) {
+            P2 a;
+            a.v = load<NT>(in.s[0] + i);
+            for (int k = 1; k < K; ++k) {
+                P2 b;
+                b.v = load<NT>(in.s[k] + i);
+                a.e[0] = a.e[0] + b.e[0];
+                a.e[1] = a.e[1] + b.e[1];
+            }
+            store<ST>(d + i, a.v);
+        }
+    }
+}
+
+// ping-pong registers (no copies): prefetch pass i+1 into one set, then fold
+// and store pass i from the other; the scheduling barrier keeps the prefetch
+// ahead of the fold's waits. Every path into the loop header ends "loads of
+// the held pass, then the previous pass's stores", so the compiler's vmcnt
+// wait for the held pass leaves the stores (and the new prefetch) in flight.
+template <int K, int U, int NT>
+__device__ __forceinline__ void load_pass(P2 (&x)[U][K], const Srcs &in, size_t base) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < K; ++k) x[u][k].v = load<NT>(in.s[k] + base + (size_t)u * 256);
+    __builtin_amdgcn_sched_barrier(0);
+}
+template <int K, int U, int ST, int NT>
+__global__ __launch_bounds__(256) void fold_pp(Srcs in, u32x4 *d, size_t nvec) {
+    const size_t step = (size_t)gridDim.x * 256 * U;
+    size_t bb = (size_t)blockIdx.x * 256 * U;
+    const size_t t = threadIdx.x;
+    auto full = [&](size_t b) { return b + 256 * U <= nvec; };
+    if (full(bb)) {
+        P2 x[U][K], y[U][K];
+        load_pass<K, U, NT>(x, in, bb + t);
+        if (full(bb + step)) {
+            load_pass<K, U, NT>(y, in, bb + step + t);
+            fold_store<K, U, ST, NT>(x, d, bb + t);
+            bb += step;  // y holds bb
+            for (;;) {
+                if (!full(bb + step)) {
+                    fold_store<K, U, ST, NT>(y, d, bb + t);
+                    bb += step;
+                    break;
+                }
+                load_pass<K, U, NT>(x, in, bb + step + t);
+                fold_store<K, U, ST, NT>(y, d, bb + t);
+                bb += step;  // x holds bb
+                if (!full(bb + step)) {
+                    fold_store<K, U, ST, NT>(x, d, bb + t);
+                    bb += step;
+                    break;
+                }
+                load_pass<K, U, NT>(y, in, bb + step + t);
+                fold_store<K, U, ST, NT>(x, d, bb + t);
+                bb += step;  // y holds bb
+            }
+        } else {
+            fold_store<K, U, ST, NT>(x, d, bb + t);
+            bb += step;
+        }
+    }
+    for (int u = 0; u < U; ++u) {
+        const size_t i = bb + t + (size_t)u * 256;
+        if (i < nvec) {
+            P2 a;
+            a.v = load<NT>(in.s[0] + i);
+            for (int k = 1; k < K; ++k) {
+                P2 b;
+                b.v = load<NT>(in.s[k] + i);
+                a.e[0] = a.e[0] + b.e[0];
+                a.e[1] = a.e[1] + b.e[1];
+            }
+            store<ST>(d + i, a.v);
+        }
+    }
+}
+
+// delayed stores: pass i's results stay in registers and are stored after
+// pass i+1's loads are issued, so the wait for pass i+1's loads leaves them
+// in flight (vmcnt retires loads and stores in issue order on gfx9: in
+// fold_gs the wait for pass i+1 also waits for pass i's store
+// acknowledgements). Full passes are block-uniform and unguarded.
+template <int K, int U>
+__device__ __forceinline__ void fold_regs(const P2 (&x)[U][K], P2 (&r)[U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        P2 a = x[u][0];
+#pragma unroll
+        for (int k = 1; k < K; ++k) {
+            a.e[0] = a.e[0] + x[u][k].e[0];
+            a.e[1] = a.e[1] + x[u][k].e[1];
+        }
+        r[u] = a;
+    }
+}
+// two result sets used alternately (the loop unrolled by two): overwriting a
+// result register that a store has not yet read would make the compiler wait
+// for that store (vmcnt(0) per pass)
+template <int K, int U, int ST, int NT>
+__device__ __forceinline__ void ds_load(P2 (&x)[U][K], const Srcs &in, size_t base) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < K; ++k) x[u][k].v = load<NT>(in.s[k] + base + (size_t)u * 256);
+    __builtin_amdgcn_sched_barrier(0);
+}
+// ST_BSC1: `buffer_store_dwordx4 ... sc1` through the builtin (the compiler
+// counts it in vmcnt; an inline-asm store it cannot see, so its waits for
+// loads issued before such stores are vmcnt(0))
+template <int U, int ST>
+__device__ __forceinline__ void ds_store(const P2 (&r)[U], u32x4 *d, size_t base) {
+    if constexpr (ST == ST_BSC1) {
+        const size_t t = threadIdx.x;
+        const size_t bbase = __builtin_amdgcn_readfirstlane((unsigned)((base - t) >> 8)) * (size_t)256;  // uniform
+        __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(d + bbase, 0, (int)0xFFFFFFF0u, 0x00020000);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            __builtin_amdgcn_raw_buffer_store_b128(r[u].v, rs, (unsigned)((t + (size_t)u * 256) * 16), 0, 16);
+        __builtin_amdgcn_sched_barrier(0);
+    } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) store<ST>(d + base + (size_t)u * 256, r[u].v);
+    }
+}
+template <int K, int U, int ST, int NT>
+__global__ __launch_bounds__(256) void fold_ds(Srcs in, u32x4 *d, size_t nvec) {
+    const size_t step = (size_t)gridDim.x * 256 * U;
+    size_t bb = (size_t)blockIdx.x * 256 * U;
+    const size_t t = threadIdx.x;
+    auto full = [&](size_t b) { return b + 256 * U <= nvec; };
+    if (full(bb)) {
+        P2 x[U][K], r0[U], r1[U];
+        ds_load<K, U, ST, NT>(x, in, bb + t);
+        fold_regs<K, U>(x, r0);
+        size_t rb = bb + t;
+        bb += step;
+        for (;;) {
+            if (!full(bb)) { ds_store<U, ST>(r0, d, rb); break; }
+            ds_load<K, U, ST, NT>(x, in, bb + t);
+            ds_store<U, ST>(r0, d, rb);
+            fold_regs<K, U>(x, r1);
+            rb = bb + t;
+            bb += step;
+            if (!full(bb)) { ds_store<U, ST>(r1, d, rb); break; }
+            ds_load<K, U, ST, NT>(x, in, bb + t);
+            ds_store<U, ST>(r1, d, rb);
+            fold_regs<K, U>(x, r0);
+            rb = bb + t;
+            bb += step;
+        }
+    }
+    for (int u = 0; u < U; ++u) {
+        const size_t i = bb + t + (size_t)u * 256;
+        if (i < nvec) {
+            P2 a;
+            a.v = load<NT>(in.s[0] + i);
+            for (int k = 1; k < K; ++k) {
+                P2 b;
+                b.v = load<NT>(in.s[k] + i);
+                a.e[0] = a.e[0] + b.e[0];
+                a.e[1] = a.e[1] + b.e[1];
+            }
+            store<ST == ST_BSC1 ? ST_SC1 : ST>(d + i, a.v);
+        }
+    }
+}
+
 template <typename F>
 double time_us(F launch) {
     hipEvent_t a, b;
@@ -270,6 +537,59 @@ int main(int argc, char **argv) {
                                                         s_, d, nvec); }));                          \
     } while (0)
 
+    if (argc > 1 && argv[1][0] == 'p') {  // software-pipelined loads vs the library shape
+        // correctness of the hand-scheduled kernel first: against fold_gs on distinct per-source data
+        {
+            Srcs s_ = srcs_sep();
+            std::vector<double> h(nvec * 2);
+            for (int k = 0; k < 8; ++k) {
+                uint64_t z = 0x9E3779B97F4A7C15ull * (k + 1);
+                for (auto &v : h) { z ^= z << 13; z ^= z >> 7; z ^= z << 17; v = (double)(int64_t)z * 0x1p-63; }
+                CHECK(hipMemcpy(sep[k], h.data(), bytes, hipMemcpyHostToDevice));
+            }
+            u32x4 *d2;
+            CHECK(hipMalloc(&d2, bytes));
+            hipLaunchKernelGGL((fold_gs<8, 4, ST_SC1, 1>), dim3(cus * 8), dim3(256), 0, 0, s_, d, nvec);
+            for (int bpc : {1, 2, 4, 8}) {
+                CHECK(hipMemset(d2, 0xff, bytes));
+                hipLaunchKernelGGL((fold_ds<8, 4, ST_BSC1, 1>), dim3(cus * bpc), dim3(256), 0, 0, s_, d2, nvec - 77);
+                CHECK(hipDeviceSynchronize());
+                std::vector<double> a(nvec * 2), b(nvec * 2);
+                CHECK(hipMemcpy(a.data(), d, bytes, hipMemcpyDeviceToHost));
+                CHECK(hipMemcpy(b.data(), d2, bytes, hipMemcpyDeviceToHost));
+                size_t bad = 0;
+                for (size_t i = 0; i < (nvec - 77) * 2; ++i) bad += memcmp(&a[i], &b[i], 8) != 0;
+                printf("fold_ds<U4> %d/CU vs fold_gs: %zu mismatches of %zu\n", bpc, bad, (nvec - 77) * 2);
+            }
+            CHECK(hipFree(d2));
+        }
+        for (int r = 0; r < 3; ++r) {
+            RUN(fold_gs, 8, 4, ST_SC1, 1, 8, srcs_sep(), "library shape");
+            RUN(fold_ds, 8, 4, ST_SC1, 1, 8, srcs_sep(), "delayed stores (asm)");
+            RUN(fold_ds, 8, 4, ST_BSC1, 1, 8, srcs_sep(), "delayed stores");
+            RUN(fold_ds, 8, 4, ST_BSC1, 1, 4, srcs_sep(), "delayed stores");
+            RUN(fold_ds, 8, 2, ST_BSC1, 1, 8, srcs_sep(), "delayed stores");
+            RUN(fold_ds, 8, 2, ST_BSC1, 1, 4, srcs_sep(), "delayed stores");
+            RUN(fold_ds, 8, 1, ST_BSC1, 1, 8, srcs_sep(), "delayed stores");
+            RUN(fold_gs, 4, 1, ST_SC1, 1, 1, srcs_sep(), "library shape");
+            RUN(fold_ds, 4, 1, ST_BSC1, 1, 1, srcs_sep(), "delayed stores");
+            RUN(fold_ds, 4, 1, ST_BSC1, 1, 2, srcs_sep(), "delayed stores");
+            RUN(fold_ds, 4, 2, ST_BSC1, 1, 2, srcs_sep(), "delayed stores");
+            RUN(fold_gs, 2, 1, ST_SC1, 1, 2, srcs_sep(), "library shape");
+            RUN(fold_ds, 2, 1, ST_BSC1, 1, 2, srcs_sep(), "delayed stores");
+            RUN(fold_ds, 2, 2, ST_BSC1, 1, 2, srcs_sep(), "delayed stores");
+            RUN(fold_ds, 2, 4, ST_BSC1, 1, 1, srcs_sep(), "delayed stores");
+            RUN(fold_ds, 2, 1, ST_BSC1, 1, 4, srcs_sep(), "delayed stores");
+            RUN(fold_gs, 1, 4, ST_NT_SC1, 0, 1, srcs_sep(), "copy, library-like");
+            RUN(fold_ds, 1, 4, ST_BSC1, 0, 1, srcs_sep(), "copy, delayed stores");
+            RUN(fold_ds, 1, 8, ST_BSC1, 0, 1, srcs_sep(), "copy, delayed stores");
+            RUN(fold_ds, 1, 4, ST_BSC1, 0, 2, srcs_sep(), "copy, delayed stores");
+            RUN(fold_pp, 8, 2, ST_SC1, 1, 8, srcs_sep(), "compiler-scheduled ping-pong");
+            RUN(fold_pp, 8, 2, ST_SC1, 1, 4, srcs_sep(), "compiler-scheduled ping-pong");
+            RUN(fold_gs, 8, 4, ST_NONE, 1, 8, srcs_sep(), "no store: read ceiling");
+        }
+        return 0;
+    }
     if (argc > 1 && argv[1][0] == 'g') {  // unguarded full passes
         for (int r = 0; r < 2; ++r) {
             RUN(fold_gs, 8, 4, ST_SC1, 1, 8, srcs_sep(), "library shape");
