@@ -77,9 +77,11 @@ def cpu_baseline(S, n_gpus, budget_s):
     with one indirect operator call per element, barrier) on this box's host
     cores, in this run, before the GPU is touched: N = max(2, n_gpus) forked
     PE processes, each pinned to a CPU of its own (the third allowed CPU on:
-    CPU 0 takes most interrupts), shared-memory transport. Bounded sample: as many calls as fit in about
-    budget_s. Also the 1-PE call (the N = 1 headline's workload) and BASELINE
-    config 1 (int sum, 2 PEs, 4 KiB)."""
+    CPU 0 takes most interrupts), shared-memory transport. Bounded sample: as
+    many calls as fit in about budget_s. Sub-records: the 1-PE call (the N = 1
+    headline's workload), 8 PEs (SURVEY 8d's N in {2, 8}; BASELINE config 3's
+    shape), BASELINE config 1 (int sum, 2 PEs, 4 KiB) and config 5's call
+    (64 KiB double sum at 8 PEs)."""
     import oracle
     npes = max(2, n_gpus)
     n = S // 8
@@ -90,9 +92,11 @@ def cpu_baseline(S, n_gpus, budget_s):
         t, cpus = oracle.cpu_baseline(op, dtype, pes, nel, 1, reps)
         return t, reps, cpus
 
-    t, reps, cpus = timed("sum", "double", npes, n, 0.6 * budget_s)
-    t1, reps1, cpus1 = timed("sum", "double", 1, n, 0.3 * budget_s)
-    tc, repsc, cpusc = timed("sum", "int", 2, 1024, 0.1 * budget_s)
+    t, reps, cpus = timed("sum", "double", npes, n, 0.4 * budget_s)
+    t1, reps1, cpus1 = timed("sum", "double", 1, n, 0.2 * budget_s)
+    t8, reps8, cpus8 = timed("sum", "double", 8, n, 0.25 * budget_s)
+    tc, repsc, cpusc = timed("sum", "int", 2, 1024, 0.05 * budget_s)
+    t5, reps5, cpus5 = timed("sum", "double", 8, 8192, 0.1 * budget_s)
     try:
         allowed = len(os.sched_getaffinity(0))
     except AttributeError:
@@ -105,10 +109,15 @@ def cpu_baseline(S, n_gpus, budget_s):
             "ms_per_call": round(t * 1e3, 3), "per_pe_gib_s": round(S / t / GIB, 4),
             "one_pe": {"value": round(S / t1 / GIB, 4), "cores": 1, "calls": reps1, "ms_per_call": round(t1 * 1e3, 3),
                        "cpus": cpus1, "note": f"1 PE x {mib} MiB: the N = 1 headline's workload"},
+            "eight_pe": {"value": round(8 * S / t8 / GIB, 4), "cores": 8, "calls": reps8,
+                         "ms_per_call": round(t8 * 1e3, 3), "per_pe_gib_s": round(S / t8 / GIB, 4), "cpus": cpus8,
+                         "note": f"8 PEs x {mib} MiB (BASELINE config 3's shape on host cores), whole-job GiB/s"},
             "config1": {"workload": "shmem_int_sum_to_all, 2 PEs, 4 KiB (BASELINE config 1; shared-memory "
                                     "transport in place of GASNet udp/mpi loopback)",
                         "us_per_call": round(tc * 1e6, 3), "per_pe_gib_s": round(4096 / tc / GIB, 4), "calls": repsc,
                         "cores": 2, "cpus": cpusc},
+            "config5": {"workload": "shmem_double_sum_to_all, 8 PEs, 64 KiB per call (BASELINE config 5's call)",
+                        "us_per_call": round(t5 * 1e6, 3), "calls": reps5, "cores": 8, "cpus": cpus5},
             "host": {"nproc": os.cpu_count(), "allowed_cpus": allowed, "cpu_model": cpu_model()}}
 
 

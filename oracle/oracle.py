@@ -110,8 +110,9 @@ def cpu_baseline_double_sum(npes, n, warm=1, reps=3):
 
 def cpu_baseline(op, dtype, npes, n, warm=1, reps=3, pin=True):
     """The reference algorithm (reduce-op.c:226-266, restated in C) as npes
-    forked host processes, PE p pinned to the p-th CPU of this process's
-    affinity mask: (median seconds per call, max over PEs; CPUs used).
+    forked host processes, each pinned to a CPU of its own from this process's
+    affinity mask (skipping its first two CPUs when there are spare ones):
+    (median seconds per call, max over PEs; CPUs used).
     op/dtype: sum on int (config 1) or double."""
     cpus = (ctypes.c_int * npes)()
     t = _load().oracle_cpu_baseline(OPS.index(op), DTYPES.index(dtype), npes, n, warm, reps, 1 if pin else 0, cpus)

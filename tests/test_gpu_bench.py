@@ -48,6 +48,7 @@ def test_bench_one_gpu_line():
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] == 2 and cb["value"] > 0
     assert cb["one_pe"]["cores"] == 1 and cb["config1"]["us_per_call"] > 0 and cb["host"]["nproc"] >= 1
+    assert cb["eight_pe"]["cores"] == 8 and cb["eight_pe"]["value"] > 0 and cb["config5"]["us_per_call"] > 0
     assert d["config"]["bytes_per_pe"] == 256 << 20
     k = d["kernels"]
     for name in ("fold_k2_double_sum", "fold_k8_double_sum", "rs_shard_n8_double_sum", "fold_k8_float_max",
