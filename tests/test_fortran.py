@@ -77,3 +77,34 @@ def test_fortran_entry_one_pe(shm, op, kind):
     assert (psync == -1).all()
     shm.free_device(dt)
     shm.free_device(ds)
+
+
+def test_fortran_include_constants_match_c_header(tmp_path):
+    """include/shmem.fh declares the collectives' work-array sizes in default
+    INTEGERs: twice the C header's `long` counts (reference src/shmem.fh:71-95
+    against src/shmem.h's values), the same SHMEM_SYNC_VALUE; and every
+    statement is valid fixed-form (column 7 on, no continuation)."""
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    fh = open(os.path.join(root, "include", "shmem.fh")).read().splitlines()
+    vals = {}
+    for line in fh:
+        if line.startswith("!") or not line.strip():
+            continue
+        assert line.startswith("      ") and not line[5].strip() and len(line) <= 72, line
+        m = re.match(r"\s+parameter \((\w+) = (-?\d+)\)$", line)
+        if m:
+            vals[m.group(1)] = int(m.group(2))
+    names = ["SHMEM_BCAST_SYNC_SIZE", "SHMEM_BARRIER_SYNC_SIZE", "SHMEM_REDUCE_SYNC_SIZE",
+             "SHMEM_REDUCE_MIN_WRKDATA_SIZE", "SHMEM_COLLECT_SYNC_SIZE", "SHMEM_SYNC_VALUE"]
+    src = tmp_path / "c.c"
+    src.write_text('#include <stdio.h>\n#include "shmem.h"\nint main(void){printf("%ld %ld %ld %ld %ld %ld\\n",'
+                   + ",".join(f"(long){n}" for n in names) + ");return 0;}\n")
+    exe = tmp_path / "c"
+    subprocess.check_call(["gcc", "-I", os.path.join(root, "include"), str(src), "-o", str(exe)])
+    cvals = [int(x) for x in subprocess.check_output([str(exe)], text=True).split()]
+    scale = ctypes.sizeof(ctypes.c_long) // ctypes.sizeof(ctypes.c_int)
+    for name, c in zip(names, cvals):
+        want = c if name == "SHMEM_SYNC_VALUE" else c * scale
+        assert vals[name] == want, (name, vals[name], c)
+    assert vals["SHMEM_REDUCE_SYNC_SIZE"] == 256 and vals["SHMEM_REDUCE_MIN_WRKDATA_SIZE"] == 128
