@@ -132,7 +132,8 @@ int mi355_convert_short (int widen, const void *src, void *dst, size_t n, void *
 #define MI355_SIG_AG_COUNT 4112
 #define MI355_SIG_ERROR 4128
 #define MI355_SIG_STAGE_COUNT 4144
-#define MI355_SIG_CHANNEL_WORDS 4160
+#define MI355_SIG_SERVER 4160    /* persistent server's call broadcast (own line, 8 words) */
+#define MI355_SIG_CHANNEL_WORDS 4176
 #define MI355_SIG_CHANNELS 2
 #define MI355_SIG_SELFTEST (MI355_SIG_CHANNELS * MI355_SIG_CHANNEL_WORDS) /* [PE]: init-time check */
 #define MI355_SIG_WORDS (MI355_SIG_SELFTEST + 1024)
@@ -200,6 +201,46 @@ typedef struct MI355PullArgs {
     unsigned long long nbytes[MI355_PULL_MAX_SEGS];
 } MI355PullArgs;
 int mi355_fused_pull (const MI355PullArgs *args, void *stream);
+
+/* ---- persistent fused server (opt-in; reduce.c, SHMEM_PERSISTENT) ----
+ * A grid of the fused kernel that stays resident and serves back-to-back
+ * calls of one (op, dtype, active set) from a mailbox in host-coherent
+ * memory instead of one launch per call: the host writes the call and
+ * advances `seq`; block 0 of the server polls it, broadcasts the call to the
+ * other blocks through this PE's signal region (MI355_SIG_SERVER) and every
+ * block runs the fused kernel's body on the members' heap bases (args->src /
+ * args->dst at offset 0) plus the call's byte offsets. The call completes
+ * as a launched one does (args->host_flag = the call's epoch).
+ * The server exits on cmd QUIT, or when no call came for idle_ticks (100 MHz
+ * ticks): it then stores state = EXITED, state_seq = the first seq it did not
+ * serve, and never serves again -- a host that rang that seq falls back to a
+ * launch. Host-staged calls (host_src/host_dst) are not served. */
+#define MI355_SERVER_RUN 1
+#define MI355_SERVER_QUIT 2
+#define MI355_SERVER_RUNNING 1
+#define MI355_SERVER_EXITED 2
+typedef struct MI355ServerMailbox {
+    /* host -> device (one 64-byte line): the call, then seq (release) */
+    unsigned long long src_off, dst_off; /* byte offsets into every member's symmetric heap */
+    unsigned long long n, shard;         /* as MI355FusedArgs */
+    unsigned epoch;
+    int oneshot;
+    unsigned cmd;                        /* MI355_SERVER_RUN / _QUIT */
+    unsigned seq;                        /* the server serves seq first_seq, first_seq + 1, ... */
+    unsigned pad0[4];
+    /* device -> host (own line) */
+    unsigned state;                      /* MI355_SERVER_RUNNING (set by the host before the launch) / _EXITED */
+    unsigned state_seq;                  /* EXITED: the first seq not served */
+    unsigned pad1[14];
+} MI355ServerMailbox;
+
+/* Launch the server on `stream` (a stream of its own: it does not finish
+ * until QUIT or idle). args: as for mi355_fused_allreduce with src/dst the
+ * members' heap bases, n/shard/oneshot/epoch unused; grid_elems sizes the
+ * grid (the calls it is expected to serve). mbox: device-accessible
+ * host-coherent memory. */
+int mi355_fused_server (const MI355FusedArgs *args, MI355ServerMailbox *mbox, unsigned first_seq,
+                        unsigned long long idle_ticks, unsigned long long grid_elems, void *stream);
 
 /* Device-side barrier over the members (one 64-lane block): ordered on
  * `stream` after the work queued before it, and the work queued after it

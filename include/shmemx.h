@@ -67,6 +67,21 @@ enum shmemx_reduce_order {
 int shmemx_set_reduce_order (int order); /* returns the previous one */
 int shmemx_get_reduce_order (void);
 
+/* Persistent fused server (opt-in; env SHMEM_PERSISTENT=1 sets it at init,
+ * SHMEM_PERSISTENT_IDLE_US = how long it stays without a call, default 1000):
+ * back-to-back blocking reductions of one (type, op, active set) that take
+ * the one-launch fused schedule (up to SHMEM_FUSED_MAX_BYTES, device-resident
+ * symmetric buffers) are served by a fused kernel left resident between
+ * calls, fed through a host-coherent mailbox: no launch per call. Results are
+ * those of the launched kernel. Caveats, hence opt-in: a call does not order
+ * after GPU work the caller queued (complete its writes to the source first),
+ * and while the server is resident it holds its blocks, so a caller's
+ * hipDeviceSynchronize waits until it idles out (shmemx_device_synchronize
+ * and every other GPU operation of this library stop it first). */
+int shmemx_set_persistent (int enable); /* returns the previous setting */
+/* calls served by a resident server, servers launched (since init) */
+void shmemx_persistent_stats (long *served, long *launched);
+
 /* Device and timing helpers (used by bench.py and the tests). */
 int shmemx_device_id (void);                 /* HIP ordinal of this PE's GPU */
 /* Link from this PE's GPU to PE pe's: type (hsa_amd_link_info_type_t: 4 =

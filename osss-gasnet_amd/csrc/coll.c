@@ -81,6 +81,8 @@ static void pull (void **dsts, const void **srcs, size_t *nbytes, int nseg);
 static void put_bytes (const char *fn, void *dest, const void *src, size_t nbytes, int pe)
 {
     shmemi_init_check (fn);
+    if (shmemi.heap != NULL)
+        shmemi_server_stop ();
     check_pe (fn, pe);
     if (shmemi.heap == NULL)
         shmemi_fatal ("%s: no GPU (SHMEM_BOOTSTRAP_ONLY)", fn);
@@ -110,6 +112,8 @@ static void put_bytes (const char *fn, void *dest, const void *src, size_t nbyte
 static void get_bytes (const char *fn, void *dest, const void *src, size_t nbytes, int pe)
 {
     shmemi_init_check (fn);
+    if (shmemi.heap != NULL)
+        shmemi_server_stop ();
     check_pe (fn, pe);
     if (shmemi.heap == NULL)
         shmemi_fatal ("%s: no GPU (SHMEM_BOOTSTRAP_ONLY)", fn);
@@ -195,6 +199,8 @@ struct cset {
 static struct cset make_set (const char *fn, int PE_start, int logPE_stride, int PE_size)
 {
     shmemi_init_check (fn);
+    if (shmemi.heap != NULL)
+        shmemi_server_stop ();
     if (shmemi.heap == NULL)
         shmemi_fatal ("%s: no GPU (SHMEM_BOOTSTRAP_ONLY)", fn);
     if (logPE_stride < 0 || logPE_stride > 30 || PE_size < 1 || PE_start < 0 ||

@@ -120,7 +120,8 @@ __device__ void publish(const MI355FusedArgs &a, const unsigned long long *cnt, 
 }
 
 // Advance the pair counts (the call is over on every member), then report.
-__device__ void finish(const MI355FusedArgs &a, unsigned long long *mine, const unsigned long long *cnt, bool ok) {
+__device__ void finish(const MI355FusedArgs &a, unsigned long long *mine, const unsigned long long *cnt, bool ok,
+                       unsigned epoch) {
     if (ok && threadIdx.x < a.nmembers) st_sys_u64(mine + MI355_SIG_CALLS + a.pe[threadIdx.x], cnt[threadIdx.x]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -130,7 +131,7 @@ __device__ void finish(const MI355FusedArgs &a, unsigned long long *mine, const 
             if (a.err_flag) __hip_atomic_store(a.err_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         }
         if (a.host_flag)
-            __hip_atomic_store(a.host_flag, ok ? a.epoch : (a.epoch | 0x80000000u), __ATOMIC_RELAXED,
+            __hip_atomic_store(a.host_flag, ok ? epoch : (epoch | 0x80000000u), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
@@ -165,6 +166,23 @@ __device__ void block_copy(void *dst, const void *src, uint64_t nbytes, unsigned
     block_drain(block_copy_issue(dst, src, nbytes, bi, nblocks));
 }
 
+// One call's parameters. The launched kernel's come from its arguments (the
+// members' buffers in a.src/a.dst, offsets 0); a persistent server's
+// (fused_server) from its mailbox, as symmetric-heap byte offsets added to
+// the members' heap bases in a.src/a.dst.
+struct Call {
+    uint64_t soff, doff;  // byte offsets added to a.src[i] / a.dst[i]
+    uint64_t n, shard;    // as MI355FusedArgs
+    unsigned epoch;
+    int oneshot;
+};
+__device__ __forceinline__ const char *src_of(const MI355FusedArgs &a, const Call &c, int i) {
+    return (const char *)a.src[i] + c.soff;
+}
+__device__ __forceinline__ char *dst_of(const MI355FusedArgs &a, const Call &c, int i) {
+    return (char *)a.dst[i] + c.doff;
+}
+
 // Member at position j of the fold order that starts with member `first`
 // and continues with the others in member order (first = 0: member order;
 // first = q: member q's reference order, reduce-op.c:226-264).
@@ -176,7 +194,7 @@ __device__ __forceinline__ int order_member(int j, int first) {
 // the order starting with `first`. kBatch members' vectors are loaded before
 // any is folded, so their (xGMI) latencies overlap instead of adding up.
 template <int OP, typename T>
-__device__ __forceinline__ Pack<T> fold_vec(const MI355FusedArgs &a, uint64_t lo, uint64_t v, int first) {
+__device__ __forceinline__ Pack<T> fold_vec(const MI355FusedArgs &a, const Call &c, uint64_t lo, uint64_t v, int first) {
     constexpr int V = 16 / sizeof(T);
     const int nm = a.nmembers;
     Pack<T> acc;
@@ -185,7 +203,7 @@ __device__ __forceinline__ Pack<T> fold_vec(const MI355FusedArgs &a, uint64_t lo
 #pragma unroll
         for (int j = 0; j < kBatch; ++j)
             if (k0 + j < nm)
-                x[j].v = ((const u32x4 *)((const char *)a.src[order_member(k0 + j, first)] + lo * sizeof(T)))[v];
+                x[j].v = ((const u32x4 *)(src_of(a, c, order_member(k0 + j, first)) + lo * sizeof(T)))[v];
 #pragma unroll
         for (int j = 0; j < kBatch; ++j) {
             if (k0 + j >= nm) break;
@@ -201,14 +219,14 @@ __device__ __forceinline__ Pack<T> fold_vec(const MI355FusedArgs &a, uint64_t lo
 }
 
 template <int OP, typename T>
-__device__ __forceinline__ T fold_elem(const MI355FusedArgs &a, uint64_t i, int first) {
+__device__ __forceinline__ T fold_elem(const MI355FusedArgs &a, const Call &c, uint64_t i, int first) {
     const int nm = a.nmembers;
     T acc;
     for (int k0 = 0; k0 < nm; k0 += kBatch) {
         T x[kBatch];
 #pragma unroll
         for (int j = 0; j < kBatch; ++j)
-            if (k0 + j < nm) x[j] = ((const T *)a.src[order_member(k0 + j, first)])[i];
+            if (k0 + j < nm) x[j] = ((const T *)src_of(a, c, order_member(k0 + j, first)))[i];
 #pragma unroll
         for (int j = 0; j < kBatch; ++j) {
             if (k0 + j >= nm) break;
@@ -221,9 +239,9 @@ __device__ __forceinline__ T fold_elem(const MI355FusedArgs &a, uint64_t i, int 
 // Where member q's version of element r of this PE's shard goes: its target
 // shard for q == me, else slot (q < me ? q : q - 1) of this PE's version area.
 template <typename T>
-__device__ __forceinline__ T *version_elem(const MI355FusedArgs &a, int q, uint64_t r) {
-    if (q == a.me) return (T *)a.dst[a.me] + (uint64_t)a.me * a.shard + r;
-    return (T *)((char *)a.ver[a.me] + (uint64_t)(q < a.me ? q : q - 1) * a.shard * sizeof(T)) + r;
+__device__ __forceinline__ T *version_elem(const MI355FusedArgs &a, const Call &c, int q, uint64_t r) {
+    if (q == a.me) return (T *)dst_of(a, c, a.me) + (uint64_t)a.me * c.shard + r;
+    return (T *)((char *)a.ver[a.me] + (uint64_t)(q < a.me ? q : q - 1) * c.shard * sizeof(T)) + r;
 }
 
 // Vector v of shard `me` in EVERY member's reference order. Up to kBatch
@@ -231,7 +249,7 @@ __device__ __forceinline__ T *version_elem(const MI355FusedArgs &a, int q, uint6
 // beyond that (and for the software x87 type, whose fold is long code) one
 // fold per member re-reads the vectors (cache hits after the first).
 template <int OP, typename T>
-__device__ __forceinline__ void versions_vec(const MI355FusedArgs &a, uint64_t lo, uint64_t v) {
+__device__ __forceinline__ void versions_vec(const MI355FusedArgs &a, const Call &c, uint64_t lo, uint64_t v) {
     constexpr int V = 16 / sizeof(T);
     const int nm = a.nmembers;
     if constexpr (!std::is_same<T, x80>::value) {
@@ -239,7 +257,7 @@ __device__ __forceinline__ void versions_vec(const MI355FusedArgs &a, uint64_t l
             Pack<T> x[kBatch];
 #pragma unroll
             for (int j = 0; j < kBatch; ++j)
-                if (j < nm) x[j].v = ((const u32x4 *)((const char *)a.src[j] + lo * sizeof(T)))[v];
+                if (j < nm) x[j].v = ((const u32x4 *)(src_of(a, c, j) + lo * sizeof(T)))[v];
 #pragma unroll
             for (int q = 0; q < kBatch; ++q) {
                 if (q >= nm) break;
@@ -251,7 +269,7 @@ __device__ __forceinline__ void versions_vec(const MI355FusedArgs &a, uint64_t l
 #pragma unroll
                     for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[k].e[e]);
                 }
-                st16_sys((u32x4 *)version_elem<T>(a, q, v * V), acc.v);
+                st16_sys((u32x4 *)version_elem<T>(a, c, q, v * V), acc.v);
             }
             return;
         }
@@ -260,12 +278,14 @@ __device__ __forceinline__ void versions_vec(const MI355FusedArgs &a, uint64_t l
     // source vector the other folds still read
     for (int j = 0; j < nm; ++j) {
         const int q = j < a.me ? j : j + 1 < nm ? j + 1 : a.me;
-        st16_sys((u32x4 *)version_elem<T>(a, q, v * V), fold_vec<OP, T>(a, lo, v, q).v);
+        st16_sys((u32x4 *)version_elem<T>(a, c, q, v * V), fold_vec<OP, T>(a, c, lo, v, q).v);
     }
 }
 
+// The whole call, on every block of the grid (the launched kernel's and the
+// server's).
 template <int OP, typename T>
-__global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
+__device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &c) {
     constexpr int V = 16 / sizeof(T);
     unsigned long long *mine = a.sig[a.me];
     __shared__ int ok_all;
@@ -282,7 +302,7 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
         // that read src[me] below wait for it like for the peers.
         if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         __syncthreads();
-        block_copy((void *)a.src[a.me], a.host_src, a.n * sizeof(T), blockIdx.x, gridDim.x);
+        block_copy((void *)src_of(a, c, a.me), a.host_src, c.n * sizeof(T), blockIdx.x, gridDim.x);
         if (last_block(mine + MI355_SIG_STAGE_COUNT)) {
             if (threadIdx.x < a.nmembers)
                 st_sys_u64(a.sig[threadIdx.x] + MI355_SIG_ARRIVE + a.pe[a.me], cnt[threadIdx.x]);
@@ -303,29 +323,29 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
         // otherwise shard `me` (the reduce-scatter leg). Ordered one-shot
         // folds in this PE's own reference order; ordered two-shot computes
         // every member's order of shard `me` (versions_vec).
-        const bool oneshot = a.oneshot != 0;
+        const bool oneshot = c.oneshot != 0;
         const bool versions = a.ordered != 0 && !oneshot;
         const int first = a.ordered != 0 && oneshot ? a.me : 0;
         bool tail_plain = false;
-        const uint64_t lo = oneshot ? 0 : (uint64_t)a.me * a.shard;
-        const uint64_t hi = oneshot ? a.n : (lo + a.shard < a.n ? lo + a.shard : a.n);
+        const uint64_t lo = oneshot ? 0 : (uint64_t)a.me * c.shard;
+        const uint64_t hi = oneshot ? c.n : (lo + c.shard < c.n ? lo + c.shard : c.n);
         if (hi > lo) {
             const uint64_t nv = (hi - lo) / V;
-            u32x4 *d = (u32x4 *)((char *)a.dst[a.me] + lo * sizeof(T));
+            u32x4 *d = (u32x4 *)(dst_of(a, c, a.me) + lo * sizeof(T));
             for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < nv;
                  v += (uint64_t)gridDim.x * kBlock) {
-                if (versions) versions_vec<OP, T>(a, lo, v);
-                else st16_sys(d + v, fold_vec<OP, T>(a, lo, v, first).v);
+                if (versions) versions_vec<OP, T>(a, c, lo, v);
+                else st16_sys(d + v, fold_vec<OP, T>(a, c, lo, v, first).v);
             }
             const uint64_t tail0 = lo + nv * V;
             if (tail0 < hi && blockIdx.x == 0 && threadIdx.x < hi - tail0) {
                 const uint64_t i = tail0 + threadIdx.x;
                 if (!versions) {
-                    ((T *)a.dst[a.me])[i] = fold_elem<OP, T>(a, i, first);
+                    ((T *)dst_of(a, c, a.me))[i] = fold_elem<OP, T>(a, c, i, first);
                 } else {
                     for (int j = 0; j < a.nmembers; ++j) {  // own version last (in place, as versions_vec)
                         const int q = j < a.me ? j : j + 1 < a.nmembers ? j + 1 : a.me;
-                        *version_elem<T>(a, q, i - lo) = fold_elem<OP, T>(a, i, q);
+                        *version_elem<T>(a, c, q, i - lo) = fold_elem<OP, T>(a, c, i, q);
                     }
                 }
             }
@@ -346,23 +366,23 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
             // ---- gather the other shards: one grid-stride loop over all of
             // them, from their owners' targets, or (ordered) from the slot of
             // this PE's version in the owners' version areas
-            const uint64_t shard_v = a.shard / V;  // a.shard is a multiple of V
+            const uint64_t shard_v = c.shard / V;  // c.shard is a multiple of V
             const uint64_t total_v = shard_v * (uint64_t)a.nmembers;
             for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g < total_v;
                  g += (uint64_t)gridDim.x * kBlock) {
                 const int j = (int)(g / shard_v);
                 if (j == a.me) continue;
                 const uint64_t r0 = (g - (uint64_t)j * shard_v) * V;  // element within shard j
-                const uint64_t e0 = (uint64_t)j * a.shard + r0;
-                if (e0 >= a.n) continue;
+                const uint64_t e0 = (uint64_t)j * c.shard + r0;
+                if (e0 >= c.n) continue;
                 const T *from = versions ? (const T *)((const char *)a.ver[j] +
-                                                       (uint64_t)(a.me < j ? a.me : a.me - 1) * a.shard * sizeof(T)) - e0 + r0
-                                         : (const T *)a.dst[j];
-                if (e0 + V <= a.n) {
+                                                       (uint64_t)(a.me < j ? a.me : a.me - 1) * c.shard * sizeof(T)) - e0 + r0
+                                         : (const T *)dst_of(a, c, j);
+                if (e0 + V <= c.n) {
                     const u32x4 v = *(const u32x4 *)(from + e0);
-                    st16_sys((u32x4 *)((char *)a.dst[a.me] + e0 * sizeof(T)), v);
+                    st16_sys((u32x4 *)(dst_of(a, c, a.me) + e0 * sizeof(T)), v);
                 } else {
-                    for (uint64_t e = e0; e < a.n; ++e) ((T *)a.dst[a.me])[e] = from[e];
+                    for (uint64_t e = e0; e < c.n; ++e) ((T *)dst_of(a, c, a.me))[e] = from[e];
                     tail_plain = true;
                 }
             }
@@ -379,7 +399,7 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
                 __syncthreads();
                 if (!wait_members(a, mine, cnt, MI355_SIG_AGDONE, true)) ok_all = 0;
                 __syncthreads();
-                finish(a, mine, cnt, ok_all != 0);
+                finish(a, mine, cnt, ok_all != 0, c.epoch);
                 return;
             }
         }
@@ -401,18 +421,116 @@ __global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         }
         __syncthreads();
-        if (ok_all) block_copy(a.host_dst, a.dst[a.me], a.n * sizeof(T), blockIdx.x, gridDim.x);
+        if (ok_all) block_copy(a.host_dst, dst_of(a, c, a.me), c.n * sizeof(T), blockIdx.x, gridDim.x);
         if (last_block(mine + MI355_SIG_STAGE_COUNT)) {
             if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             __syncthreads();
             if (!wait_members(a, mine, cnt, MI355_SIG_AGDONE, true)) ok_all = 0;
             __syncthreads();
-            finish(a, mine, cnt, ok_all != 0);
+            finish(a, mine, cnt, ok_all != 0, c.epoch);
         }
         return;
     }
 fail:
-    finish(a, mine, cnt, false);
+    finish(a, mine, cnt, false, c.epoch);
+}
+
+template <int OP, typename T>
+__global__ __launch_bounds__(kBlock) void fused_allreduce(MI355FusedArgs a) {
+    fused_body<OP, T>(a, Call{0, 0, a.n, a.shard, a.epoch, a.oneshot});
+}
+
+// ---------------------------------------------------------------------------
+// persistent server (mi355_reduce.h, mi355_fused_server)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ unsigned ld_sys_u32(const unsigned *p) {
+    return __hip_atomic_load(const_cast<unsigned *>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys_u32(unsigned *p, unsigned v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Block 0's lane 0 takes the next call from the host mailbox (or QUIT: on the
+// host's command, or after idle_ticks without a call) and broadcasts it in the
+// signal region; every other block's lane 0 waits for the broadcast. Every
+// block then holds the call in f[] (LDS). A broadcast seq only advances after
+// the host saw the previous call complete, which needs every block, so no
+// block can miss one.
+__device__ void server_next(const MI355FusedArgs &a, MI355ServerMailbox *mb, unsigned seq,
+                            unsigned long long idle_ticks, unsigned long long *f) {
+    unsigned long long *slot = a.sig[a.me] + MI355_SIG_SERVER;
+    if (threadIdx.x == 0) {
+        if (blockIdx.x == 0) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            unsigned cmd = MI355_SERVER_QUIT;
+            bool idle = false;
+            while (true) {
+                if (ld_sys_u32(&mb->seq) == seq) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                    cmd = ld_sys_u32(&mb->cmd);
+                    break;
+                }
+                if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
+                    // final look: a call rung before this point is served;
+                    // after it, the host sees EXITED and launches instead
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+                    if (ld_sys_u32(&mb->seq) == seq) continue;
+                    idle = true;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            f[1] = cmd;
+            if (cmd == MI355_SERVER_RUN) {
+                f[2] = ld_sys_u64(&mb->src_off);
+                f[3] = ld_sys_u64(&mb->dst_off);
+                f[4] = ld_sys_u64(&mb->n);
+                f[5] = ld_sys_u64(&mb->shard);
+                f[6] = (unsigned long long)ld_sys_u32(&mb->epoch) |
+                       ((unsigned long long)(unsigned)ld_sys_u32((const unsigned *)&mb->oneshot) << 32);
+            }
+            for (int k = 1; k < 7; ++k) st_sys_u64(slot + k, f[k]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            st_sys_u64(slot, seq);
+            if (cmd != MI355_SERVER_RUN) {
+                // every other block has its QUIT once it reads the broadcast;
+                // tell the host which seq was not served
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                st_sys_u32(&mb->state_seq, idle ? seq : seq + 1);
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+                st_sys_u32(&mb->state, MI355_SERVER_EXITED);
+            }
+        } else {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            unsigned spins = 0;
+            f[1] = MI355_SERVER_QUIT;
+            while (true) {
+                if (ld_sys_u64(slot) == seq) {
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+                    for (int k = 1; k < 7; ++k) f[k] = ld_sys_u64(slot + k);
+                    break;
+                }
+                // block 0 broadcasts a call or QUIT within idle_ticks (plus a
+                // call's duration); this bound is only a safety net
+                if ((++spins & 63u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks + idle_ticks) break;
+                __builtin_amdgcn_s_sleep(2);
+            }
+        }
+    }
+    __syncthreads();
+}
+
+template <int OP, typename T>
+__global__ __launch_bounds__(kBlock) void fused_server(MI355FusedArgs a, MI355ServerMailbox *mb, unsigned first_seq,
+                                                       unsigned long long idle_ticks) {
+    __shared__ unsigned long long f[8];
+    for (unsigned seq = first_seq;; ++seq) {
+        server_next(a, mb, seq, idle_ticks, f);
+        if (f[1] != MI355_SERVER_RUN) return;
+        const Call c{f[2], f[3], f[4], f[5], (unsigned)f[6], (int)(f[6] >> 32)};
+        fused_body<OP, T>(a, c);
+        __syncthreads();  // f[] is rewritten by the next server_next
+    }
 }
 
 // One-launch pull collective: arrive, copy this member's segments (sources
@@ -431,7 +549,7 @@ __global__ __launch_bounds__(kBlock) void fused_pull(MI355PullArgs p) {
     if (!wait_members(a, mine, cnt, MI355_SIG_ARRIVE, false)) ok_all = 0;
     __syncthreads();
     if (!ok_all) {  // this block timed out: report it (the host aborts the job)
-        finish(a, mine, cnt, false);
+        finish(a, mine, cnt, false, a.epoch);
         return;
     }
     {
@@ -446,7 +564,7 @@ __global__ __launch_bounds__(kBlock) void fused_pull(MI355PullArgs p) {
         __syncthreads();
         if (!wait_members(a, mine, cnt, MI355_SIG_AGDONE, true)) ok_all = 0;
         __syncthreads();
-        finish(a, mine, cnt, ok_all != 0);
+        finish(a, mine, cnt, ok_all != 0, a.epoch);
     }
 }
 
@@ -461,7 +579,7 @@ __global__ __launch_bounds__(64) void device_barrier(MI355FusedArgs a) {
     if (threadIdx.x < a.nmembers && threadIdx.x != a.me)
         st_sys_u64(a.sig[threadIdx.x] + MI355_SIG_ARRIVE + a.pe[a.me], cnt[threadIdx.x]);
     const bool ok = wait_members(a, mine, cnt, MI355_SIG_ARRIVE, false);
-    finish(a, mine, cnt, ok);
+    finish(a, mine, cnt, ok, a.epoch);
 }
 
 extern "C" void mi355i_take_launch_events(void **start_event, void **stop_event);  // combine.hip
@@ -532,6 +650,34 @@ int launch_op(const MI355FusedArgs &a, unsigned grid, hipStream_t st) {
             break;                                                                     \
         } else {                                                                       \
             return MI355_E_UNSUP;                                                      \
+        }
+        CASE(MI355_OP_SUM)
+        CASE(MI355_OP_PROD)
+        CASE(MI355_OP_AND)
+        CASE(MI355_OP_OR)
+        CASE(MI355_OP_XOR)
+        CASE(MI355_OP_MIN)
+        CASE(MI355_OP_MAX)
+#undef CASE
+    default: return MI355_E_INVAL;
+    }
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+template <typename T>
+int launch_server(const MI355FusedArgs &a, MI355ServerMailbox *mb, unsigned first_seq, unsigned long long idle_ticks,
+                  unsigned grid, hipStream_t st) {
+    switch (a.op) {
+#define CASE(O)                                                                                          \
+    case O:                                                                                              \
+        if constexpr (valid_pair<O, T>()) {                                                             \
+            auto k = fused_server<O, T>;                                                                 \
+            hipLaunchKernelGGL(k, dim3(coresident_grid((const void *)k, grid, a.share)), dim3(kBlock), 0, st, a, mb, \
+                               first_seq, idle_ticks);                                                   \
+            break;                                                                                       \
+        } else {                                                                                         \
+            return MI355_E_UNSUP;                                                                        \
         }
         CASE(MI355_OP_SUM)
         CASE(MI355_OP_PROD)
@@ -656,4 +802,38 @@ extern "C" int mi355_device_barrier(const MI355FusedArgs *a, void *stream) {
     hipLaunchKernelGGL(device_barrier, dim3(1), dim3(64), 0, (hipStream_t)stream, *a);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
+}
+
+extern "C" int mi355_fused_server(const MI355FusedArgs *a, MI355ServerMailbox *mbox, unsigned first_seq,
+                                  unsigned long long idle_ticks, unsigned long long grid_elems, void *stream) {
+    if (a == nullptr || mbox == nullptr || !mi355_op_supported(a->op, a->dtype)) return MI355_E_UNSUP;
+    if (a->nmembers < 2 || a->nmembers > MI355_FUSED_MAX_MEMBERS || a->me < 0 || a->me >= a->nmembers)
+        return MI355_E_INVAL;
+    if (a->host_src != nullptr || a->host_dst != nullptr || a->host_flag == nullptr) return MI355_E_INVAL;
+    for (int i = 0; i < a->nmembers; ++i)
+        if (a->src[i] == nullptr || a->dst[i] == nullptr || a->sig[i] == nullptr ||
+            (((uintptr_t)a->src[i] | (uintptr_t)a->dst[i]) & 15) != 0 || a->pe[i] < 0 ||
+            a->pe[i] >= MI355_SIG_RSDONE)
+            return MI355_E_INVAL;
+    if (a->ordered)
+        for (int i = 0; i < a->nmembers; ++i)
+            if (a->ver[i] == nullptr || ((uintptr_t)a->ver[i] & 15) != 0) return MI355_E_INVAL;
+    // the grid a launched call of grid_elems elements would get (one-shot size)
+    const size_t es = mi355_dtype_size(a->dtype);
+    uint64_t grid = (grid_elems * es + 16 * kBlock - 1) / (16 * kBlock);
+    if (grid < 1) grid = 1;
+    if (grid > MI355_FUSED_MAX_BLOCKS) grid = MI355_FUSED_MAX_BLOCKS;
+    hipStream_t st = (hipStream_t)stream;
+    switch (a->dtype) {
+    case MI355_SHORT: return launch_server<int16_t>(*a, mbox, first_seq, idle_ticks, (unsigned)grid, st);
+    case MI355_INT: return launch_server<int32_t>(*a, mbox, first_seq, idle_ticks, (unsigned)grid, st);
+    case MI355_LONG:
+    case MI355_LONGLONG: return launch_server<int64_t>(*a, mbox, first_seq, idle_ticks, (unsigned)grid, st);
+    case MI355_FLOAT: return launch_server<float>(*a, mbox, first_seq, idle_ticks, (unsigned)grid, st);
+    case MI355_DOUBLE: return launch_server<double>(*a, mbox, first_seq, idle_ticks, (unsigned)grid, st);
+    case MI355_LONGDOUBLE: return launch_server<x80>(*a, mbox, first_seq, idle_ticks, (unsigned)grid, st);
+    case MI355_COMPLEXF: return launch_server<cplxf>(*a, mbox, first_seq, idle_ticks, (unsigned)grid, st);
+    case MI355_COMPLEXD: return launch_server<cplxd>(*a, mbox, first_seq, idle_ticks, (unsigned)grid, st);
+    default: return MI355_E_INVAL;
+    }
 }

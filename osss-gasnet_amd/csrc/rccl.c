@@ -113,6 +113,8 @@ int shmemi_rccl_comm (void **comm)
 int shmemx_rccl_init (double timeout_s)
 {
     shmemi_init_check ("shmemx_rccl_init");
+    if (shmemi.heap != NULL)
+        shmemi_server_stop ();
     if (shmemi.rccl_comm != NULL)
         return 0;
     char why[160] = "";
@@ -134,6 +136,7 @@ static int rccl_allreduce_short (int op, const void *src, void *dst, size_t n);
 
 int shmemi_rccl_allreduce (int op, int dtype, const void *src, void *dst, size_t n)
 {
+    shmemi_server_stop (); /* RCCL's kernels wait on the peers too */
     if (dtype == MI355_SHORT)
         return rccl_allreduce_short (op, src, dst, n);
     ncclDataType_t t;

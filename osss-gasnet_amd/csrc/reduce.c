@@ -201,6 +201,7 @@ static int device_flags_ok (const struct aset *s)
 
 static void device_barrier (const MI355FusedArgs *a, hipStream_t st)
 {
+    shmemi_server_stop (); /* two spin-waiting grids need not fit beside each other */
     const int rc = mi355_device_barrier (a, st);
     if (rc != 0)
         shmemi_fatal ("device barrier launch failed: %d", rc);
@@ -432,11 +433,160 @@ static void fused_order (MI355FusedArgs *a, const struct aset *s, int chan)
             a->ver[i] = shmemi_peer_ptr (aset_pe (s, i), shmemi.order_off + (size_t) chan * shmemi.order_chunk);
 }
 
+/* ---------------------------------------------------------------------- */
+/* persistent fused server (opt-in: SHMEM_PERSISTENT=1, shmemx_set_persistent) */
+/* ---------------------------------------------------------------------- */
+/* A blocking call pays a launch and its dispatch (~6 us, profiles/r02/
+ * kernarg_probe.txt) before the first block runs. When fused calls of one
+ * (op, dtype, active set) come back to back (the second within
+ * SHMEM_PERSISTENT_IDLE_US of the first), the fused kernel is left resident
+ * on a stream of its own (mi355_fused_server): a call then writes its
+ * offsets, sizes and epoch into the mailbox and waits for the epoch as
+ * usual. The server leaves after SHMEM_PERSISTENT_IDLE_US without a call, or
+ * when any other GPU operation of the library needs the device (device
+ * barriers, other fused or pull kernels, RCCL, stream-ordered calls,
+ * shmemx_device_synchronize, host heap changes, finalize). Not ordered after
+ * the caller's queued GPU work: the caller's writes to the source must be
+ * complete (synchronized) before the call -- hence opt-in. */
+static int server_matches (int op, int dtype, const struct aset *s)
+{
+    return shmemi.srv.running && shmemi.srv.op == op && shmemi.srv.dtype == dtype && shmemi.srv.start == s->start &&
+           shmemi.srv.stride == s->stride && shmemi.srv.size == s->size;
+}
+
+/* The server has left (EXITED): later servers start past its last seq. */
+static void server_gone (void)
+{
+    const unsigned after = shmemi.srv.mb->state_seq + 1;
+    if ((int) (after - shmemi.srv.seq) > 0)
+        shmemi.srv.seq = after;
+    shmemi.srv.running = 0;
+    SHMEMI_HIP (hipStreamSynchronize (shmemi.srv.st)); /* the grid has drained */
+}
+
+static void server_wait_exited (void)
+{
+    const double t0 = shmemi_now ();
+    unsigned spins = 0;
+    while (__atomic_load_n (&shmemi.srv.mb->state, __ATOMIC_ACQUIRE) != MI355_SERVER_EXITED) {
+        __builtin_ia32_pause ();
+        if ((++spins & 1023u) == 0) {
+            const hipError_t e = hipStreamQuery (shmemi.srv.st);
+            if (e != hipSuccess && e != hipErrorNotReady)
+                shmemi_fatal ("persistent fused server failed: %s", hipGetErrorString (e));
+            if (shmemi_now () - t0 > shmemi.barrier_timeout)
+                shmemi_fatal ("persistent fused server did not exit within %.0f s", shmemi.barrier_timeout);
+        }
+    }
+}
+
+void shmemi_server_stop (void)
+{
+    if (!shmemi.srv.running)
+        return;
+    MI355ServerMailbox *mb = shmemi.srv.mb;
+    if (__atomic_load_n (&mb->state, __ATOMIC_ACQUIRE) != MI355_SERVER_EXITED) {
+        mb->cmd = MI355_SERVER_QUIT;
+        __atomic_store_n (&mb->seq, shmemi.srv.seq++, __ATOMIC_RELEASE);
+        server_wait_exited ();
+    }
+    server_gone ();
+    SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "persistent fused server stopped");
+}
+
+/* Serve one call; 0 when the server had already left (the caller launches). */
+static int server_call (size_t dst_off, size_t src_off, size_t n, size_t shard, int oneshot)
+{
+    MI355ServerMailbox *mb = shmemi.srv.mb;
+    const unsigned epoch = shmemi_next_epoch ();
+    mb->src_off = src_off;
+    mb->dst_off = dst_off;
+    mb->n = n;
+    mb->shard = shard;
+    mb->epoch = epoch;
+    mb->oneshot = oneshot;
+    mb->cmd = MI355_SERVER_RUN;
+    __atomic_store_n (&mb->seq, shmemi.srv.seq++, __ATOMIC_RELEASE);
+    const double t0 = shmemi_now ();
+    unsigned spins = 0;
+    for (;;) {
+        const unsigned v = __atomic_load_n (shmemi.sig_flag, __ATOMIC_ACQUIRE);
+        if ((v & 0x7fffffffu) == epoch) {
+            if (v & 0x80000000u)
+                shmemi_fatal ("fused reduction timed out waiting for the other PEs of the active set");
+            ++shmemi.srv.served;
+            return 1;
+        }
+        if (__atomic_load_n (&mb->state, __ATOMIC_ACQUIRE) == MI355_SERVER_EXITED) {
+            /* it left without taking this call (idle): the flag cannot come */
+            if ((__atomic_load_n (shmemi.sig_flag, __ATOMIC_ACQUIRE) & 0x7fffffffu) == epoch)
+                continue;
+            server_gone ();
+            return 0;
+        }
+        __builtin_ia32_pause ();
+        if ((++spins & 1023u) == 0) {
+            const hipError_t e = hipStreamQuery (shmemi.srv.st);
+            if (e != hipSuccess && e != hipErrorNotReady)
+                shmemi_fatal ("persistent fused server failed: %s", hipGetErrorString (e));
+            if (shmemi_now () - t0 > shmemi.barrier_timeout)
+                shmemi_fatal ("persistent fused server: call not completed within %.0f s", shmemi.barrier_timeout);
+        }
+    }
+}
+
+static void server_start (int op, int dtype, size_t n, const struct aset *s)
+{
+    MI355FusedArgs a;
+    member_args (&a, s, SHMEMI_CHAN_HOST);
+    a.op = op;
+    a.dtype = dtype;
+    for (int i = 0; i < s->size; ++i) {
+        a.src[i] = shmemi_peer_ptr (a.pe[i], 0);
+        a.dst[i] = shmemi_peer_ptr (a.pe[i], 0);
+    }
+    a.host_flag = shmemi.sig_flag;
+    a.ordered = ordered_pair (op, dtype, s->size);
+    if (a.ordered)
+        for (int i = 0; i < s->size; ++i)
+            a.ver[i] = shmemi_peer_ptr (a.pe[i], shmemi.order_off + (size_t) SHMEMI_CHAN_HOST * shmemi.order_chunk);
+    MI355ServerMailbox *mb = shmemi.srv.mb;
+    mb->state = MI355_SERVER_RUNNING;
+    mb->state_seq = 0;
+    const int rc = mi355_fused_server (&a, mb, shmemi.srv.seq, (unsigned long long) (shmemi.srv.idle_s * 1e8), n,
+                                       shmemi.srv.st);
+    if (rc != 0) {
+        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "persistent fused server not started: %d", rc);
+        return;
+    }
+    shmemi.srv.running = 1;
+    shmemi.srv.op = op;
+    shmemi.srv.dtype = dtype;
+    shmemi.srv.start = s->start;
+    shmemi.srv.stride = s->stride;
+    shmemi.srv.size = s->size;
+    shmemi.srv.grid_elems = n;
+    ++shmemi.srv.launched;
+    SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "persistent fused server started (%d members, sized for %zu elements)",
+                  s->size, n);
+}
+
 /* host_src/host_dst: device-accessible page-locked host buffers of this PE
  * staged in-kernel into src_off / out of dst_off (mi355_reduce.h), or NULL. */
 static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
                          const struct aset *s, const void *host_src, void *host_dst)
 {
+    const int servable = shmemi.srv.enabled && host_src == NULL && host_dst == NULL;
+    const double t_call = servable ? shmemi_now () : 0.0;
+    if (servable && server_matches (op, dtype, s) && n <= 4 * shmemi.srv.grid_elems) {
+        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: persistent fused server (%zu elements, %d members)", n, s->size);
+        if (server_call (dst_off, src_off, n, shard_chunk (n, es, s->size),
+                         n * es <= shmemi.oneshot_max && dst_off != src_off)) {
+            shmemi.srv.last_end = shmemi_now ();
+            return;
+        }
+    }
+    shmemi_server_stop (); /* a different call: the launched grid must fit */
     SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: fused one-launch P2P, %s, %s (%zu elements, %d members)%s",
                   n * es <= shmemi.oneshot_max && dst_off != src_off ? "one-shot" : "reduce-scatter + all-gather",
                   ordered_pair (op, dtype, s->size) ? "every member's reference order" : "PE_start order", n,
@@ -473,6 +623,12 @@ static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t sr
                       s->size, n, rc);
     if (shmemi_wait_flag (a.epoch) != a.epoch)
         shmemi_fatal ("fused reduction timed out waiting for the other PEs of the active set");
+    if (servable) {
+        /* the second call of a burst leaves the kernel resident for the next */
+        if (shmemi.srv.last_end >= 0.0 && t_call - shmemi.srv.last_end < shmemi.srv.idle_s)
+            server_start (op, dtype, 2 * n, s); /* a grid for calls up to 8x this one */
+        shmemi.srv.last_end = shmemi_now ();
+    }
 }
 
 /* EXACT: fold everything in this PE's reference order into dst; dst must
@@ -769,6 +925,7 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
                          shmemi_rccl_supported (op, dtype);
     if (use_rccl && kt != PK_HOST && ks != PK_HOST && !overlap) {
         SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: RCCL allreduce");
+        shmemi_server_stop ();
         if (shmemi_rccl_allreduce (op, dtype, source, target, n) != 0)
             shmemi_fatal ("%s: ncclAllReduce failed", fn);
         return;
@@ -811,6 +968,7 @@ static void stream_begin (const char *fn)
     shmemi_init_check (fn);
     if (shmemi.heap == NULL)
         shmemi_fatal ("%s: no GPU (SHMEM_BOOTSTRAP_ONLY set?)", fn);
+    shmemi_server_stop (); /* its grid and the stream-ordered ones need not fit together */
     shmemi_check_stream_err (fn);
 }
 

@@ -61,6 +61,18 @@ static double now_s (void)
 }
 
 double shmemx_wtime (void) { return now_s (); }
+double shmemi_now (void) { return now_s (); }
+
+/* Ask a running persistent server to exit without waiting for it (fatal
+ * paths; it also leaves on its own after SHMEM_PERSISTENT_IDLE_US). */
+static void server_quit_nowait (void)
+{
+    if (shmemi.srv.running && shmemi.srv.mb != NULL) {
+        shmemi.srv.mb->cmd = MI355_SERVER_QUIT;
+        __atomic_store_n (&shmemi.srv.mb->seq, shmemi.srv.seq, __ATOMIC_RELEASE);
+        shmemi.srv.running = 0;
+    }
+}
 
 void shmemi_fatal (const char *fmt, ...)
 {
@@ -71,6 +83,7 @@ void shmemi_fatal (const char *fmt, ...)
     va_end (ap);
     fprintf (stderr, "[shmem PE %d/%d] FATAL: %s\n", shmemi.mype, shmemi.npes, msg);
     fflush (stderr);
+    server_quit_nowait ();
     if (shmemi.seg != NULL) {
         int zero = 0;
         if (atomic_compare_exchange_strong (&shmemi.seg->abort_flag, &zero, 1)) {
@@ -373,6 +386,28 @@ static void signal_init (void)
     SHMEMI_HIP (hipDeviceSynchronize ());
     shmemi.sig_count = (unsigned *) d;
     shmemi.sig_epoch = 0;
+}
+
+/* The persistent server's mailbox (host-coherent, same address on both
+ * sides) and stream; SHMEM_PERSISTENT=1 turns it on (reduce.c). */
+static void server_init (void)
+{
+    void *h = NULL, *d = NULL;
+    SHMEMI_HIP (hipHostMalloc (&h, sizeof (MI355ServerMailbox), hipHostMallocCoherent | hipHostMallocMapped));
+    SHMEMI_HIP (hipHostGetDevicePointer (&d, h, 0));
+    if (d != h)
+        shmemi_fatal ("host-coherent server mailbox maps to a different device address");
+    memset (h, 0, sizeof (MI355ServerMailbox));
+    shmemi.srv.mb = (MI355ServerMailbox *) h;
+    shmemi.srv.seq = 1;
+    SHMEMI_HIP (hipStreamCreateWithFlags (&shmemi.srv.st, hipStreamNonBlocking));
+    static const char *pe_env[] = {"SHMEM_PERSISTENT", NULL};
+    static const char *idle_env[] = {"SHMEM_PERSISTENT_IDLE_US", NULL};
+    shmemi.srv.enabled = env_long (pe_env, 0) != 0;
+    const long idle_us = env_long (idle_env, 1000);
+    shmemi.srv.idle_s = (idle_us < 10 ? 10 : idle_us) * 1e-6;
+    shmemi.srv.running = 0;
+    shmemi.srv.last_end = -1.0;
 }
 
 /* Epochs live in the low 31 bits; bit 31 marks a kernel-side timeout. */
@@ -711,6 +746,8 @@ static int heap_kind_device (void)
 void *pshmem_malloc (size_t size)
 {
     shmemi_init_check ("shmem_malloc");
+    if (shmemi.heap != NULL)
+        shmemi_server_stop (); /* hipHostRegister below */
     if (heap_kind_device ())
         return shmemx_malloc_device (size);
     void *p = NULL;
@@ -782,6 +819,8 @@ static void host_free_one (struct shmemi_hostblk *h)
 void pshmem_free (void *ptr)
 {
     shmemi_init_check ("shmem_free");
+    if (shmemi.heap != NULL)
+        shmemi_server_stop (); /* hipHostUnregister below */
     shmem_barrier_all ();
     if (ptr == NULL)
         return;
@@ -865,6 +904,7 @@ void pshmem_init (void)
     heap_init ();
     signal_init ();
     sigmem_init ();
+    server_init ();
     shmemi.fused_max = env_size ("SHMEM_FUSED_MAX_BYTES", (size_t) 1 << 20);
     shmemi.oneshot_max = env_size ("SHMEM_ONESHOT_MAX_BYTES", (size_t) 64 << 10);
 
@@ -922,6 +962,8 @@ void pshmem_finalize (void)
     if (!shmemi.initialized)
         return;
     SHMEMI_TRACE (SHMEMI_LOG_FINALIZE, "finalizing (PE %d of %d)", shmemi.mype, shmemi.npes);
+    if (shmemi.device >= 0 && shmemi.heap != NULL)
+        shmemi_server_stop ();
     /* stream-ordered collectives still queued on the caller's streams finish
      * first (they only wait on peers' kernels that are already enqueued) */
     if (shmemi.device >= 0 && shmemi.heap != NULL)
@@ -962,6 +1004,12 @@ void pshmem_finalize (void)
     free (shmemi.peer_sig);
     shmemi.peer_sig = NULL;
     shmemi.stream_err = NULL;
+    if (shmemi.srv.mb != NULL)
+        (void) hipHostFree (shmemi.srv.mb);
+    shmemi.srv.mb = NULL;
+    if (shmemi.srv.st != NULL)
+        (void) hipStreamDestroy (shmemi.srv.st);
+    shmemi.srv.st = NULL;
     if (shmemi.sig_flag != NULL)
         (void) hipHostFree (shmemi.sig_flag);
     if (shmemi.sig_count != NULL)
@@ -999,6 +1047,7 @@ void pshmem_finalize (void)
 
 void pshmem_global_exit (int status)
 {
+    server_quit_nowait ();
     if (shmemi.seg != NULL) {
         int zero = 0;
         if (atomic_compare_exchange_strong (&shmemi.seg->abort_flag, &zero, 1)) {
@@ -1117,7 +1166,30 @@ int shmemx_peer_link (int pe, int *link_type, int *hops)
     return 0;
 }
 
-void shmemx_device_synchronize (void) { SHMEMI_HIP (hipDeviceSynchronize ()); }
+void shmemx_device_synchronize (void)
+{
+    if (shmemi.initialized && shmemi.heap != NULL)
+        shmemi_server_stop (); /* a resident server would hold the synchronization until it idles out */
+    SHMEMI_HIP (hipDeviceSynchronize ());
+}
+
+int shmemx_set_persistent (int enable)
+{
+    shmemi_init_check ("shmemx_set_persistent");
+    const int prev = shmemi.srv.enabled;
+    shmemi.srv.enabled = enable != 0;
+    if (!enable && shmemi.heap != NULL)
+        shmemi_server_stop ();
+    return prev;
+}
+
+void shmemx_persistent_stats (long *served, long *launched)
+{
+    if (served != NULL)
+        *served = shmemi.srv.served;
+    if (launched != NULL)
+        *launched = shmemi.srv.launched;
+}
 
 void shmemx_memcpy (void *dst, const void *src, size_t nbytes)
 {
@@ -1150,6 +1222,7 @@ void shmemx_kernel_timing (int enable)
 void shmemi_order_after_caller (int host_wait)
 {
     if (shmemi.entry_sync) {
+        shmemi_server_stop ();
         SHMEMI_HIP (hipDeviceSynchronize ());
         return;
     }

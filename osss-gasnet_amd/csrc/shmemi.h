@@ -114,6 +114,20 @@ struct shmemi_state {
     /* stream-ordered collectives (shmemx_*_on_stream, streamops.c) */
     unsigned *stream_err;       /* host-coherent: a device-side wait timed out */
 
+    /* persistent fused server (opt-in, SHMEM_PERSISTENT; reduce.c) */
+    struct {
+        int enabled;            /* SHMEM_PERSISTENT / shmemx_set_persistent */
+        double idle_s;          /* SHMEM_PERSISTENT_IDLE_US: the server exits after this long without a call */
+        int running;
+        int op, dtype, start, stride, size;  /* the calls it serves */
+        unsigned long long grid_elems;       /* the grid it was sized for */
+        unsigned seq;           /* next mailbox seq */
+        struct MI355ServerMailbox *mb;       /* host-coherent, device-accessible */
+        hipStream_t st;         /* non-blocking stream of its own */
+        double last_end;        /* when the last fused call returned (burst detection) */
+        long served, launched;  /* statistics */
+    } srv;
+
     /* kernel timing */
     int timing;
     int ntimed;
@@ -137,6 +151,12 @@ int shmemi_pe_same_device (int pe);
 void shmemi_order_after_caller (int host_wait);
 void shmemi_check_stream_err (const char *fn);
 void shmemi_peer_acquire (hipStream_t st);
+double shmemi_now (void);
+
+/* reduce.c: the persistent fused server; every GPU operation that could wait
+ * on it (another spin-waiting grid, a device-wide synchronization, freeing
+ * memory) stops it first */
+void shmemi_server_stop (void);
 
 /* reduce.c: device-flag barrier on the library stream (host channel) */
 int shmemi_dev_barrier_ok (int PE_start, int stride, int PE_size);

@@ -48,6 +48,8 @@ def load(path=LIB_PATH):
         "shmemx_is_device_symmetric": ([_vp], _i),
         "shmemx_set_reduce_algorithm": ([_i], _i), "shmemx_get_reduce_algorithm": ([], _i),
         "shmemx_set_reduce_order": ([_i], _i), "shmemx_get_reduce_order": ([], _i),
+        "shmemx_set_persistent": ([_i], _i),
+        "shmemx_persistent_stats": ([ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_long)], None),
         "shmemx_device_id": ([], _i), "shmemx_device_synchronize": ([], None),
         "shmemx_peer_link": ([_i, ctypes.POINTER(_i), ctypes.POINTER(_i)], _i),
         "shmemx_memcpy": ([_vp, _vp, _sz], None), "shmemx_wtime": ([], ctypes.c_double),
@@ -122,6 +124,16 @@ class Shmem:
     def set_order(self, name):
         """"reference": every PE gets the reference's result for itself; "pe_start": PE_start's everywhere"""
         return self.lib.shmemx_set_reduce_order(ORDERS[name])
+
+    def set_persistent(self, enable):
+        """opt-in persistent fused server (shmemx.h); returns the previous setting"""
+        return bool(self.lib.shmemx_set_persistent(1 if enable else 0))
+
+    def persistent_stats(self):
+        """(calls served by a resident server, servers launched) since init"""
+        a, b = ctypes.c_long(), ctypes.c_long()
+        self.lib.shmemx_persistent_stats(ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
 
     def sync(self):
         self.lib.shmemx_device_synchronize()
