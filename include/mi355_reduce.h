@@ -205,9 +205,9 @@ int mi355_fused_pull (const MI355PullArgs *args, void *stream);
 /* ---- persistent fused server (opt-in; reduce.c, SHMEM_PERSISTENT) ----
  * A grid of the fused kernel that stays resident and serves back-to-back
  * calls of one (op, dtype, active set) from a mailbox in host-coherent
- * memory instead of one launch per call: the host writes the call and
- * advances `seq`; block 0 of the server polls it, broadcasts the call to the
- * other blocks through this PE's signal region (MI355_SIG_SERVER) and every
+ * memory instead of one launch per call: the host writes the call and its
+ * seq; block 0 of the server polls it, broadcasts the call to the other
+ * blocks through this PE's signal region (MI355_SIG_SERVER, same layout) and every
  * block runs the fused kernel's body on the members' heap bases (args->src /
  * args->dst at offset 0) plus the call's byte offsets. The call completes
  * as a launched one does (args->host_flag = the call's epoch).
@@ -220,14 +220,17 @@ int mi355_fused_pull (const MI355PullArgs *args, void *stream);
 #define MI355_SERVER_RUNNING 1
 #define MI355_SERVER_EXITED 2
 typedef struct MI355ServerMailbox {
-    /* host -> device (one 64-byte line): the call, then seq (release) */
+    /* host -> device, one 64-byte line the server reads with one load: the
+     * call, then seq_head and seq_tail (release, in that order); a snapshot
+     * counts only when both hold the seq it waits for */
+    unsigned seq_head;                   /* the server serves seq first_seq, first_seq + 1, ... */
+    unsigned cmd;                        /* MI355_SERVER_RUN / _QUIT */
     unsigned long long src_off, dst_off; /* byte offsets into every member's symmetric heap */
     unsigned long long n, shard;         /* as MI355FusedArgs */
     unsigned epoch;
     int oneshot;
-    unsigned cmd;                        /* MI355_SERVER_RUN / _QUIT */
-    unsigned seq;                        /* the server serves seq first_seq, first_seq + 1, ... */
-    unsigned pad0[4];
+    unsigned pad0[3];
+    unsigned seq_tail;
     /* device -> host (own line) */
     unsigned state;                      /* MI355_SERVER_RUNNING (set by the host before the launch) / _EXITED */
     unsigned state_seq;                  /* EXITED: the first seq not served */
@@ -236,11 +239,13 @@ typedef struct MI355ServerMailbox {
 
 /* Launch the server on `stream` (a stream of its own: it does not finish
  * until QUIT or idle). args: as for mi355_fused_allreduce with src/dst the
- * members' heap bases, n/shard/oneshot/epoch unused; grid_elems sizes the
- * grid (the calls it is expected to serve). mbox: device-accessible
- * host-coherent memory. */
+ * members' heap bases, n/shard/oneshot/epoch unused; grid_vecs sizes the
+ * grid as a launch of the calls it is expected to serve (16-byte vectors
+ * folded or gathered per PE: the one-shot array, or the gathered shards). mbox: device-accessible
+ * host-coherent memory. One member (nmembers = 1) serves the 1-PE identity:
+ * one-shot calls copy the source to the target. */
 int mi355_fused_server (const MI355FusedArgs *args, MI355ServerMailbox *mbox, unsigned first_seq,
-                        unsigned long long idle_ticks, unsigned long long grid_elems, void *stream);
+                        unsigned long long idle_ticks, unsigned long long grid_vecs, void *stream);
 
 /* Device-side barrier over the members (one 64-lane block): ordered on
  * `stream` after the work queued before it, and the work queued after it

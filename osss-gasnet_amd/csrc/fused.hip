@@ -450,49 +450,49 @@ __device__ __forceinline__ void st_sys_u32(unsigned *p, unsigned v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Block 0's lane 0 takes the next call from the host mailbox (or QUIT: on the
-// host's command, or after idle_ticks without a call) and broadcasts it in the
-// signal region; every other block's lane 0 waits for the broadcast. Every
+// Block 0 takes the next call from the host mailbox (or QUIT: on the host's
+// command, or after idle_ticks without a call) and broadcasts it in the
+// signal region; every other block waits for the broadcast. Both lines are
+// read whole by lanes 0-15 of wave 0 (one 64-byte request) and count when
+// their head and tail words both hold the awaited seq (written last). Every
 // block then holds the call in f[] (LDS). A broadcast seq only advances after
 // the host saw the previous call complete, which needs every block, so no
 // block can miss one.
+__device__ __forceinline__ bool line_has(const unsigned *line, unsigned seq, unsigned &v) {
+    v = ld_sys_u32(line + (threadIdx.x & 15));
+    const unsigned head = __shfl(v, 0), tail = __shfl(v, 15);
+    return head == seq && tail == seq;
+}
+
 __device__ void server_next(const MI355FusedArgs &a, MI355ServerMailbox *mb, unsigned seq,
-                            unsigned long long idle_ticks, unsigned long long *f) {
-    unsigned long long *slot = a.sig[a.me] + MI355_SIG_SERVER;
-    if (threadIdx.x == 0) {
+                            unsigned long long idle_ticks, unsigned *f) {
+    unsigned *slot = (unsigned *)(a.sig[a.me] + MI355_SIG_SERVER);
+    if (threadIdx.x < 64) {
+        const unsigned lane = threadIdx.x;
+        unsigned v = 0;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         if (blockIdx.x == 0) {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-            unsigned cmd = MI355_SERVER_QUIT;
+            const unsigned *box = (const unsigned *)mb;
             bool idle = false;
-            while (true) {
-                if (ld_sys_u32(&mb->seq) == seq) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                    cmd = ld_sys_u32(&mb->cmd);
-                    break;
-                }
+            while (!line_has(box, seq, v)) {
                 if (__builtin_amdgcn_s_memrealtime() - t0 > idle_ticks) {
                     // final look: a call rung before this point is served;
                     // after it, the host sees EXITED and launches instead
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
-                    if (ld_sys_u32(&mb->seq) == seq) continue;
+                    if (line_has(box, seq, v)) break;
                     idle = true;
                     break;
                 }
                 __builtin_amdgcn_s_sleep(2);
             }
-            f[1] = cmd;
-            if (cmd == MI355_SERVER_RUN) {
-                f[2] = ld_sys_u64(&mb->src_off);
-                f[3] = ld_sys_u64(&mb->dst_off);
-                f[4] = ld_sys_u64(&mb->n);
-                f[5] = ld_sys_u64(&mb->shard);
-                f[6] = (unsigned long long)ld_sys_u32(&mb->epoch) |
-                       ((unsigned long long)(unsigned)ld_sys_u32((const unsigned *)&mb->oneshot) << 32);
-            }
-            for (int k = 1; k < 7; ++k) st_sys_u64(slot + k, f[k]);
+            if (idle && lane == 1) v = MI355_SERVER_QUIT;  // dword 1: cmd
+            // broadcast: the call (dwords 1-14), then head and tail
+            if (lane >= 1 && lane < 15) st_sys_u32(slot + lane, v);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            st_sys_u64(slot, seq);
-            if (cmd != MI355_SERVER_RUN) {
+            if (lane == 0 || lane == 15) st_sys_u32(slot + lane, seq);
+            if (lane < 16) f[lane] = v;
+            const unsigned cmd = __shfl(v, 1);
+            if (cmd != MI355_SERVER_RUN && lane == 0) {
                 // every other block has its QUIT once it reads the broadcast;
                 // tell the host which seq was not served
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -501,20 +501,18 @@ __device__ void server_next(const MI355FusedArgs &a, MI355ServerMailbox *mb, uns
                 st_sys_u32(&mb->state, MI355_SERVER_EXITED);
             }
         } else {
-            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             unsigned spins = 0;
-            f[1] = MI355_SERVER_QUIT;
-            while (true) {
-                if (ld_sys_u64(slot) == seq) {
-                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-                    for (int k = 1; k < 7; ++k) f[k] = ld_sys_u64(slot + k);
-                    break;
-                }
+            bool got = true;
+            while (!line_has(slot, seq, v)) {
                 // block 0 broadcasts a call or QUIT within idle_ticks (plus a
                 // call's duration); this bound is only a safety net
-                if ((++spins & 63u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks + idle_ticks) break;
+                if ((++spins & 63u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > a.timeout_ticks + idle_ticks) {
+                    got = false;
+                    break;
+                }
                 __builtin_amdgcn_s_sleep(2);
             }
+            if (lane < 16) f[lane] = got ? v : (lane == 1 ? MI355_SERVER_QUIT : 0u);
         }
     }
     __syncthreads();
@@ -523,11 +521,12 @@ __device__ void server_next(const MI355FusedArgs &a, MI355ServerMailbox *mb, uns
 template <int OP, typename T>
 __global__ __launch_bounds__(kBlock) void fused_server(MI355FusedArgs a, MI355ServerMailbox *mb, unsigned first_seq,
                                                        unsigned long long idle_ticks) {
-    __shared__ unsigned long long f[8];
+    __shared__ unsigned f[16];  // the mailbox line (MI355ServerMailbox's first 16 dwords)
     for (unsigned seq = first_seq;; ++seq) {
         server_next(a, mb, seq, idle_ticks, f);
         if (f[1] != MI355_SERVER_RUN) return;
-        const Call c{f[2], f[3], f[4], f[5], (unsigned)f[6], (int)(f[6] >> 32)};
+        auto u64 = [&](int w) { return (uint64_t)f[w] | ((uint64_t)f[w + 1] << 32); };
+        const Call c{u64(2), u64(4), u64(6), u64(8), f[10], (int)f[11]};
         fused_body<OP, T>(a, c);
         __syncthreads();  // f[] is rewritten by the next server_next
     }
@@ -805,9 +804,10 @@ extern "C" int mi355_device_barrier(const MI355FusedArgs *a, void *stream) {
 }
 
 extern "C" int mi355_fused_server(const MI355FusedArgs *a, MI355ServerMailbox *mbox, unsigned first_seq,
-                                  unsigned long long idle_ticks, unsigned long long grid_elems, void *stream) {
+                                  unsigned long long idle_ticks, unsigned long long grid_vecs, void *stream) {
     if (a == nullptr || mbox == nullptr || !mi355_op_supported(a->op, a->dtype)) return MI355_E_UNSUP;
-    if (a->nmembers < 2 || a->nmembers > MI355_FUSED_MAX_MEMBERS || a->me < 0 || a->me >= a->nmembers)
+    // one member: the 1-PE identity (one-shot copy of the caller's source)
+    if (a->nmembers < 1 || a->nmembers > MI355_FUSED_MAX_MEMBERS || a->me < 0 || a->me >= a->nmembers)
         return MI355_E_INVAL;
     if (a->host_src != nullptr || a->host_dst != nullptr || a->host_flag == nullptr) return MI355_E_INVAL;
     for (int i = 0; i < a->nmembers; ++i)
@@ -818,9 +818,8 @@ extern "C" int mi355_fused_server(const MI355FusedArgs *a, MI355ServerMailbox *m
     if (a->ordered)
         for (int i = 0; i < a->nmembers; ++i)
             if (a->ver[i] == nullptr || ((uintptr_t)a->ver[i] & 15) != 0) return MI355_E_INVAL;
-    // the grid a launched call of grid_elems elements would get (one-shot size)
-    const size_t es = mi355_dtype_size(a->dtype);
-    uint64_t grid = (grid_elems * es + 16 * kBlock - 1) / (16 * kBlock);
+    // the grid a launched call moving grid_vecs 16-byte vectors per PE gets
+    uint64_t grid = (grid_vecs + kBlock - 1) / kBlock;
     if (grid < 1) grid = 1;
     if (grid > MI355_FUSED_MAX_BLOCKS) grid = MI355_FUSED_MAX_BLOCKS;
     hipStream_t st = (hipStream_t)stream;

@@ -487,7 +487,9 @@ void shmemi_server_stop (void)
     MI355ServerMailbox *mb = shmemi.srv.mb;
     if (__atomic_load_n (&mb->state, __ATOMIC_ACQUIRE) != MI355_SERVER_EXITED) {
         mb->cmd = MI355_SERVER_QUIT;
-        __atomic_store_n (&mb->seq, shmemi.srv.seq++, __ATOMIC_RELEASE);
+        const unsigned seq = shmemi.srv.seq++;
+        __atomic_store_n (&mb->seq_head, seq, __ATOMIC_RELEASE);
+        __atomic_store_n (&mb->seq_tail, seq, __ATOMIC_RELEASE);
         server_wait_exited ();
     }
     server_gone ();
@@ -506,7 +508,9 @@ static int server_call (size_t dst_off, size_t src_off, size_t n, size_t shard, 
     mb->epoch = epoch;
     mb->oneshot = oneshot;
     mb->cmd = MI355_SERVER_RUN;
-    __atomic_store_n (&mb->seq, shmemi.srv.seq++, __ATOMIC_RELEASE);
+    const unsigned seq = shmemi.srv.seq++;
+    __atomic_store_n (&mb->seq_head, seq, __ATOMIC_RELEASE);
+    __atomic_store_n (&mb->seq_tail, seq, __ATOMIC_RELEASE);
     const double t0 = shmemi_now ();
     unsigned spins = 0;
     for (;;) {
@@ -535,7 +539,7 @@ static int server_call (size_t dst_off, size_t src_off, size_t n, size_t shard, 
     }
 }
 
-static void server_start (int op, int dtype, size_t n, const struct aset *s)
+static void server_start (int op, int dtype, size_t es, size_t n, int oneshot, const struct aset *s)
 {
     MI355FusedArgs a;
     member_args (&a, s, SHMEMI_CHAN_HOST);
@@ -553,7 +557,10 @@ static void server_start (int op, int dtype, size_t n, const struct aset *s)
     MI355ServerMailbox *mb = shmemi.srv.mb;
     mb->state = MI355_SERVER_RUNNING;
     mb->state_seq = 0;
-    const int rc = mi355_fused_server (&a, mb, shmemi.srv.seq, (unsigned long long) (shmemi.srv.idle_s * 1e8), n,
+    /* the grid of this call's launch (mi355_fused_allreduce) */
+    const unsigned long long vecs = oneshot || s->size == 1 ? (n * es + 15) / 16
+                                                            : shard_chunk (n, es, s->size) * es / 16 * (s->size - 1);
+    const int rc = mi355_fused_server (&a, mb, shmemi.srv.seq, (unsigned long long) (shmemi.srv.idle_s * 1e8), vecs,
                                        shmemi.srv.st);
     if (rc != 0) {
         SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "persistent fused server not started: %d", rc);
@@ -571,14 +578,18 @@ static void server_start (int op, int dtype, size_t n, const struct aset *s)
                   s->size, n);
 }
 
+static void copy_local (size_t dst_off, size_t src_off, size_t nbytes, int timed);
+
 /* host_src/host_dst: device-accessible page-locked host buffers of this PE
- * staged in-kernel into src_off / out of dst_off (mi355_reduce.h), or NULL. */
+ * staged in-kernel into src_off / out of dst_off (mi355_reduce.h), or NULL.
+ * A one-member set (the 1-PE identity copy) comes here only with the
+ * persistent server enabled: served, or else one copy kernel. */
 static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
                          const struct aset *s, const void *host_src, void *host_dst)
 {
     const int servable = shmemi.srv.enabled && host_src == NULL && host_dst == NULL;
     const double t_call = servable ? shmemi_now () : 0.0;
-    if (servable && server_matches (op, dtype, s) && n <= 4 * shmemi.srv.grid_elems) {
+    if (servable && server_matches (op, dtype, s) && n <= 2 * shmemi.srv.grid_elems) {
         SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: persistent fused server (%zu elements, %d members)", n, s->size);
         if (server_call (dst_off, src_off, n, shard_chunk (n, es, s->size),
                          n * es <= shmemi.oneshot_max && dst_off != src_off)) {
@@ -587,46 +598,51 @@ static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t sr
         }
     }
     shmemi_server_stop (); /* a different call: the launched grid must fit */
-    SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: fused one-launch P2P, %s, %s (%zu elements, %d members)%s",
-                  n * es <= shmemi.oneshot_max && dst_off != src_off ? "one-shot" : "reduce-scatter + all-gather",
-                  ordered_pair (op, dtype, s->size) ? "every member's reference order" : "PE_start order", n,
-                  s->size, host_src != NULL ? ", staging host buffers in-kernel" : "");
-    MI355FusedArgs a;
-    memset (&a, 0, sizeof a);
-    a.op = op;
-    a.dtype = dtype;
-    a.nmembers = s->size;
-    a.me = s->me;
-    a.n = n;
-    a.shard = shard_chunk (n, es, s->size);
-    for (int i = 0; i < s->size; ++i) {
-        const int pe = aset_pe (s, i);
-        a.pe[i] = pe;
-        a.src[i] = shmemi_peer_ptr (pe, src_off);
-        a.dst[i] = shmemi_peer_ptr (pe, dst_off);
-        a.sig[i] = shmemi.peer_sig[pe] + SHMEMI_CHAN_HOST * MI355_SIG_CHANNEL_WORDS;
+    if (s->size == 1) {
+        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: 1-PE identity, one copy of %zu bytes", n * es);
+        copy_local (dst_off, src_off, n * es, 1);
+    } else {
+        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: fused one-launch P2P, %s, %s (%zu elements, %d members)%s",
+                      n * es <= shmemi.oneshot_max && dst_off != src_off ? "one-shot" : "reduce-scatter + all-gather",
+                      ordered_pair (op, dtype, s->size) ? "every member's reference order" : "PE_start order", n,
+                      s->size, host_src != NULL ? ", staging host buffers in-kernel" : "");
+        MI355FusedArgs a;
+        memset (&a, 0, sizeof a);
+        a.op = op;
+        a.dtype = dtype;
+        a.nmembers = s->size;
+        a.me = s->me;
+        a.n = n;
+        a.shard = shard_chunk (n, es, s->size);
+        for (int i = 0; i < s->size; ++i) {
+            const int pe = aset_pe (s, i);
+            a.pe[i] = pe;
+            a.src[i] = shmemi_peer_ptr (pe, src_off);
+            a.dst[i] = shmemi_peer_ptr (pe, dst_off);
+            a.sig[i] = shmemi.peer_sig[pe] + SHMEMI_CHAN_HOST * MI355_SIG_CHANNEL_WORDS;
+        }
+        a.host_flag = shmemi.sig_flag;
+        a.epoch = shmemi_next_epoch ();
+        a.err_flag = shmemi.stream_err;
+        a.timeout_ticks = (unsigned long long) (shmemi.barrier_timeout * 1e8);
+        a.host_src = host_src;
+        a.host_dst = host_dst;
+        a.share = shmemi.local_pes;
+        a.oneshot = n * es <= shmemi.oneshot_max && dst_off != src_off;
+        fused_order (&a, s, SHMEMI_CHAN_HOST);
+        shmemi_timed_begin (); /* the call's one (dominant) kernel */
+        const int rc = mi355_fused_allreduce (&a, shmemi.stream);
+        shmemi_timed_end ();
+        if (rc != 0)
+            shmemi_fatal ("fused reduction launch failed (op %d, dtype %d, %d PEs, %zu elements): %d", op, dtype,
+                          s->size, n, rc);
+        if (shmemi_wait_flag (a.epoch) != a.epoch)
+            shmemi_fatal ("fused reduction timed out waiting for the other PEs of the active set");
     }
-    a.host_flag = shmemi.sig_flag;
-    a.epoch = shmemi_next_epoch ();
-    a.err_flag = shmemi.stream_err;
-    a.timeout_ticks = (unsigned long long) (shmemi.barrier_timeout * 1e8);
-    a.host_src = host_src;
-    a.host_dst = host_dst;
-    a.share = shmemi.local_pes;
-    a.oneshot = n * es <= shmemi.oneshot_max && dst_off != src_off;
-    fused_order (&a, s, SHMEMI_CHAN_HOST);
-    shmemi_timed_begin (); /* the call's one (dominant) kernel */
-    const int rc = mi355_fused_allreduce (&a, shmemi.stream);
-    shmemi_timed_end ();
-    if (rc != 0)
-        shmemi_fatal ("fused reduction launch failed (op %d, dtype %d, %d PEs, %zu elements): %d", op, dtype,
-                      s->size, n, rc);
-    if (shmemi_wait_flag (a.epoch) != a.epoch)
-        shmemi_fatal ("fused reduction timed out waiting for the other PEs of the active set");
     if (servable) {
         /* the second call of a burst leaves the kernel resident for the next */
         if (shmemi.srv.last_end >= 0.0 && t_call - shmemi.srv.last_end < shmemi.srv.idle_s)
-            server_start (op, dtype, 2 * n, s); /* a grid for calls up to 8x this one */
+            server_start (op, dtype, es, n, n * es <= shmemi.oneshot_max && dst_off != src_off, s);
         shmemi.srv.last_end = shmemi_now ();
     }
 }
@@ -681,6 +697,10 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
             return;
         }
         if (!overlap) {
+            if (shmemi.srv.enabled && nbytes <= shmemi.fused_max && ((dst_off | src_off) & 15) == 0) {
+                fused_range (op, dtype, es, dst_off, src_off, n, s, NULL, NULL); /* persistent server */
+                return;
+            }
             SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: 1-PE identity, one copy of %zu bytes", nbytes);
             copy_local (dst_off, src_off, nbytes, 1);
             return;

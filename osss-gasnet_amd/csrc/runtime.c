@@ -69,7 +69,8 @@ static void server_quit_nowait (void)
 {
     if (shmemi.srv.running && shmemi.srv.mb != NULL) {
         shmemi.srv.mb->cmd = MI355_SERVER_QUIT;
-        __atomic_store_n (&shmemi.srv.mb->seq, shmemi.srv.seq, __ATOMIC_RELEASE);
+        __atomic_store_n (&shmemi.srv.mb->seq_head, shmemi.srv.seq, __ATOMIC_RELEASE);
+        __atomic_store_n (&shmemi.srv.mb->seq_tail, shmemi.srv.seq, __ATOMIC_RELEASE);
         shmemi.srv.running = 0;
     }
 }

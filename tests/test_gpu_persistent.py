@@ -47,14 +47,15 @@ def run(npes, script, seed=1, extra=None, timeout=300):
     return stats
 
 
-@pytest.mark.parametrize("npes", [2, 3])
+@pytest.mark.parametrize("npes", [1, 2, 3])
 def test_bursts_served_bit_exact(npes):
+    # one PE: the identity copy, served by a one-member server (in-place calls move nothing)
     st = run(npes, "burst", seed=npes)
     for s in st:
         assert s["checked"] == 192
         # most calls of a batch are served by a resident server (restarted
         # when a call is more than 4x the size it was started for)
-        assert s["served"] >= 120 and s["launched"] >= 6, s
+        assert s["served"] >= (90 if npes == 1 else 120) and s["launched"] >= 6, s
 
 
 def test_interrupted_bursts():
