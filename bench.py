@@ -121,7 +121,7 @@ def cpu_baseline(S, n_gpus, budget_s):
             "host": {"nproc": os.cpu_count(), "allowed_cpus": allowed, "cpu_model": cpu_model()}}
 
 
-def fused_same_gpu(npes, calls):
+def fused_same_gpu(npes, calls, persistent=False):
     """The fused one-launch schedule (fused.hip), which every call up to 1 MiB
     per PE takes at N > 1, measured on this box's one GPU: `npes` PE processes
     of tools/fused_bench.py sharing it (started from this process before it
@@ -132,7 +132,8 @@ def fused_same_gpu(npes, calls):
     not xGMI."""
     import subprocess
     import uuid
-    env = dict(os.environ, SHMEM_NPES=str(npes), SHMEM_JOB_ID="fb" + uuid.uuid4().hex[:10], SHMEM_DEVICE="0")
+    env = dict(os.environ, SHMEM_NPES=str(npes), SHMEM_JOB_ID="fb" + uuid.uuid4().hex[:10], SHMEM_DEVICE="0",
+               SHMEM_PERSISTENT="1" if persistent else "0")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
     script = os.path.join(ROOT, "tools", "fused_bench.py")
@@ -155,6 +156,10 @@ def fused_same_gpu(npes, calls):
     d = json.loads(lines[-1])
     d["note"] = ("fused_allreduce (one launch per call: device-side arrival/done flags) with the PEs sharing this one "
                  "GPU; us_per_call is entry-to-return, max over PEs; kernel_avg_us the fused kernel's duration")
+    if persistent:
+        d["note"] = ("the same calls with SHMEM_PERSISTENT=1: after the first two, each call is served by the fused "
+                     "kernel left resident (mi355_fused_server, fed through a host-coherent mailbox), no launch; "
+                     "kernel_avg_us covers only the launched calls")
     return d
 
 
@@ -308,9 +313,10 @@ def main():
         cpu = cpu_baseline(S, args.gpus, args.cpu_seconds)
     # the fused kernel on 2 PE processes sharing this GPU (children; this
     # process has not touched the GPU yet)
-    fused = None
+    fused = fused_p = None
     if world == 1 and not args.no_fused and not args.host:
         fused = fused_same_gpu(2, 4096 if args.no_small is False else 512)
+        fused_p = fused_same_gpu(2, 4096 if args.no_small is False else 512, persistent=True)
 
     os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(2 * S + (64 << 20)))
     os.environ.setdefault("SHMEM_DEVICE_SCRATCH_SIZE", str(96 << 20))
@@ -372,6 +378,24 @@ def main():
         steps(small_calls, small_n)
         shm.sync()
         t_small = (time.perf_counter() - ts0) / small_calls
+        shm.barrier_all()
+
+    # N = 1: the same calls with the opt-in persistent server (shmemx.h
+    # shmemx_set_persistent): the identity copy served by a resident one-member
+    # fused kernel, no launch per call. Not at N > 1 (kept out of the driver's
+    # multi-GPU line; the same-GPU multi-PE figures are in fused_same_gpu_persistent).
+    t_small_p = None
+    if small_calls and npes == 1 and not args.host:
+        shm.set_persistent(True)
+        served0, launched0 = shm.persistent_stats()
+        steps(20, small_n)
+        shm.barrier_all()
+        ts0 = time.perf_counter()
+        steps(small_calls, small_n)
+        t_small_p = (time.perf_counter() - ts0) / small_calls
+        served1, launched1 = shm.persistent_stats()
+        shm.set_persistent(False)  # stops the server
+        shm.sync()
         shm.barrier_all()
 
     # N > 1: the same K calls through RCCL (ncclAllReduce on the whole job,
@@ -625,10 +649,17 @@ def main():
             "small_call": None if t_small is None else
             {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small * 1e6, 2), "calls": small_calls,
              "note": "BASELINE config 5 shape: 4096 back-to-back 64 KiB shmem_double_sum_to_all calls, max over PEs"},
+            "small_call_persistent": None if t_small_p is None else
+            {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small_p * 1e6, 2), "calls": small_calls,
+             "served": served1 - served0, "servers_launched": launched1 - launched0,
+             "note": "the same calls with the opt-in persistent server (SHMEM_PERSISTENT): a resident kernel takes each "
+                     "call from a host-coherent mailbox instead of a launch; the call ends when the host sees its "
+                     "completion flag, as launched ones do (the timed region ends at the last call's return)"},
             "check": check,
             "op_coverage": ops,
             "kernels": kernels,
             "fused_same_gpu": fused,
+            "fused_same_gpu_persistent": fused_p,
         }
         print(json.dumps(out), flush=True)
     if args.host:

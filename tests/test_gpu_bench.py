@@ -59,6 +59,12 @@ def test_bench_one_gpu_line():
     assert "error" not in f, f
     for leg in f["legs"].values():
         assert leg["check"].startswith("bit-exact") and leg["us_per_call"] > 0 and leg["kernel_avg_us"] > 0, leg
+    fp = d["fused_same_gpu_persistent"]
+    assert "error" not in fp, fp
+    for leg in fp["legs"].values():
+        assert leg["check"].startswith("bit-exact") and leg["us_per_call"] > 0, leg
+    sp = d["small_call_persistent"]
+    assert sp["us_per_call"] > 0 and sp["served"] >= sp["calls"] - 2 and sp["servers_launched"] >= 1, sp
 
 
 @pytest.mark.multipe
@@ -67,6 +73,6 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison():
              "--master-addr", "127.0.0.1", "--master-port", "29563", "bench.py", "--gpus", "2", "--steps", "5",
              "--warmup", "2", "--force-rccl-compare"])
     common(d, 2)
-    assert d["cpu_baseline"] is None
+    assert d["cpu_baseline"] is None and d["small_call_persistent"] is None
     assert "error" in d["rccl_compare"], d["rccl_compare"]
     assert d["xgmi"]["busbw_GB_s_per_pe"] > 0
