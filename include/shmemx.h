@@ -73,13 +73,16 @@ int shmemx_get_reduce_order (void);
  * the one-launch fused schedule (up to SHMEM_FUSED_MAX_BYTES, device-resident
  * symmetric buffers) are served by a fused kernel left resident between
  * calls, fed through a host-coherent mailbox: no launch per call. Results are
- * those of the launched kernel. Caveats, hence opt-in: a call does not order
- * after GPU work the caller queued (complete its writes to the source first),
- * and while the server is resident it holds its blocks, so a caller's
- * hipDeviceSynchronize waits until it idles out (shmemx_device_synchronize
- * and every other GPU operation of this library stop it first). */
+ * those of the launched kernel. Caveats, hence opt-in: a served call is not
+ * ordered after GPU work the caller queued -- complete it first (the caller's
+ * writes to the source must be done); and while the server is resident, HIP
+ * calls that wait on the null stream or the whole device (hipDeviceSynchronize,
+ * hipStreamSynchronize(0), hipMemcpy) return only once it idles out -- on this
+ * HIP the null stream waits for the server's non-blocking stream too.
+ * shmemx_device_synchronize and every other GPU operation of this library
+ * stop it first. */
 int shmemx_set_persistent (int enable); /* returns the previous setting */
-/* calls served by a resident server, servers launched (since init) */
+/* since init: calls served by a resident server, servers launched */
 void shmemx_persistent_stats (long *served, long *launched);
 
 /* Device and timing helpers (used by bench.py and the tests). */

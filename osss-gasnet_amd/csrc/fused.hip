@@ -527,7 +527,15 @@ __global__ __launch_bounds__(kBlock) void fused_server(MI355FusedArgs a, MI355Se
         if (f[1] != MI355_SERVER_RUN) return;
         auto u64 = [&](int w) { return (uint64_t)f[w] | ((uint64_t)f[w + 1] << 32); };
         const Call c{u64(2), u64(4), u64(6), u64(8), f[10], (int)f[11]};
-        fused_body<OP, T>(a, c);
+        if (a.nmembers == 1) {
+            // the 1-PE identity: nobody to wait for -- copy, count the
+            // blocks out, the last one reports
+            block_copy(dst_of(a, c, 0), src_of(a, c, 0), c.n * sizeof(T), blockIdx.x, gridDim.x);
+            if (last_block(a.sig[0] + MI355_SIG_AG_COUNT) && threadIdx.x == 0)
+                __hip_atomic_store(a.host_flag, c.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        } else {
+            fused_body<OP, T>(a, c);
+        }
         __syncthreads();  // f[] is rewritten by the next server_next
     }
 }

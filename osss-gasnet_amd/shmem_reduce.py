@@ -49,7 +49,7 @@ def load(path=LIB_PATH):
         "shmemx_set_reduce_algorithm": ([_i], _i), "shmemx_get_reduce_algorithm": ([], _i),
         "shmemx_set_reduce_order": ([_i], _i), "shmemx_get_reduce_order": ([], _i),
         "shmemx_set_persistent": ([_i], _i),
-        "shmemx_persistent_stats": ([ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_long)], None),
+        "shmemx_persistent_stats": ([ctypes.POINTER(ctypes.c_long)] * 2, None),
         "shmemx_device_id": ([], _i), "shmemx_device_synchronize": ([], None),
         "shmemx_peer_link": ([_i, ctypes.POINTER(_i), ctypes.POINTER(_i)], _i),
         "shmemx_memcpy": ([_vp, _vp, _sz], None), "shmemx_wtime": ([], ctypes.c_double),

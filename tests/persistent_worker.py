@@ -124,6 +124,31 @@ elif script == "race":
     idle = float(os.environ.get("SHMEM_PERSISTENT_IDLE_US", "1000")) * 1e-6
     for k in range(10):
         batch("sum", "double", 40, 2048, gap=lambda: idle * 2.0 * prng.random())
+elif script == "ordered":
+    # the documented contract: GPU work the caller queued on the null stream
+    # (a 30 ms kernel, then a device-to-device copy of new data into the
+    # source) is completed by the caller before the call; that wait returns
+    # once a resident server idles out, and the call sees the new data
+    L = shm.lib
+    busy = ctypes.CDLL(os.path.join(ROOT, "osss-gasnet_amd", "lib", "libtestbusy.so"))
+    busy.test_busy_launch.argtypes = [ctypes.c_double, ctypes.c_int, ctypes.c_void_p]
+    L.hipMemcpyAsync.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    n = 4096
+    for rnd in range(4):
+        xa = [source("sum", "double", n, seed + 2 * rnd, p) for p in range(npes)]
+        xb = [source("sum", "double", n, seed + 2 * rnd + 1, p) for p in range(npes)]
+        shm.put(src_buf, xa[me])
+        shm.put(src_buf + (CAP >> 1), xb[me])  # the new data, elsewhere in the heap
+        shm.barrier_all()
+        for k in range(6):  # a burst: the server is resident after the second call
+            shm.to_all("sum", "double", dst_buf, src_buf, n, 0, 0, npes)
+        assert busy.test_busy_launch(30.0, 1, None) == 0
+        assert L.hipMemcpyAsync(src_buf, src_buf + (CAP >> 1), n * 8, 3, None) == 0  # hipMemcpyDeviceToDevice
+        assert L.hipStreamSynchronize(None) == 0
+        shm.to_all("sum", "double", dst_buf, src_buf, n, 0, 0, npes)
+        assert_match(shm.get(dst_buf, n, "double"), oracle.reduce_pe("sum", "double", xb, me), "sum", "double",
+                     f"PE {me} round {rnd}: the call after queued null-stream work")
+        checked += 1
 else:
     raise SystemExit(f"unknown script {script}")
 

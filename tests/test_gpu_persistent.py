@@ -5,7 +5,9 @@ checked bit-exact against the oracle's result for that PE; the stats show
 that a resident server served the calls. Scripts: bursts of every kind of
 call the server takes (one-shot/two-shot, in place, offsets, ordered pairs);
 bursts interrupted by operations that stop it; gaps longer than its idle
-time; gaps around the idle time (a call rung as the server leaves)."""
+time; gaps around the idle time (a call rung as the server leaves); a call
+after GPU work the caller queued and then completed (it sees that work's
+result)."""
 import json
 import os
 import subprocess
@@ -75,3 +77,12 @@ def test_call_rung_as_the_server_leaves():
     st = run(2, "race", seed=11, extra={"SHMEM_PERSISTENT_IDLE_US": "60"})
     for s in st:
         assert s["checked"] == 400 and s["launched"] >= 10 and s["served"] >= 10, s
+
+
+@pytest.mark.parametrize("npes", [1, 2])
+def test_call_after_the_callers_queued_work(npes):
+    # the caller completes its queued null-stream work (hipStreamSynchronize)
+    # before the call: no hang, and the call reduces the new data
+    st = run(npes, "ordered", seed=13)
+    for s in st:
+        assert s["checked"] == 4 and s["launched"] >= 1, s
