@@ -131,6 +131,8 @@ void shmemi_trace_show_info (void)
         {"SHMEM_REDUCE_ORDER", "reference (each PE gets the reference's result for itself) | pe_start"},
         {"SHMEM_DEVICE_ORDER_SIZE", "version areas of the per-PE-order schedule (default 512M, 2 channels)"},
         {"SHMEM_FUSED_GRID_SHARE", "size the spin-waiting grids as if this many PEs shared the GPU"},
+        {"SHMEM_PERSISTENT", "1: back-to-back fused calls served by a resident fused kernel (opt-in; shmemx.h)"},
+        {"SHMEM_PERSISTENT_IDLE_US", "the persistent server leaves after this long without a call (default 1000)"},
         {"SHMEM_FUSED_MAX_BYTES", "largest message for the one-launch fused reduction (default 1M)"},
         {"SHMEM_ONESHOT_MAX_BYTES", "largest fused message folded one-shot, not reduce-scatter + all-gather (default 64K)"},
         {"SHMEM_BARRIER_TIMEOUT", "seconds before a barrier wait aborts the job (default 600)"},
