@@ -111,6 +111,18 @@ elif script == "mixed":
             b = shm.get(dst_buf + (CAP >> 1), 64, "long")
             assert (b == np.arange(64, dtype=np.int64)).all(), f"broadcast mismatch on PE {me}"
         batch("sum", "double", 6, 4096)
+        # a stream-ordered reduction (its own spin-waiting kernel) while a server is resident
+        xs = [source("max", "float", 3000, seed + 10 + rnd, p) for p in range(npes)]
+        shm.put(src_buf + (CAP >> 1), xs[me])
+        batch("sum", "double", 4, 4096)
+        st = shm.stream_create()
+        shm.to_all_on_stream("max", "float", dst_buf + (CAP >> 1), src_buf + (CAP >> 1), 3000, 0, 0, npes, st)
+        shm.stream_sync(st)
+        shm.stream_destroy(st)
+        assert_match(shm.get(dst_buf + (CAP >> 1), 3000, "float"), oracle.reduce_pe("max", "float", xs, me), "max",
+                     "float", f"PE {me} stream-ordered call")
+        checked += 1
+        batch("sum", "double", 4, 4096)
         shm.sync()
 elif script == "idle":
     # gaps longer than the server's idle time: it leaves between calls, and
