@@ -283,15 +283,22 @@ __device__ __forceinline__ void versions_vec(const MI355FusedArgs &a, const Call
 }
 
 // The whole call, on every block of the grid (the launched kernel's and the
-// server's).
+// server's). next_counts: this block ran the previous call of the same
+// active set (a server's later calls), so every pair count is the one it
+// held then plus one -- LDS keeps them, no read of CALLS.
 template <int OP, typename T>
-__device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &c) {
+__device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &c, bool next_counts = false) {
     constexpr int V = 16 / sizeof(T);
     unsigned long long *mine = a.sig[a.me];
     __shared__ int ok_all;
     __shared__ unsigned long long cnt[MI355_FUSED_MAX_MEMBERS];
     if (threadIdx.x == 0) ok_all = 1;
-    load_counts(a, mine, cnt);
+    if (next_counts) {
+        if (threadIdx.x < a.nmembers) ++cnt[threadIdx.x];
+        __syncthreads();
+    } else {
+        load_counts(a, mine, cnt);
+    }
 
     const bool staged = a.host_src != nullptr;
     if (staged) {
@@ -534,7 +541,7 @@ __global__ __launch_bounds__(kBlock) void fused_server(MI355FusedArgs a, MI355Se
             if (last_block(a.sig[0] + MI355_SIG_AG_COUNT) && threadIdx.x == 0)
                 __hip_atomic_store(a.host_flag, c.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         } else {
-            fused_body<OP, T>(a, c);
+            fused_body<OP, T>(a, c, seq != first_seq);
         }
         __syncthreads();  // f[] is rewritten by the next server_next
     }
