@@ -212,11 +212,52 @@ __device__ __forceinline__ void orders_element(const OrdersParams &p, int64_t i)
 // before the loads (the stores' data registers are reused as load addresses
 // across the branches), which halved the kernel's rate at 2-4 sources
 // (tools/orders_probe.hip; rocprofv3 160 vs 82 us at 4 x 64 MiB).
+// The software x87 sum/product: NSRC * (NSRC - 1) soft-float operations per
+// element do not unroll, and the sources held in a register array indexed by
+// the loop variables would live in scratch memory; instead each member's
+// fold re-reads the sources (hits in L2 after the first member), the member
+// whose output aliases its source (in place) last. (x87 min/max, a compare
+// and a select, keeps the register form: 210 vs 337 us at 8 x 32 MiB.)
+template <int OP, int NSRC, bool ALL>
+__device__ __forceinline__ void x80_orders_vector(const OrdersParams &p, uint64_t i) {
+    int last = -1;
+#pragma unroll 1
+    for (int q = 0; q < NSRC; ++q) {
+        if (!ALL && p.dst[q] == nullptr) continue;
+        if (p.dst[q] == p.src[q]) {
+            last = q;
+            continue;
+        }
+        x80 acc = ((const x80 *)p.src[q])[i];
+#pragma unroll 1
+        for (int k = 0; k < NSRC; ++k)
+            if (k != q) acc = apply<OP>(acc, ((const x80 *)p.src[k])[i]);
+        Pack<x80> o;
+        o.e[0] = acc;
+        st16_fold((u32x4 *)p.dst[q] + i, o.v);
+    }
+    if (last >= 0) {
+        x80 acc = ((const x80 *)p.src[last])[i];
+#pragma unroll 1
+        for (int k = 0; k < NSRC; ++k)
+            if (k != last) acc = apply<OP>(acc, ((const x80 *)p.src[k])[i]);
+        Pack<x80> o;
+        o.e[0] = acc;
+        st16_fold((u32x4 *)p.dst[last] + i, o.v);
+    }
+}
+
 template <int OP, typename T, int NSRC, int UNROLL, int POL, bool ALL>
 __global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
     constexpr int V = 16 / sizeof(T);
     const uint64_t nvec = p.nvec;
     const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
+    if constexpr (std::is_same<T, x80>::value && (OP == MI355_OP_SUM || OP == MI355_OP_PROD)) {
+        for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (uint64_t)gridDim.x * kBlock)
+            x80_orders_vector<OP, NSRC, ALL>(p, i);
+        signal_done(p.sig, false);
+        return;
+    }
     for (uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x; base < nvec;
          base += step) {
         Pack<T> x[UNROLL][NSRC];

@@ -94,6 +94,22 @@ __device__ __forceinline__ bool is_inf(const x80 &a) {
 }
 __device__ __forceinline__ bool is_zero(const x80 &a) { return efield(a) == 0 && a.m == 0; }
 
+// c ? a : b as masks on the two 64-bit words: a select of structs (or of
+// their fields, which the compiler turns back into a select of their
+// addresses) keeps both operands in scratch memory -- two scratch stores per
+// operation in the fold loops.
+__device__ __forceinline__ x80 pick(bool c, const x80 &a, const x80 &b) {
+    const uint64_t k = 0ull - (uint64_t)c;
+    uint64_t ah, bh;
+    __builtin_memcpy(&ah, &a.se, 8);  // sign/exponent and padding
+    __builtin_memcpy(&bh, &b.se, 8);
+    x80 r;
+    r.m = (a.m & k) | (b.m & ~k);
+    const uint64_t h = (ah & k) | (bh & ~k);
+    __builtin_memcpy(&r.se, &h, 8);
+    return r;
+}
+
 __device__ __forceinline__ x80 make(int s, int e, uint64_t m, const x80 &padsrc) {
     x80 r = padsrc;  // keep the accumulator's padding bytes
     r.m = m;
@@ -112,10 +128,10 @@ __device__ __forceinline__ x80 nan_result(const x80 &a, const x80 &b) {
     const bool na = is_nan(a), nb = is_nan(b);
     if (na && nb) {
         const uint64_t ma = a.m | 0x4000000000000000ull, mb = b.m | 0x4000000000000000ull;
-        if (ma != mb) return quiet(ma > mb ? a : b);
-        return quiet(sign(a) == 0 ? a : b);
+        if (ma != mb) return quiet(pick(ma > mb, a, b));
+        return quiet(pick(sign(a) == 0, a, b));
     }
-    return quiet(na ? a : b);
+    return quiet(pick(na, a, b));
 }
 
 __device__ __forceinline__ int exp_of(const x80 &a) {  // value = m * 2^E
@@ -169,13 +185,100 @@ __device__ __forceinline__ x80 round_pack(int s, u128 W, int Ew, bool sticky, co
     return make(s, ef, m, padsrc);
 }
 
-__device__ __forceinline__ x80 add(const x80 &a, const x80 &b) {
+// Round-to-nearest-even of a 64-bit significand m with the 64 bits below it
+// in rem (and a sticky bit beyond them): true when m must go up by one.
+__device__ __forceinline__ bool round_up(uint64_t m, uint64_t rem, bool sticky) {
+    constexpr uint64_t half = 0x8000000000000000ull;
+    return rem > half || (rem == half && (sticky || (m & 1)));
+}
+
+// Fast path of add/mul: both operands normal with exponent fields in
+// [1, kFastMax], so every result is normal or an exact zero and no rounding
+// can overflow; the rest (zeros, denormals, infinities, NaNs, unsupported
+// encodings, near-overflow exponents, alignment shifts beyond 64 bits,
+// results that would be denormal) takes the general path. Both paths round
+// the exact result once, so they agree bit for bit where both apply.
+constexpr int kFastMax = kEmaxField - 3;
+__device__ __forceinline__ bool fast_operand(const x80 &a) {
+    const int e = efield(a);
+    return e >= 1 && e <= kFastMax && jbit(a);
+}
+
+// The fast paths run when every active lane of the wave can take them (one
+// vote, a uniform branch); otherwise the whole wave takes the general path.
+// (Diverging per lane between the two paths gave nondeterministic one-ulp
+// errors in the general path's results on gfx950 -- test_longdouble_
+// random_encodings -- so the choice is per wave.)
+__device__ __forceinline__ bool add_fast(const x80 &a, const x80 &b, x80 &r) {
+    if (fast_operand(a) && fast_operand(b)) {
+        const int ea = efield(a), eb = efield(b);
+        const bool a_big = (ea > eb) || (ea == eb && a.m >= b.m);
+        const int EA = a_big ? ea : eb, d = a_big ? ea - eb : eb - ea;
+        const uint64_t MA = a_big ? a.m : b.m, MB = a_big ? b.m : a.m;
+        const int sa = sign(a), sb = sign(b);  // scalars: no struct select
+        const int sA = a_big ? sa : sb, sB = a_big ? sb : sa;
+        if (d <= 64) {
+            // B aligned under A in 128 bits, exactly: A = MA:0, B = Bh:Bl
+            const uint64_t Bh = d == 64 ? 0 : MB >> d;
+            const uint64_t Bl = d == 0 ? 0 : (d == 64 ? MB : MB << (64 - d));
+            if (sA == sB) {
+                uint64_t hi = MA + Bh, lo = Bl;
+                int E = EA;
+                bool sticky = false;
+                if (hi < MA) {  // carry out: shift the 129-bit sum right by one
+                    sticky = (lo & 1) != 0;
+                    lo = (lo >> 1) | (hi << 63);
+                    hi = (hi >> 1) | 0x8000000000000000ull;
+                    ++E;
+                }
+                if (round_up(hi, lo, sticky)) {
+                    if (++hi == 0) {
+                        hi = 0x8000000000000000ull;
+                        ++E;
+                    }
+                }
+                r = make(sA, E, hi, a);
+                return true;
+            }
+            // A - B >= 0, exact in 128 bits
+            uint64_t lo = 0 - Bl;
+            uint64_t hi = MA - Bh - (Bl != 0 ? 1 : 0);
+            if (hi == 0 && lo == 0) {  // exact cancellation: +0
+                r = make(0, 0, 0, a);
+                return true;
+            }
+            const int L = hi ? 127 - __builtin_clzll(hi) : 63 - __builtin_clzll(lo);
+            const int shift = 127 - L;  // normalize the leading bit to bit 127
+            if (EA - shift >= 1) {
+                if (shift >= 64) {
+                    hi = lo << (shift - 64);
+                    lo = 0;
+                } else if (shift > 0) {
+                    hi = (hi << shift) | (lo >> (64 - shift));
+                    lo <<= shift;
+                }
+                int E = EA - shift;
+                if (round_up(hi, lo, false)) {
+                    if (++hi == 0) {
+                        hi = 0x8000000000000000ull;
+                        ++E;
+                    }
+                }
+                r = make(sA, E, hi, a);
+                return true;
+            }
+        }
+    }
+    return false;
+}
+
+__device__ __forceinline__ x80 add_general(const x80 &a, const x80 &b) {
     if (unsupported(a) || unsupported(b)) return indefinite(a);
     if (is_nan(a) || is_nan(b)) return nan_result(a, b);
     const int sa = sign(a), sb = sign(b);
     if (is_inf(a) || is_inf(b)) {
         if (is_inf(a) && is_inf(b) && sa != sb) return indefinite(a);
-        return is_inf(a) ? a : make(sb, kEmaxField, 0x8000000000000000ull, a);
+        return pick(is_inf(a), a, make(sb, kEmaxField, 0x8000000000000000ull, a));
     }
     if (is_zero(a) && is_zero(b)) return make(sa & sb, 0, 0, a);
     // order by magnitude: A >= B
@@ -208,7 +311,39 @@ __device__ __forceinline__ x80 add(const x80 &a, const x80 &b) {
     return round_pack(sA, W, EA - 62, sticky, a);
 }
 
-__device__ __forceinline__ x80 mul(const x80 &a, const x80 &b) {
+__device__ __forceinline__ x80 add(const x80 &a, const x80 &b) {
+    x80 r = a;
+    const bool ok = add_fast(a, b, r);
+    if (__all(ok)) return r;
+    return add_general(a, b);
+}
+
+__device__ __forceinline__ bool mul_fast(const x80 &a, const x80 &b, x80 &r) {
+    if (fast_operand(a) && fast_operand(b)) {
+        // biased exponent of the product with its leading bit at 127 (or 126)
+        const int E = efield(a) + efield(b) - kBias + 1;
+        if (E >= 2 && E <= kFastMax) {
+            uint64_t hi = __umul64hi(a.m, b.m), lo = a.m * b.m;
+            int Ef = E;
+            if ((hi >> 63) == 0) {  // leading bit at 126: one left shift
+                hi = (hi << 1) | (lo >> 63);
+                lo <<= 1;
+                --Ef;
+            }
+            if (round_up(hi, lo, false)) {
+                if (++hi == 0) {
+                    hi = 0x8000000000000000ull;
+                    ++Ef;
+                }
+            }
+            r = make(sign(a) ^ sign(b), Ef, hi, a);
+            return true;
+        }
+    }
+    return false;
+}
+
+__device__ __forceinline__ x80 mul_general(const x80 &a, const x80 &b) {
     if (unsupported(a) || unsupported(b)) return indefinite(a);
     if (is_nan(a) || is_nan(b)) return nan_result(a, b);
     const int s = sign(a) ^ sign(b);
@@ -220,6 +355,13 @@ __device__ __forceinline__ x80 mul(const x80 &a, const x80 &b) {
     if (is_zero(a) || is_zero(b)) return make(s, 0, 0, a);
     const u128 P = mk(__umul64hi(a.m, b.m), a.m * b.m);
     return round_pack(s, P, exp_of(a) + exp_of(b), false, a);
+}
+
+__device__ __forceinline__ x80 mul(const x80 &a, const x80 &b) {
+    x80 r = a;
+    const bool ok = mul_fast(a, b, r);
+    if (__all(ok)) return r;
+    return mul_general(a, b);
 }
 
 // a < b on the x87 (false when unordered: NaN or an unsupported encoding).
@@ -244,6 +386,6 @@ template <int OP>
 __device__ __forceinline__ x80 x80_op(x80 a, x80 b) {
     if constexpr (OP == 0) return x80d::add(a, b);          // MI355_OP_SUM
     else if constexpr (OP == 1) return x80d::mul(a, b);     // MI355_OP_PROD
-    else if constexpr (OP == 5) return x80d::less(a, b) ? a : b;   // MI355_OP_MIN
-    else return x80d::less(b, a) ? a : b;                   // MI355_OP_MAX: a > b
+    else if constexpr (OP == 5) return x80d::pick(x80d::less(a, b), a, b);  // MI355_OP_MIN
+    else return x80d::pick(x80d::less(b, a), a, b);                   // MI355_OP_MAX: a > b
 }

@@ -179,6 +179,67 @@ def test_longdouble_random_encodings(shm, dev):
         dev.free()
 
 
+def _x80(rng, n, e, m=None, s=None):
+    """long doubles from sign, biased exponent field and significand arrays"""
+    raw = np.zeros((n, 16), dtype=np.uint8)
+    if m is None:
+        m = rng.integers(0, 2**64, n, dtype=np.uint64, endpoint=False) | np.uint64(1 << 63)
+    if s is None:
+        s = rng.integers(0, 2, n).astype(np.uint16)
+    se = (s.astype(np.uint16) << np.uint16(15)) | np.asarray(e, dtype=np.uint16)
+    raw[:, 0:8] = m.view(np.uint8).reshape(n, 8)
+    raw[:, 8:10] = se.view(np.uint8).reshape(n, 2)
+    return raw.view(np.longdouble).reshape(n)
+
+
+@pytest.mark.parametrize("case", ["near", "spread", "cancel", "edges", "mixed"])
+def test_longdouble_add_mul_paths(shm, dev, case):
+    """x80.h's fast add/mul (normal operands, exponent fields up to 0x7FFC,
+    alignment within 64 bits, normal results) and its general path meet at
+    their boundaries: sums and products of two sources, 2^20 pairs per case,
+    bit-exact against the host x87 (gcc long double, the oracle).
+      near    exponent differences 0-3, random signs: carries, cancellations
+      spread  differences 0-70: the 64-bit alignment limit and beyond
+      cancel  b = -a with its last significand bits perturbed: deep cancellation
+      edges   exponent fields near 1 and near 0x7FFC-0x7FFE: denormal and
+              overflowing results, and operands just outside the fast path
+      mixed   the above with zeros, denormals, infinities and NaNs sprinkled in"""
+    rng = np.random.default_rng({"near": 1, "spread": 2, "cancel": 3, "edges": 4, "mixed": 5}[case])
+    n = 1 << 20
+    e0 = rng.integers(1, 0x7FFF, n)
+    if case == "near":
+        ea, eb = e0 % 0x7F00 + 100, None
+        eb = ea + rng.integers(-3, 4, n)
+    elif case == "spread":
+        ea = rng.integers(16000, 16800, n)
+        eb = ea - rng.integers(0, 71, n)
+    elif case == "cancel":
+        a = _x80(rng, n, rng.integers(100, 32000, n))
+        m = a.view(np.uint8).reshape(n, 16)[:, 0:8].copy().view(np.uint64).reshape(n)
+        m2 = m ^ rng.integers(0, 1 << 12, n, dtype=np.uint64)
+        se = a.view(np.uint8).reshape(n, 16)[:, 8:10].copy().view(np.uint16).reshape(n)
+        b = _x80(rng, n, se & np.uint16(0x7FFF), m=m2 | np.uint64(1 << 63), s=((se >> np.uint16(15)) ^ np.uint16(1)))
+        srcs = [a, b]
+    elif case in ("edges", "mixed"):
+        pick = rng.integers(0, 3, n)
+        ea = np.where(pick == 0, rng.integers(1, 80, n), np.where(pick == 1, rng.integers(0x7FF8, 0x7FFF, n),
+                                                                   rng.integers(16000, 16800, n)))
+        eb = np.where(pick == 0, rng.integers(1, 80, n), np.where(pick == 1, rng.integers(0x3F80, 0x4080, n),
+                                                                   ea - rng.integers(-2, 3, n)))
+        eb = np.clip(eb, 1, 0x7FFE)
+    if case != "cancel":
+        srcs = [_x80(rng, n, ea), _x80(rng, n, eb)]
+    if case == "mixed":
+        specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 5e-4940], dtype=np.longdouble)
+        for k in range(2):
+            where = rng.random(n) < 0.05
+            srcs[k][where] = specials[rng.integers(0, len(specials), int(where.sum()))]
+    for op in ("sum", "prod"):
+        got = gpu_fold(shm, dev, op, "longdouble", srcs)
+        assert_match(got, oracle.reduce_pe(op, "longdouble", srcs, 0), op, "longdouble", ctx=case)
+        dev.free()
+
+
 def test_complex_prod_annex_g_cases(shm, dev):
     inf, nan = np.inf, np.nan
     vals = [complex(inf, nan), complex(nan, inf), complex(inf, inf), complex(nan, nan), complex(0, 0),

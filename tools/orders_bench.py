@@ -29,8 +29,16 @@ L = shm.lib
 L.mi355_time_next_launch.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
 L.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), ctypes.c_void_p, ctypes.c_void_p]
 src_arena, out_arena = shm.malloc_device(S), shm.malloc_device(S)
-shm.put(src_arena, np.random.default_rng(3).random(S // 8) - 0.5)
+rand = np.random.default_rng(3).random(S // 8) - 0.5
 shm.put(out_arena, np.zeros(S // 8))
+
+
+def fill(dtype):
+    """source values of the type (long double: normal x87 values, not double bit patterns)"""
+    if dtype == "longdouble":
+        shm.put(src_arena, rand[:S // 16].astype(np.longdouble))
+    else:
+        shm.put(src_arena, rand)
 e0, e1 = ctypes.c_void_p(), ctypes.c_void_p()
 L.hipEventCreate(ctypes.byref(e0))
 L.hipEventCreate(ctypes.byref(e1))
@@ -52,8 +60,9 @@ def timed(launch):
 
 
 for op, dtype in [("sum", "double"), ("sum", "float"), ("max", "float"), ("min", "double"), ("prod", "complexd"),
-                  ("sum", "complexf"), ("sum", "longdouble"), ("max", "longdouble")]:
+                  ("sum", "complexf"), ("sum", "longdouble"), ("prod", "longdouble"), ("max", "longdouble")]:
     es = np.dtype(shmem_reduce.NP[dtype]).itemsize
+    fill(dtype)
     for npes in (2, 4, 8):
         shard = S // npes
         n = shard // es
