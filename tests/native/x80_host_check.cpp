@@ -1,0 +1,74 @@
+// x80_host_check.cpp -- osss-gasnet_amd/csrc/x80.h (the GPU's x87 long double
+// arithmetic in integer code) compiled for the CPU and checked bit for bit
+// against the host's own x87 `long double` + and * (what the reference's
+// reduce-op.c:99 element functions execute), on pairs aimed at both of its
+// paths and the boundaries between them: exponent differences 0-3 and 0-70,
+// fields near 1 and near the top, exact and near cancellation, random fields.
+// Built and run by tests/test_x80_host.py (CPU). usage: x80_host_check [pairs per case]
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <random>
+
+#define __device__
+#define __forceinline__ inline
+#define __all(x) (x)
+static inline uint64_t __umul64hi(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
+#include "x80.h"
+
+static bool same(const x80 &a, long double v) {
+    unsigned char w[10];
+    memcpy(w, &v, 10);
+    return memcmp(&a, w, 10) == 0;
+}
+
+int main(int argc, char **argv) {
+    const long per = argc > 1 ? atol(argv[1]) : 1000000;
+    std::mt19937_64 g(7);
+    long bad = 0, n = 0;
+    auto mk = [&](int e, int s) {
+        x80 r;
+        memset(&r, 0, sizeof r);
+        r.m = g() | (1ull << 63);
+        r.se = (uint16_t)((s << 15) | e);
+        return r;
+    };
+    for (int round = 0; round < 6; ++round)
+        for (long i = 0; i < per; ++i) {
+            int ea, eb;
+            switch (round) {
+            case 0: ea = 100 + (int)(g() % 32500); eb = ea + (int)(g() % 7) - 3; break;
+            case 1: ea = 16000 + (int)(g() % 800); eb = ea - (int)(g() % 71); break;
+            case 2: ea = 1 + (int)(g() % 80); eb = 1 + (int)(g() % 80); break;
+            case 3: ea = 0x7FF8 + (int)(g() % 7); eb = 0x3F80 + (int)(g() % 256); break;
+            case 4: ea = 1 + (int)(g() % 0x7FFE); eb = 1 + (int)(g() % 0x7FFE); break;
+            default: ea = 16383 + (int)(g() % 5); eb = ea; break;
+            }
+            if (eb < 1) eb = 1;
+            if (eb > 0x7FFE) eb = 0x7FFE;
+            x80 a = mk(ea, (int)(g() & 1)), b = mk(eb, (int)(g() & 1));
+            if (round == 5) {  // b = -a with the low significand bits perturbed
+                b.m = (a.m ^ (g() & 0xFFF)) | (1ull << 63);
+                b.se = a.se ^ 0x8000;
+            }
+            long double la, lb;
+            memset(&la, 0, sizeof la);
+            memset(&lb, 0, sizeof lb);
+            memcpy(&la, &a, 10);
+            memcpy(&lb, &b, 10);
+            volatile long double s = la + lb, p = la * lb;
+            ++n;
+            if (!same(x80d::add(a, b), s)) {
+                if (bad < 5) printf("add mismatch: case %d fields %d %d\n", round, ea, eb);
+                ++bad;
+            }
+            if (!same(x80d::mul(a, b), p)) {
+                if (bad < 5) printf("mul mismatch: case %d fields %d %d\n", round, ea, eb);
+                ++bad;
+            }
+        }
+    printf("%ld pairs, %ld mismatches\n", n, bad);
+    return bad != 0;
+}
