@@ -320,6 +320,9 @@ def main():
 
     os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(2 * S + (64 << 20)))
     os.environ.setdefault("SHMEM_DEVICE_SCRATCH_SIZE", str(96 << 20))
+    # a PE that never arrives ends the bench within two minutes with the
+    # library's diagnostic (the library default, 600 s, suits long jobs)
+    os.environ.setdefault("SHMEM_BARRIER_TIMEOUT", "120")
     shm = shmem_reduce.Shmem()
     shm.init()
     shm.set_algorithm(args.algorithm)

@@ -68,15 +68,19 @@ static int rccl_comm_create (double timeout_s, char *why, size_t why_len)
     ncclUniqueId id;
     _Static_assert (sizeof id <= sizeof shmemi.seg->rccl_id, "ncclUniqueId too large");
     memset (&id, 0, sizeof id);
-    if (shmemi.mype == 0 && ncclGetUniqueId (&id) != ncclSuccess) {
-        snprintf (why, why_len, "ncclGetUniqueId failed");
-        return -1; /* the other PEs time out below */
-    }
+    const int id_failed = shmemi.mype == 0 && ncclGetUniqueId (&id) != ncclSuccess;
+    if (id_failed)
+        memset (&id, 0, sizeof id); /* published as all zero: every PE gives up */
     if (shmemi.seg != NULL) { /* one PE has no bootstrap segment */
         if (shmemi.mype == 0)
             memcpy (shmemi.seg->rccl_id, &id, sizeof id);
         shmemi_barrier_set (0, 1, shmemi.npes);
         memcpy (&id, shmemi.seg->rccl_id, sizeof id);
+    }
+    static const ncclUniqueId zero_id;
+    if (id_failed || memcmp (&id, &zero_id, sizeof id) == 0) {
+        snprintf (why, why_len, "ncclGetUniqueId failed on PE 0");
+        return -1;
     }
     ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
     cfg.blocking = 0;

@@ -242,11 +242,13 @@ def test_more_than_eight_pes_one_gpu(tmp_path, npes):
 
 def test_reduction_while_another_kernel_holds_every_cu(tmp_path):
     """PE 0 enters each collective right after queueing, on a stream of its
-    own, a kernel that fills every CU for 300 ms: its spin-waiting grid (fused
-    one-launch, or the device barriers of the multi-launch schedule) can only
-    start block by block as that kernel drains, while its peers already wait
-    in theirs. Every call must complete with the right result, well inside
-    the barrier timeout."""
+    own, a kernel that fills every CU for 300 ms (the helper returns once all
+    of its blocks are resident): its spin-waiting grid (fused one-launch, or
+    the device barriers of the multi-launch schedule) starts block by block as
+    that kernel drains -- or, when the GPU's scheduler time-slices the busy
+    queue out (seen on some boxes: the call then returns in ~0.1 ms), at once
+    -- while its peers already wait in theirs. Every call must complete with
+    the right result, well inside the barrier timeout."""
     cases = make_cases([("sum", "double")], 8000, [[0, 0, 3]], "dev", "p2p", 0)        # fused one-shot
     cases += make_cases([("max", "float")], 100000, [[0, 0, 3]], "dev", "p2p", 100)   # fused two-shot
     cases += make_cases([("sum", "double")], 300000, [[0, 0, 3]], "dev", "p2p", 200)  # multi-launch
@@ -256,7 +258,8 @@ def test_reduction_while_another_kernel_holds_every_cu(tmp_path):
     check(results, cases)
     for c in cases:
         t = float(results[0][str(c["id"]) + "_seconds"][0])
-        assert 0.2 < t < 10.0, f"case {c['id']}: {t:.3f} s from the busy launch to the call's return"
+        assert t < 10.0, f"case {c['id']}: {t:.3f} s from the busy launch to the call's return"
+        print(f"case {c['id']}: {t * 1e3:.1f} ms from the busy grid holding every CU to the call's return")
 
 
 def test_largest_messages(tmp_path):
