@@ -43,7 +43,7 @@ def oshrun_queues(npes, env):
     return mod.hw_queue_env(npes, True, env)
 
 
-def run_pes(npes, cases, tmp_path, extra_env=None, timeout=600):
+def run_pes(npes, cases, tmp_path, extra_env=None, timeout=600, per_pe_env=None):
     spec = tmp_path / "spec.json"
     spec.write_text(json.dumps({"cases": cases}))
     env = dict(os.environ)
@@ -62,6 +62,7 @@ def run_pes(npes, cases, tmp_path, extra_env=None, timeout=600):
     procs = []
     for pe in range(npes):
         e = dict(env, SHMEM_PE=str(pe))
+        e.update((per_pe_env or {}).get(pe, {}))
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "pe_worker.py"), str(spec), str(tmp_path)],
                                       env=e, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
@@ -426,3 +427,75 @@ def test_random_sequence_stress(tmp_path):
                                                      "SHMEM_DEVICE_SCRATCH_SIZE": "3M",
                                                      "SHMEM_DEVICE_ORDER_SIZE": "256K"})
     check(results, cases)
+
+
+# The RCCL schedule (SHMEM_REDUCE_ALGORITHM=rccl, csrc/rccl.c) with more than
+# one rank. RCCL refuses two ranks on one GPU of one host ("Duplicate GPU
+# detected"), and the test box has one GPU, so each PE announces a host of its
+# own (NCCL_HOSTID): RCCL then connects the ranks through its socket network
+# transport over loopback instead of xGMI. The transport is not what is under
+# test -- the library's glue is: communicator bring-up through the bootstrap
+# segment, the type/operator mapping, short widened to int32 and truncated,
+# complex sum as 2n reals, staging of host arrays, in place.
+RCCL_PAIRS = [("sum", "double"), ("sum", "float"), ("prod", "double"), ("sum", "int"), ("prod", "long"),
+              ("max", "longlong"), ("min", "int"), ("sum", "short"), ("prod", "short"), ("max", "short"),
+              ("sum", "complexd"), ("sum", "complexf"), ("max", "double"), ("min", "float")]
+
+
+def rccl_multi_rank(npes, cases, tmp_path):
+    per_pe = {pe: {"NCCL_HOSTID": f"shmem-rccl-test-pe{pe}"} for pe in range(npes)}
+    return run_pes(npes, cases, tmp_path, per_pe_env=per_pe,
+                   extra_env={"NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1", "SHMEM_DEVICE_SCRATCH_SIZE": "3M"})
+
+
+def check_rccl(results, cases, npes):
+    """RCCL's own reduction order: integers bit-exact; at 2 PEs FP sum/prod
+    too (a + b and a * b commute in IEEE arithmetic); at 3 PEs FP sums and
+    products within DESIGN.md's bounds 2 (N-1) u sum|x_i| and 2 (N-1) u
+    |prod x_i| of the reference's result for the PE;
+    FP min/max equal as values where no input is NaN (RCCL's NaN and +-0
+    selects are not the reference's -- one reason RCCL is opt-in)."""
+    for c in cases:
+        op, dtype, n = c["op"], c["dtype"], c["n"]
+        srcs = [source(op, dtype, n, c["seed"], pe) for pe in range(npes)]
+        for pe in range(npes):
+            got = results[pe][str(c["id"])]
+            want = oracle.reduce_pe(op, dtype, srcs, pe)
+            ctx = f"rccl case {c['id']} {c['mode']} PE {pe}:"
+            fp = dtype in ("float", "double", "complexf", "complexd")
+            if not fp or (op in ("sum", "prod") and npes == 2):
+                assert_match(got, want, op, dtype, ctx=ctx)
+                continue
+            x = np.stack(srcs)
+            if op in ("min", "max"):
+                ok = ~np.isnan(x).any(axis=0)
+                assert (got[ok] == want[ok]).all(), f"{ctx} {op}/{dtype} differs from the reference's value"
+                continue
+            g, w, xs = (np.asarray(a).astype(np.complex128 if dtype.startswith("complex") else np.float64)
+                        for a in (got, want, x))
+            u = 2.0 ** -53 if dtype in ("double", "complexd") else 2.0 ** -24
+            tiny = np.finfo(np.float64 if dtype in ("double", "complexd") else np.float32).tiny
+            parts = (xs.real, xs.imag) if dtype.startswith("complex") else (xs,)
+            # subnormal inputs round relative to the subnormal grid, not to u
+            normal = np.logical_and.reduce([((np.abs(q) >= tiny) | (q == 0)).all(axis=0) for q in parts])
+            with np.errstate(all="ignore"):
+                fin = np.isfinite(xs).all(axis=0) & np.isfinite(g) & np.isfinite(w) & normal
+                mag = np.abs(xs).sum(axis=0) if op == "sum" else np.abs(np.prod(xs, axis=0))
+                bound = 2 * (npes - 1) * u * mag * (2 if dtype.startswith("complex") else 1)
+                err = np.abs(g - w)
+            bad = np.nonzero(fin & (err != 0) & ~(err <= bound))[0]  # a NaN bound: Inf x 0 among the inputs
+            assert len(bad) == 0, (f"{ctx} {op}/{dtype}: {len(bad)} elements above the stated bound; first at "
+                                   f"{bad[0]}: got {g[bad[0]]!r} want {w[bad[0]]!r} inputs {xs[:, bad[0]]!r}")
+
+
+@pytest.mark.parametrize("npes", [2, 3])
+def test_rccl_schedule_multi_rank(tmp_path, npes):
+    cases = make_cases(RCCL_PAIRS, 4099, [[0, 0, npes]], "dev", "rccl", 0)
+    cases += make_cases(RCCL_PAIRS, 1001, [[0, 0, npes]], "inplace", "rccl", 100)
+    cases += make_cases(RCCL_PAIRS[:4] + [("sum", "short")], 100000, [[0, 0, npes]], "host", "rccl", 200)
+    # pairs RCCL does not have, and a sub-set of the PEs: the P2P schedule
+    cases += make_cases([("xor", "int"), ("prod", "complexd")], 515, [[0, 0, npes]], "dev", "rccl", 300)
+    cases += make_cases([("sum", "double")], 515, [[0, 0, npes - 1]], "dev", "rccl", 400)
+    results = rccl_multi_rank(npes, cases, tmp_path)
+    check_rccl(results, cases[:-3], npes)
+    check(results, cases[-3:])
