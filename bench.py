@@ -325,6 +325,10 @@ def main():
     os.environ.setdefault("SHMEM_BARRIER_TIMEOUT", "120")
     shm = shmem_reduce.Shmem()
     shm.init()
+    # the init self-test found peer heap reads broken: the library runs the
+    # RCCL pairs through RCCL whatever is selected
+    rccl_fallback = shm.n_pes() > 1 and shm.lib.shmemx_get_reduce_algorithm() == shmem_reduce.ALGORITHMS["rccl"] \
+        and args.algorithm != "rccl"
     shm.set_algorithm(args.algorithm)
     me, npes = shm.my_pe(), shm.n_pes()
     if args.host:
@@ -421,7 +425,7 @@ def main():
     sys.stdout.flush()
     saved_stdout = os.dup(1)
     os.dup2(2, 1)
-    if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host:
+    if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host and not rccl_fallback:
         # non-blocking RCCL bring-up with a deadline; every PE must have it
         mine = np.array([1 if shm.lib.shmemx_rccl_init(60.0) == 0 else 0], dtype=np.int32)
         allok = np.zeros(1, dtype=np.int32)
@@ -450,7 +454,7 @@ def main():
         t_rccl_local = time.perf_counter() - tr0
         shm.barrier_all()
         shm.set_algorithm(args.algorithm)
-    if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host:
+    if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host and not rccl_fallback:
         steps(1)  # the target again from the default schedule (RCCL wrote it), for the check below
     sys.stdout.flush()
     os.dup2(saved_stdout, 1)
@@ -467,7 +471,7 @@ def main():
     if t_small is not None:
         t_small = max_over_pes(t_small)
     rccl = None
-    if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host and not rccl_ok:
+    if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host and not rccl_ok and not rccl_fallback:
         rccl = {"error": "RCCL did not come up (communicator within 60 s, or a probe allreduce) on every PE; "
                          "comparison skipped"}
     if t_rccl_local is not None:
@@ -493,10 +497,18 @@ def main():
         import oracle
         srcs = [synth(p, idx) for p in range(npes)]
         want = oracle.reduce_pe("sum", "double", srcs, me)
-        bad = int((got.view(np.uint64) != want.view(np.uint64)).sum())
-        bad = int(max_over_pes(bad))
-        check = "bit-exact vs the reference's per-PE order on every PE, %d samples each" % len(idx) if bad == 0 \
-            else "MISMATCH %d of %d samples (worst PE)" % (bad, len(idx))
+        if rccl_fallback:
+            # RCCL's order: within 2 (N-1) u sum|x_i| of the reference's result
+            bound = 2 * (npes - 1) * 2.0 ** -53 * np.abs(np.stack(srcs)).sum(axis=0)
+            bad = int(max_over_pes(int((np.abs(got - want) > bound).sum())))
+            check = ("RCCL fallback (peer heap reads failed the init self-test): within 2(N-1)u sum|x| of the "
+                     "reference's per-PE result on every PE, %d samples each" % len(idx) if bad == 0
+                     else "MISMATCH %d of %d samples beyond the FP bound (worst PE)" % (bad, len(idx)))
+        else:
+            bad = int((got.view(np.uint64) != want.view(np.uint64)).sum())
+            bad = int(max_over_pes(bad))
+            check = "bit-exact vs the reference's per-PE order on every PE, %d samples each" % len(idx) if bad == 0 \
+                else "MISMATCH %d of %d samples (worst PE)" % (bad, len(idx))
         del got_full
 
     kernels = None
@@ -526,6 +538,9 @@ def main():
         for name, op, dtype, es, gen in (
                 ("float_max", "max", "float", 4, lambda pe, i: synth(pe, i).astype(np.float32)),
                 ("longlong_and", "and", "longlong", 8, synth_bits)):
+            if rccl_fallback and op == "and":
+                ops[name] = {"skipped": "RCCL fallback (peer heap reads failed the init self-test): no bitwise and"}
+                continue
             no = ob // es
             shm.put(src, gen(me, np.arange(no, dtype=np.uint64)))
             oloop = shmem_reduce.bench_loop(name=name)
@@ -568,6 +583,8 @@ def main():
         shard = S // npes
         kname = (f"combine_orders_vec<sum,double,{npes}> (reduce-scatter leg: every PE's reference order)"
                  if npes <= 8 else f"mi355_combine_orders, {npes} sources (one left fold per member)")
+        if rccl_fallback:
+            kname = "ncclAllReduce (RCCL fallback: P2P self-test failed; the whole exchange, not one leg)"
         remote = (npes - 1) * shard
         hbm_bytes = 2 * npes * shard
         achieved = remote / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
@@ -643,7 +660,8 @@ def main():
             "data": "synthetic (splitmix64 full-mantissa doubles, device-resident symmetric heap)",
             "config": {"workload": f"shmem_double_sum_to_all, {npes} PE = {npes} GPU, {args.mib} MiB "
                                    f"{'host-memory (staged)' if args.host else 'device-resident'} array per PE", "nreduce": n, "bytes_per_pe": S,
-                       "algorithm": args.algorithm, "parallelism": f"pe{npes}"},
+                       "algorithm": "rccl (fallback: P2P self-test failed)" if rccl_fallback else args.algorithm,
+                       "parallelism": f"pe{npes}"},
             "per_pe_gib_s": round(S / t_step / GIB, 2),
             "roofline": roofline,
             "xgmi": xgmi,

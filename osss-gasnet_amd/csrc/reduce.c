@@ -687,7 +687,7 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
     const int same = dst_off == src_off;
     if (s->size > 1 && shmemi.p2p_broken)
         shmemi_fatal ("peer GPU memory reads failed the init self-test; only the RCCL pairs "
-                      "(sum/prod/min/max on short/int/long/float/double, complex sum) can run");
+                      "(sum/prod/min/max on short/int/long/float/double, complex sum) over all PEs can run");
     const int overlap = ranges_overlap (dst_off, src_off, nbytes);
 
     if (s->size == 1) {
@@ -941,8 +941,10 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
                       target == source ? "are the same buffer" : overlap ? "overlap, using temporary target"
                                                                           : "do not overlap");
     }
-    const int use_rccl = shmemi.algorithm == SHMEMX_REDUCE_RCCL && s.size == shmemi.npes && s.size > 1 &&
-                         shmemi_rccl_supported (op, dtype);
+    /* RCCL by request, or whenever the init self-test found peer heap reads
+     * broken (whatever the selected algorithm): the pairs RCCL has still run */
+    const int use_rccl = (shmemi.algorithm == SHMEMX_REDUCE_RCCL || shmemi.p2p_broken) && s.size == shmemi.npes &&
+                         s.size > 1 && shmemi_rccl_supported (op, dtype);
     if (use_rccl && kt != PK_HOST && ks != PK_HOST && !overlap) {
         SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: RCCL allreduce");
         shmemi_server_stop ();

@@ -499,3 +499,17 @@ def test_rccl_schedule_multi_rank(tmp_path, npes):
     results = rccl_multi_rank(npes, cases, tmp_path)
     check_rccl(results, cases[:-3], npes)
     check(results, cases[-3:])
+
+
+def test_peer_heap_mapping_failure_runs_rccl_pairs(tmp_path):
+    """One PE cannot map the peers' heaps (SHMEM_TEST_IPC_FAIL=heap on PE 1):
+    every PE agrees at init that the P2P schedules cannot run, and the pairs
+    RCCL has then go through RCCL whatever schedule is selected (here the
+    default) -- with RCCL's own order, as test_rccl_schedule_multi_rank."""
+    cases = make_cases(RCCL_PAIRS, 4099, [[0, 0, 3]], "dev", "auto", 0)
+    cases += make_cases(RCCL_PAIRS[:4], 100000, [[0, 0, 3]], "host", "auto", 100)
+    per_pe = {pe: {"NCCL_HOSTID": f"shmem-rccl-test-pe{pe}"} for pe in range(3)}
+    results = run_pes(3, cases, tmp_path, per_pe_env=per_pe,
+                      extra_env={"NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1", "SHMEM_TEST_IPC_FAIL": "heap",
+                                 "SHMEM_DEVICE_SCRATCH_SIZE": "3M"})
+    check_rccl(results, cases, 3)
