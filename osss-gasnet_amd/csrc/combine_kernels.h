@@ -36,8 +36,9 @@ struct Signal {
 
 // Publish recipe of MI355X_MICROARCH.md (inter-workgroup visibility, valid
 // form "sc1 payload + drained waves + flag"): the bulk stores are
-// write-through (`nt sc1`, st16), so once every wave has drained its stores
-// they are in memory for any agent; a block that also made plain stores (an
+// write-through (`nt sc1` st16 in the copy, `sc1` st16_fold in the folds), so
+// once every wave has drained its stores they are in memory for any agent; a
+// block that also made plain stores (an
 // element tail, an unaligned kernel) first writes its XCD's L2 back with an
 // agent-scope release. One lane per block counts the block in; the last
 // block resets the counter and stores the epoch to the host-coherent flag.
@@ -364,7 +365,8 @@ inline unsigned grid_for(uint64_t units_per_block_pass, uint64_t units, int bloc
 
 // Launch shape per source count, from tools/hbm_sweep.hip and
 // tools/fold_bench.py on MI355X (256 MiB per source, double sums,
-// non-temporal loads + `nt sc1` stores; GB/s counts (k+1) x 256 MiB;
+// non-temporal loads + `nt sc1` stores at the time; the folds store `sc1`
+// since round 2, see st16_fold; GB/s counts (k+1) x 256 MiB;
 // profiles/r01/hbm_sweep_v5.txt, fold_bench_k_sources.jsonl):
 //   k=2: 1 vector/lane,  2 blocks/CU     6.4 TB/s
 //   k=3: 2 vectors/lane, 1 block/CU      6.5 TB/s
