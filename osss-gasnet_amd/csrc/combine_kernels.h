@@ -214,37 +214,32 @@ __device__ __forceinline__ void orders_element(const OrdersParams &p, int64_t i)
 // across the branches), which halved the kernel's rate at 2-4 sources
 // (tools/orders_probe.hip; rocprofv3 160 vs 82 us at 4 x 64 MiB).
 // The software x87 sum/product: NSRC * (NSRC - 1) soft-float operations per
-// element do not unroll, and the sources held in a register array indexed by
-// the loop variables would live in scratch memory; instead each member's
-// fold re-reads the sources (hits in L2 after the first member), the member
-// whose output aliases its source (in place) last. (x87 min/max, a compare
-// and a select, keeps the register form: 210 vs 337 us at 8 x 32 MiB.)
+// element are too much code to unroll over the members, and a register array
+// indexed by a rolled loop's variable lives in scratch memory. So the NSRC
+// sources are loaded once into registers and only the member loop q stays
+// rolled: member q's operands -- its own source first, then the others in
+// member order -- are picked from the registers with compile-time indices
+// and masks (x80d::pick): the first operand is v[q], the j-th after it v[j]
+// for j < q and v[j + 1] otherwise. All loads precede every store, so an
+// output that aliases its source (in place) is safe. (Round 2 before this:
+// each member's fold re-read the sources from L2 one dependent load per
+// operation.)
 template <int OP, int NSRC, bool ALL>
 __device__ __forceinline__ void x80_orders_vector(const OrdersParams &p, uint64_t i) {
-    int last = -1;
+    x80 v[NSRC];
+#pragma unroll
+    for (int k = 0; k < NSRC; ++k) v[k] = ((const x80 *)p.src[k])[i];
 #pragma unroll 1
     for (int q = 0; q < NSRC; ++q) {
         if (!ALL && p.dst[q] == nullptr) continue;
-        if (p.dst[q] == p.src[q]) {
-            last = q;
-            continue;
-        }
-        x80 acc = ((const x80 *)p.src[q])[i];
-#pragma unroll 1
-        for (int k = 0; k < NSRC; ++k)
-            if (k != q) acc = apply<OP>(acc, ((const x80 *)p.src[k])[i]);
+        x80 acc = v[0];
+#pragma unroll
+        for (int k = 1; k < NSRC; ++k) acc = x80d::pick(q == k, v[k], acc);
+#pragma unroll
+        for (int j = 0; j + 1 < NSRC; ++j) acc = apply<OP>(acc, x80d::pick(j < q, v[j], v[j + 1]));
         Pack<x80> o;
         o.e[0] = acc;
         st16_fold((u32x4 *)p.dst[q] + i, o.v);
-    }
-    if (last >= 0) {
-        x80 acc = ((const x80 *)p.src[last])[i];
-#pragma unroll 1
-        for (int k = 0; k < NSRC; ++k)
-            if (k != last) acc = apply<OP>(acc, ((const x80 *)p.src[k])[i]);
-        Pack<x80> o;
-        o.e[0] = acc;
-        st16_fold((u32x4 *)p.dst[last] + i, o.v);
     }
 }
 
