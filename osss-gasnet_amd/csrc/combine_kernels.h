@@ -385,16 +385,25 @@ template <int NSRC, typename T> struct Shape {
 // same width. Complex types: one vector per lane (NSRC*(NSRC-1) complex
 // products per vector do not fit the registers of deeper unrolling; the
 // loads in flight come from more blocks instead).
-// min/max from 5 sources: two vectors per lane (the compare-select chains of
+// min/max at 8 sources: one vector per lane (the compare-select chains of
 // every member's fold hold more registers than the adds; at four vectors per
-// lane double min at 8 sources ran at 5.1 TB/s against 6.5 for the sum).
+// lane double min at 8 sources ran at 5.1 TB/s against 6.5 for the sum; float
+// max 86.2 -> 82.7 us at two -> one, profiles/r02/orders_vs_fold_alu_shapes.jsonl).
+// 3-4 sources of min/max or complex products: eight blocks per CU (alu4:
+// float max 95.2 -> 81.2 us, complex double product 102.7 -> 80.7 at 4 x 64 MiB).
 template <int OP, int NSRC, typename T> struct OrdersShape {
     static constexpr bool cplx = std::is_same<T, cplxf>::value || std::is_same<T, cplxd>::value;
     static constexpr bool sel = (OP == MI355_OP_MIN || OP == MI355_OP_MAX) && NSRC >= 5;
     using S = Shape<NSRC, T>;
-    static constexpr int unroll = cplx ? 1 : sel && S::unroll > 2 ? 2 : S::unroll;
-    static constexpr int blocks_per_cu = cplx ? (S::blocks_per_cu * S::unroll < 8 ? S::blocks_per_cu * S::unroll : 8)
-                                              : S::blocks_per_cu;
+    // 3-4 sources with compare-select chains or complex products: the sum's
+    // shape there (one block per CU) leaves too few waves to hide their ALU
+    // latency; eight blocks per CU
+    static constexpr bool alu4 = !S::alu_heavy && NSRC >= 3 && NSRC <= 4 &&
+                                 (OP == MI355_OP_MIN || OP == MI355_OP_MAX || (cplx && OP == MI355_OP_PROD));
+    static constexpr int unroll = cplx ? 1 : alu4 ? 2 : sel && S::unroll > 2 ? 1 : S::unroll;
+    static constexpr int blocks_per_cu = alu4 ? 8
+                                         : cplx ? (S::blocks_per_cu * S::unroll < 8 ? S::blocks_per_cu * S::unroll : 8)
+                                                : S::blocks_per_cu;
     static constexpr int policy = POL_NT_LOAD;
 };
 
