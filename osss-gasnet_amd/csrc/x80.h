@@ -365,19 +365,21 @@ __device__ __forceinline__ x80 mul(const x80 &a, const x80 &b) {
 }
 
 // a < b on the x87 (false when unordered: NaN or an unsupported encoding).
+// Branch-free: a value orders by sign, then by (exponent, significand) --
+// zero lowest (E = kEmin, m = 0; denormals share kEmin with the smallest
+// normals and order below them by their cleared integer bit), infinity
+// highest -- except that the two zeros are equal. (An early-return form
+// diverged per lane and ran the every-member max at 8 sources 3.8x slower
+// than the plain fold.)
 __device__ __forceinline__ bool less(const x80 &a, const x80 &b) {
-    if (unsupported(a) || unsupported(b) || is_nan(a) || is_nan(b)) return false;
-    const bool za = is_zero(a), zb = is_zero(b);
-    if (za && zb) return false;
+    const bool unordered = unsupported(a) | unsupported(b) | is_nan(a) | is_nan(b);
+    const bool both_zero = is_zero(a) & is_zero(b);
     const int sa = sign(a), sb = sign(b);
-    if (za) return sb == 0;  // 0 < b  iff b positive (non-zero)
-    if (zb) return sa == 1;  // a < 0  iff a negative
-    if (sa != sb) return sa == 1;
-    // same sign: compare magnitudes (inf has the largest exponent field)
     const int ea = is_inf(a) ? 0x10000 : exp_of(a), eb = is_inf(b) ? 0x10000 : exp_of(b);
-    const bool mag_lt = (ea < eb) || (ea == eb && a.m < b.m);
-    const bool mag_gt = (ea > eb) || (ea == eb && a.m > b.m);
-    return sa == 0 ? mag_lt : mag_gt;
+    const bool mag_lt = (ea < eb) | ((ea == eb) & (a.m < b.m));
+    const bool mag_gt = (ea > eb) | ((ea == eb) & (a.m > b.m));
+    const bool lt = sa != sb ? sa == 1 : (sa == 0 ? mag_lt : mag_gt);
+    return !unordered & !both_zero & lt;
 }
 
 }  // namespace x80d

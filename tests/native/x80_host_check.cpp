@@ -70,5 +70,50 @@ int main(int argc, char **argv) {
             }
         }
     printf("%ld pairs, %ld mismatches\n", n, bad);
-    return bad != 0;
+    // x80d::less against the host's x87 `<` (unordered -- NaN or an encoding
+    // the 387 refuses -- compares false), over every encoding class: zeros,
+    // denormals, pseudo-denormals, normals with near and far exponents and
+    // equal significands, infinities, quiet/signalling NaNs, unnormals,
+    // pseudo-infinities and pseudo-NaNs
+    auto any = [&](int e0) {
+        x80 r;
+        memset(&r, 0, sizeof r);
+        const int cls = (int)(g() % 11);
+        int e = e0;
+        uint64_t m = g() | (1ull << 63);
+        switch (cls) {
+        case 0: e = 0; m = 0; break;                                          // zero
+        case 1: e = 0; m = g() >> (1 + g() % 63); break;                      // denormal
+        case 2: e = 0; break;                                                 // pseudo-denormal
+        case 3: e = 0x7FFF; m = 1ull << 63; break;                            // infinity
+        case 4: e = 0x7FFF; m = (1ull << 63) | (g() >> 2) | 1; break;         // NaN
+        case 5: e = 1 + (int)(g() % 0x7FFE); m = g() >> 1; break;             // unnormal
+        case 6: e = 0x7FFF; m = g() >> 1; break;                              // pseudo-inf / pseudo-NaN
+        default: break;                                                       // normal near e0
+        }
+        r.m = m;
+        r.se = (uint16_t)(((g() & 1) << 15) | e);
+        return r;
+    };
+    long nc = 0, badc = 0;
+    for (long i = 0; i < per; ++i) {
+        const int e0 = 1 + (int)(g() % 0x7FFE);
+        x80 a = any(e0), b = any(e0 + (int)(g() % 3) - 1 < 1 ? 1 : e0);
+        if (g() % 4 == 0) b = a;                                             // equal values
+        if (g() % 8 == 0) { b = a; b.se ^= 0x8000; }                          // opposite signs, +-0
+        long double la, lb;
+        memset(&la, 0, sizeof la);
+        memset(&lb, 0, sizeof lb);
+        memcpy(&la, &a, 10);
+        memcpy(&lb, &b, 10);
+        const bool want = la < lb, want2 = lb < la;
+        ++nc;
+        if (x80d::less(a, b) != want || x80d::less(b, a) != want2) {
+            if (badc < 5) printf("less mismatch: fields %04x %016llx vs %04x %016llx\n", a.se,
+                                 (unsigned long long)a.m, b.se, (unsigned long long)b.m);
+            ++badc;
+        }
+    }
+    printf("compare: %ld pairs, %ld mismatches\n", nc, badc);
+    return bad != 0 || badc != 0;
 }
