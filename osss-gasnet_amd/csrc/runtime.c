@@ -642,6 +642,7 @@ static void interconnect_selftest (void)
                              "using the RCCL schedule\n");
         shmemi.algorithm = SHMEMX_REDUCE_RCCL;
         shmemi.p2p_broken = 1;
+        shmemi.fused_max = 0; /* its kernels read the peers' heaps too: every PE takes the same path */
     }
     shmemi_barrier_set (0, 1, np);
 }

@@ -513,3 +513,27 @@ def test_peer_heap_mapping_failure_runs_rccl_pairs(tmp_path):
                       extra_env={"NCCL_SOCKET_IFNAME": "lo", "NCCL_IB_DISABLE": "1", "SHMEM_TEST_IPC_FAIL": "heap",
                                  "SHMEM_DEVICE_SCRATCH_SIZE": "3M"})
     check_rccl(results, cases, 3)
+
+
+def test_peer_heap_mapping_failure_other_pairs_abort_cleanly(tmp_path):
+    """With the peers' heaps unmapped (SHMEM_TEST_IPC_FAIL=heap on PE 1), a
+    pair RCCL does not have (int xor), small or large, device or host arrays,
+    must end the job with the library's message on every PE -- no PE may take
+    a kernel path that reads a peer's heap."""
+    for n, mode in ((16, "dev"), (16, "host"), (300000, "dev")):
+        env = dict(os.environ, SHMEM_NPES="3", SHMEM_JOB_ID=uuid.uuid4().hex[:12], SHMEM_DEVICE="0",
+                   SHMEM_DEVICE_HEAP_SIZE="32M", SHMEM_DEVICE_SCRATCH_SIZE="3M", SHMEM_BARRIER_TIMEOUT="60",
+                   SHMEM_TEST_IPC_FAIL="heap", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+        code = ("import sys,os; sys.path[:0]=[%r,%r]\n" % (HERE, os.path.join(os.path.dirname(HERE), "osss-gasnet_amd")) +
+                "import numpy as np, shmem_reduce\nshm=shmem_reduce.Shmem(); shm.init()\n"
+                f"n={n}\n"
+                + ("d=shm.malloc_device(8*n); s=d\n" if mode == "dev" else
+                   "a=np.ones(n,dtype=np.int32); d=a.ctypes.data; s=d\n") +
+                "shm.to_all('xor','int',d,s,n,0,0,3)\nprint('CALL-RETURNED', flush=True)\nshm.finalize()\n")
+        procs = [subprocess.Popen([sys.executable, "-c", code],
+                                  env=dict(env, SHMEM_PE=str(pe), NCCL_HOSTID=f"shmem-rccl-test-pe{pe}"),
+                                  stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True) for pe in range(3)]
+        outs = [p.communicate(timeout=120)[0] for p in procs]
+        for p, out in zip(procs, outs):
+            assert p.returncode != 0 and "CALL-RETURNED" not in out, out[-2000:]
+        assert any("only the RCCL pairs" in o for o in outs), outs
