@@ -210,66 +210,47 @@ __device__ __forceinline__ bool fast_operand(const x80 &a) {
 // errors in the general path's results on gfx950 -- test_longdouble_
 // random_encodings -- so the choice is per wave.)
 __device__ __forceinline__ bool add_fast(const x80 &a, const x80 &b, x80 &r) {
-    if (fast_operand(a) && fast_operand(b)) {
-        const int ea = efield(a), eb = efield(b);
-        const bool a_big = (ea > eb) || (ea == eb && a.m >= b.m);
-        const int EA = a_big ? ea : eb, d = a_big ? ea - eb : eb - ea;
-        const uint64_t MA = a_big ? a.m : b.m, MB = a_big ? b.m : a.m;
-        const int sa = sign(a), sb = sign(b);  // scalars: no struct select
-        const int sA = a_big ? sa : sb, sB = a_big ? sb : sa;
-        if (d <= 64) {
-            // B aligned under A in 128 bits, exactly: A = MA:0, B = Bh:Bl
-            const uint64_t Bh = d == 64 ? 0 : MB >> d;
-            const uint64_t Bl = d == 0 ? 0 : (d == 64 ? MB : MB << (64 - d));
-            if (sA == sB) {
-                uint64_t hi = MA + Bh, lo = Bl;
-                int E = EA;
-                bool sticky = false;
-                if (hi < MA) {  // carry out: shift the 129-bit sum right by one
-                    sticky = (lo & 1) != 0;
-                    lo = (lo >> 1) | (hi << 63);
-                    hi = (hi >> 1) | 0x8000000000000000ull;
-                    ++E;
-                }
-                if (round_up(hi, lo, sticky)) {
-                    if (++hi == 0) {
-                        hi = 0x8000000000000000ull;
-                        ++E;
-                    }
-                }
-                r = make(sA, E, hi, a);
-                return true;
-            }
-            // A - B >= 0, exact in 128 bits
-            uint64_t lo = 0 - Bl;
-            uint64_t hi = MA - Bh - (Bl != 0 ? 1 : 0);
-            if (hi == 0 && lo == 0) {  // exact cancellation: +0
-                r = make(0, 0, 0, a);
-                return true;
-            }
-            const int L = hi ? 127 - __builtin_clzll(hi) : 63 - __builtin_clzll(lo);
-            const int shift = 127 - L;  // normalize the leading bit to bit 127
-            if (EA - shift >= 1) {
-                if (shift >= 64) {
-                    hi = lo << (shift - 64);
-                    lo = 0;
-                } else if (shift > 0) {
-                    hi = (hi << shift) | (lo >> (64 - shift));
-                    lo <<= shift;
-                }
-                int E = EA - shift;
-                if (round_up(hi, lo, false)) {
-                    if (++hi == 0) {
-                        hi = 0x8000000000000000ull;
-                        ++E;
-                    }
-                }
-                r = make(sA, E, hi, a);
-                return true;
-            }
-        }
-    }
-    return false;
+    // One straight-line path for effective addition and subtraction (every
+    // choice a select; a branchy form diverged per lane on the operands'
+    // signs, carries and cancellations, and the every-member fold ran both
+    // sides of every branch): B aligned under A = MA:0 in 128 bits, exactly;
+    // A + B, or A + (~B + 1) when the signs differ (A >= B, so no borrow out);
+    // then one normalization: right by one on a carry out of the addition,
+    // left by the leading zeros after a subtraction; one rounding.
+    const int ea = efield(a), eb = efield(b);
+    const bool a_big = (ea > eb) | ((ea == eb) & (a.m >= b.m));
+    const int EA = a_big ? ea : eb;
+    const int d = a_big ? ea - eb : eb - ea;
+    const uint64_t MA = a_big ? a.m : b.m, MB = a_big ? b.m : a.m;
+    const int sa = sign(a), sb = sign(b);
+    const int sA = a_big ? sa : sb;
+    const bool sub = sa != sb;
+    const int dd = d < 64 ? d : 64;
+    const uint64_t Bh = dd == 64 ? 0 : MB >> (dd & 63);
+    const uint64_t Bl = dd == 0 ? 0 : MB << ((64 - dd) & 63);  // dd = 64: MB << 0 = MB
+    const uint64_t lo = sub ? 0 - Bl : Bl;
+    const uint64_t hi = MA + (sub ? ~Bh + (Bl == 0 ? 1 : 0) : Bh);
+    const bool carry = !sub & (hi < MA);
+    const bool zero = sub & (hi == 0) & (lo == 0);  // exact cancellation: +0
+    // leading zeros of hi:lo after a subtraction (0 after an addition)
+    const int lz = !sub ? 0 : hi != 0 ? __builtin_clzll(hi) : 64 + (lo != 0 ? __builtin_clzll(lo) : 63);
+    const int l = lz & 63;
+    // hi:lo << lz (lz in [0, 127]) or >> 1 (carry: the 129th bit comes back in at the top)
+    const uint64_t sh_hi = lz >= 64 ? lo << l : l == 0 ? hi : (hi << l) | (lo >> (64 - l));
+    const uint64_t sh_lo = lz >= 64 ? 0 : lo << l;
+    const uint64_t nhi = carry ? (hi >> 1) | 0x8000000000000000ull : sh_hi;
+    const uint64_t nlo = carry ? (lo >> 1) | (hi << 63) : sh_lo;
+    const bool sticky = carry & ((lo & 1) != 0);
+    int E = EA + (carry ? 1 : 0) - lz;
+    const bool up = round_up(nhi, nlo, sticky);
+    uint64_t m = nhi + (up ? 1 : 0);
+    const bool wrap = up & (m == 0);
+    m = wrap ? 0x8000000000000000ull : m;
+    E += wrap ? 1 : 0;
+    const int fa = fast_operand(a), fb = fast_operand(b);  // ints: evaluated without branches
+    const bool ok = fa & fb & (d <= 64) & (zero | (E >= 1));
+    r = zero ? make(0, 0, 0, a) : make(sA, E, m, a);
+    return ok;
 }
 
 __device__ __forceinline__ x80 add_general(const x80 &a, const x80 &b) {
@@ -372,8 +353,10 @@ __device__ __forceinline__ x80 mul(const x80 &a, const x80 &b) {
 // diverged per lane and ran the every-member max at 8 sources 3.8x slower
 // than the plain fold.)
 __device__ __forceinline__ bool less(const x80 &a, const x80 &b) {
-    const bool unordered = unsupported(a) | unsupported(b) | is_nan(a) | is_nan(b);
-    const bool both_zero = is_zero(a) & is_zero(b);
+    const int ua = unsupported(a), ub = unsupported(b), na = is_nan(a), nb = is_nan(b);  // ints: no branches
+    const int za = is_zero(a), zb = is_zero(b);
+    const bool unordered = ua | ub | na | nb;
+    const bool both_zero = za & zb;
     const int sa = sign(a), sb = sign(b);
     const int ea = is_inf(a) ? 0x10000 : exp_of(a), eb = is_inf(b) ? 0x10000 : exp_of(b);
     const bool mag_lt = (ea < eb) | ((ea == eb) & (a.m < b.m));
