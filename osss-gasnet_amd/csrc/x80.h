@@ -300,28 +300,22 @@ __device__ __forceinline__ x80 add(const x80 &a, const x80 &b) {
 }
 
 __device__ __forceinline__ bool mul_fast(const x80 &a, const x80 &b, x80 &r) {
-    if (fast_operand(a) && fast_operand(b)) {
-        // biased exponent of the product with its leading bit at 127 (or 126)
-        const int E = efield(a) + efield(b) - kBias + 1;
-        if (E >= 2 && E <= kFastMax) {
-            uint64_t hi = __umul64hi(a.m, b.m), lo = a.m * b.m;
-            int Ef = E;
-            if ((hi >> 63) == 0) {  // leading bit at 126: one left shift
-                hi = (hi << 1) | (lo >> 63);
-                lo <<= 1;
-                --Ef;
-            }
-            if (round_up(hi, lo, false)) {
-                if (++hi == 0) {
-                    hi = 0x8000000000000000ull;
-                    ++Ef;
-                }
-            }
-            r = make(sign(a) ^ sign(b), Ef, hi, a);
-            return true;
-        }
-    }
-    return false;
+    // straight-line like add_fast: the 128-bit product's leading bit is at
+    // 127 or 126 (one conditional left shift, as a select), one rounding
+    const int E = efield(a) + efield(b) - kBias + 1;  // biased exponent, leading bit at 127
+    const uint64_t hi = __umul64hi(a.m, b.m), lo = a.m * b.m;
+    const bool low = (hi >> 63) == 0;  // leading bit at 126
+    const uint64_t nhi = low ? (hi << 1) | (lo >> 63) : hi;
+    const uint64_t nlo = low ? lo << 1 : lo;
+    int Ef = E - (low ? 1 : 0);
+    const bool up = round_up(nhi, nlo, false);
+    uint64_t m = nhi + (up ? 1 : 0);
+    const bool wrap = up & (m == 0);
+    m = wrap ? 0x8000000000000000ull : m;
+    Ef += wrap ? 1 : 0;
+    const int fa = fast_operand(a), fb = fast_operand(b);  // ints: evaluated without branches
+    r = make(sign(a) ^ sign(b), Ef, m, a);
+    return fa & fb & (E >= 2) & (E <= kFastMax);
 }
 
 __device__ __forceinline__ x80 mul_general(const x80 &a, const x80 &b) {
