@@ -269,6 +269,29 @@ __global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
         for (int u = 0; u < UNROLL; ++u) {
             const uint64_t i = base + (uint64_t)u * kBlock;
             if (i >= nvec) continue;
+            if constexpr ((OP == MI355_OP_MIN || OP == MI355_OP_MAX) && std::is_floating_point<T>::value) {
+                // When no operand is a NaN or a zero, `a < b ? a : b` picks the
+                // same bits in every order (equal non-zero numbers have one
+                // encoding): one fold serves every member. The members'
+                // orders only differ on NaNs and +-0 ties (reduce-op.c:138-150),
+                // which take the per-member folds below (wave-uniform choice).
+                bool plain = true;
+#pragma unroll
+                for (int k = 0; k < NSRC; ++k)
+#pragma unroll
+                    for (int e = 0; e < V; ++e) plain &= (x[u][k].e[e] == x[u][k].e[e]) & (x[u][k].e[e] != T(0));
+                if (__all(plain)) {
+                    Pack<T> m = x[u][0];
+#pragma unroll
+                    for (int k = 1; k < NSRC; ++k)
+#pragma unroll
+                        for (int e = 0; e < V; ++e) m.e[e] = apply<OP>(m.e[e], x[u][k].e[e]);
+#pragma unroll
+                    for (int q = 0; q < NSRC; ++q)
+                        if (ALL || p.dst[q] != nullptr) st16_fold((u32x4 *)p.dst[q] + i, m.v);
+                    continue;
+                }
+            }
 #pragma unroll
             for (int q = 0; q < NSRC; ++q) {
                 if (!ALL && p.dst[q] == nullptr) continue;
