@@ -125,6 +125,39 @@ def test_combine_orders_any_number_of_sources(shm, dev, op, dtype, nsrc):
         dev.free()
 
 
+@pytest.mark.parametrize("op,dtype", [("min", "double"), ("max", "double"), ("min", "float"), ("max", "float")])
+@pytest.mark.parametrize("nsrc", [2, 3, 5, 8])
+def test_combine_orders_minmax_sparse_specials(shm, dev, op, dtype, nsrc):
+    """The every-member min/max folds one value for every member on vectors
+    whose operands hold no NaN and no zero, and runs the per-member chains
+    only where they do: 200 000 full-mantissa elements per source with a few
+    NaNs, +-0 and equal-value ties planted, so that one launch mixes both
+    paths; every member's output against the reference's own order."""
+    rng = np.random.default_rng(7 * nsrc + len(op))
+    n = 200000
+    t = oracle.NP[dtype]
+    srcs = []
+    for k in range(nsrc):
+        x = ((rng.uniform(-1, 1, n) + 2.0 ** -30) * np.exp2(rng.integers(-4, 4, n))).astype(t)
+        x[x == 0] = t(1.5)
+        pos = rng.integers(0, n, 24)
+        x[pos[:8]] = t(np.nan)
+        x[pos[8:16]] = t(0.0)
+        x[pos[16:20]] = t(-0.0)
+        x[pos[20:]] = t(0.25)  # ties with the other sources' planted 0.25
+        srcs.append(x)
+    common = rng.integers(0, n, 16)  # the same positions in every source: +0/-0 and NaN across members
+    for k, x in enumerate(srcs):
+        x[common[:8]] = t(0.0) if k % 2 else t(-0.0)
+        x[common[8:12]] = t(np.nan) if k == nsrc - 1 else t(0.5)
+        x[common[12:]] = t(0.25)
+    want = oracle.reduce_all(op, dtype, srcs)
+    got = gpu_orders(shm, dev, op, dtype, srcs)
+    for q, g in got.items():
+        assert_match(g, want[q], op, dtype, ctx=f"nsrc={nsrc} member {q}")
+    dev.free()
+
+
 @pytest.mark.parametrize("op,dtype", [("sum", "double"), ("xor", "int"), ("max", "float"), ("prod", "complexf"),
                                       ("min", "longdouble"), ("sum", "short")])
 @pytest.mark.parametrize("nsrc", [1, 2, 5, 8, 9, 12, 17])
