@@ -229,14 +229,27 @@ __device__ __forceinline__ void x80_orders_vector(const OrdersParams &p, uint64_
     x80 v[NSRC];
 #pragma unroll
     for (int k = 0; k < NSRC; ++k) v[k] = ((const x80 *)p.src[k])[i];
+    // Member 1's order (s1, s0, s2, ...) gives member 0's value (s0, s1, s2,
+    // ...): x87 + and * commute, NaN and signed-zero rules included, and the
+    // rest of the two chains is the same -- one chain fewer per element.
+    x80 first = v[0];
+    bool have_first = false;
 #pragma unroll 1
     for (int q = 0; q < NSRC; ++q) {
         if (!ALL && p.dst[q] == nullptr) continue;
         x80 acc = v[0];
+        if (q == 1 && have_first) {
+            acc = first;
+        } else {
 #pragma unroll
-        for (int k = 1; k < NSRC; ++k) acc = x80d::pick(q == k, v[k], acc);
+            for (int k = 1; k < NSRC; ++k) acc = x80d::pick(q == k, v[k], acc);
 #pragma unroll
-        for (int j = 0; j + 1 < NSRC; ++j) acc = apply<OP>(acc, x80d::pick(j < q, v[j], v[j + 1]));
+            for (int j = 0; j + 1 < NSRC; ++j) acc = apply<OP>(acc, x80d::pick(j < q, v[j], v[j + 1]));
+            if (q == 0) {
+                first = acc;
+                have_first = true;
+            }
+        }
         Pack<x80> o;
         o.e[0] = acc;
         st16_fold((u32x4 *)p.dst[q] + i, o.v);
