@@ -256,6 +256,17 @@ __device__ __forceinline__ void x80_orders_vector(const OrdersParams &p, uint64_
     }
 }
 
+// Operand classes on which min/max selects are order-independent (above).
+template <typename T>
+__device__ __forceinline__ bool single_fold_ok(const T &v) {
+    if constexpr (std::is_same<T, x80>::value) {
+        const int e = v.se & 0x7FFF;
+        return (e >= 1) & (e <= 0x7FFE) & ((v.m >> 63) != 0);
+    } else {
+        return (v == v) & (v != T(0));
+    }
+}
+
 template <int OP, typename T, int NSRC, int UNROLL, int POL, bool ALL>
 __global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
     constexpr int V = 16 / sizeof(T);
@@ -282,17 +293,20 @@ __global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
         for (int u = 0; u < UNROLL; ++u) {
             const uint64_t i = base + (uint64_t)u * kBlock;
             if (i >= nvec) continue;
-            if constexpr ((OP == MI355_OP_MIN || OP == MI355_OP_MAX) && std::is_floating_point<T>::value) {
-                // When no operand is a NaN or a zero, `a < b ? a : b` picks the
-                // same bits in every order (equal non-zero numbers have one
-                // encoding): one fold serves every member. The members'
-                // orders only differ on NaNs and +-0 ties (reduce-op.c:138-150),
-                // which take the per-member folds below (wave-uniform choice).
+            if constexpr ((OP == MI355_OP_MIN || OP == MI355_OP_MAX) &&
+                          (std::is_floating_point<T>::value || std::is_same<T, x80>::value)) {
+                // When no operand is a NaN or a zero (long double: every operand
+                // a normal number), `a < b ? a : b` picks the same value bits in
+                // every order (equal numbers of these classes have one
+                // encoding): one fold serves every member. The members' orders
+                // only differ on NaNs, +-0 ties and (x87) equal values with
+                // different encodings (reduce-op.c:138-150), which take the
+                // per-member folds below (wave-uniform choice).
                 bool plain = true;
 #pragma unroll
                 for (int k = 0; k < NSRC; ++k)
 #pragma unroll
-                    for (int e = 0; e < V; ++e) plain &= (x[u][k].e[e] == x[u][k].e[e]) & (x[u][k].e[e] != T(0));
+                    for (int e = 0; e < V; ++e) plain &= single_fold_ok(x[u][k].e[e]);
                 if (__all(plain)) {
                     Pack<T> m = x[u][0];
 #pragma unroll

@@ -158,6 +158,47 @@ def test_combine_orders_minmax_sparse_specials(shm, dev, op, dtype, nsrc):
     dev.free()
 
 
+def x87(sign, efield, mant):
+    """One long double from its fields (x86 80-bit format in 16 bytes)."""
+    b = np.zeros(16, dtype=np.uint8)
+    b[:8] = np.frombuffer(np.uint64(mant).tobytes(), dtype=np.uint8)
+    b[8:10] = np.frombuffer(np.uint16((sign << 15) | efield).tobytes(), dtype=np.uint8)
+    return b.view(np.longdouble)[0]
+
+
+@pytest.mark.parametrize("op", ["min", "max"])
+@pytest.mark.parametrize("nsrc", [2, 5, 8])
+def test_combine_orders_x87_minmax_sparse_specials(shm, dev, op, nsrc):
+    """Long double min/max: one fold serves every member only where every
+    operand is a normal number; sparse NaNs, +-0, denormals and -- the x87's
+    own case -- a pseudo-denormal beside the normal of the same value (equal
+    numbers, different encodings: the select keeps the first) must take the
+    per-member chains."""
+    rng = np.random.default_rng(11 * nsrc + len(op))
+    n = 100000
+    t = np.longdouble
+    tie_normal, tie_pseudo = x87(0, 1, 0x8000000000000123), x87(0, 0, 0x8000000000000123)
+    assert tie_normal == tie_pseudo
+    srcs = []
+    for k in range(nsrc):
+        x = ((rng.uniform(-1, 1, n) + 2.0 ** -30) * np.exp2(rng.integers(-4, 4, n))).astype(t)
+        pos = rng.integers(0, n, 16)
+        x[pos[:4]] = t(np.nan)
+        x[pos[4:8]] = t(0.0)
+        x[pos[8:12]] = np.finfo(t).tiny / 8
+        x[pos[12:]] = tie_pseudo
+        srcs.append(x)
+    common = rng.integers(0, n, 12)
+    for k, x in enumerate(srcs):
+        x[common[:6]] = tie_pseudo if k % 2 else tie_normal  # equal values, two encodings, across members
+        x[common[6:]] = t(-0.0) if k % 2 else t(0.0)
+    want = oracle.reduce_all(op, "longdouble", srcs)
+    got = gpu_orders(shm, dev, op, "longdouble", srcs)
+    for q, g in got.items():
+        assert_match(g, want[q], op, "longdouble", ctx=f"nsrc={nsrc} member {q}")
+    dev.free()
+
+
 @pytest.mark.parametrize("op,dtype", [("sum", "double"), ("xor", "int"), ("max", "float"), ("prod", "complexf"),
                                       ("min", "longdouble"), ("sum", "short")])
 @pytest.mark.parametrize("nsrc", [1, 2, 5, 8, 9, 12, 17])
