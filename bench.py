@@ -10,10 +10,14 @@ the timed region starts). K steps are bracketed by shmem_barrier_all + a
 device synchronize on both sides; the time is the max over PEs.
 
 value = N * 256 MiB / t_step / 2^30 (whole job); per-PE S/t_step is also
-printed. roofline: the dominant kernel's algorithmic bytes per launch / its
-average duration from HIP events recorded by the library on its own stream.
-cpu_baseline: the reference algorithm restated in C (oracle/liboracle.so),
-1 PE on 1 host core, timed on a bounded sample before the GPU is touched.
+printed. roofline: the dominant kernel of the schedule the library actually
+ran (shmemx_last_call_info: its name as rocprofv3 prints it, its sources,
+outputs and bytes), its algorithmic bytes per launch / its average duration
+from HIP events recorded by the library on its own stream.
+cpu_baseline: the reference algorithm restated in C (oracle/liboracle.so) as
+max(2, N) PE processes, one pinned host core each, on a bounded sample, run
+by rank 0 before any rank's PE joins the job (the other ranks wait in the
+bootstrap), at every N.
 """
 import argparse
 import json
@@ -94,7 +98,10 @@ def cpu_baseline(S, n_gpus, budget_s):
 
     t, reps, cpus = timed("sum", "double", npes, n, 0.4 * budget_s)
     t1, reps1, cpus1 = timed("sum", "double", 1, n, 0.2 * budget_s)
-    t8, reps8, cpus8 = timed("sum", "double", 8, n, 0.25 * budget_s)
+    if npes == 8:   # the headline's own N: the same run
+        t8, reps8, cpus8 = t, reps, cpus
+    else:
+        t8, reps8, cpus8 = timed("sum", "double", 8, n, 0.25 * budget_s)
     tc, repsc, cpusc = timed("sum", "int", 2, 1024, 0.05 * budget_s)
     t5, reps5, cpus5 = timed("sum", "double", 8, 8192, 0.1 * budget_s)
     try:
@@ -161,6 +168,73 @@ def fused_same_gpu(npes, calls, persistent=False):
                      "kernel left resident (mi355_fused_server, fed through a host-coherent mailbox), no launch; "
                      "kernel_avg_us covers only the launched calls")
     return d
+
+
+def traffic_for(rec, key, host):
+    """HBM bytes per launch from the PMC passes committed in
+    profiles/pmc_traffic.json (tools/pmc_traffic.py: FETCH_SIZE x 2 +
+    WRITE_SIZE, gfx950 correction), put into rec["traffic"] only when the
+    entry was profiled from kernel sources with the hash of this tree
+    (shmem_reduce.kernel_source_hash); otherwise traffic stays null and the
+    returned note says why."""
+    if host:
+        return "host-staged run: no PMC profile"
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        tr = json.load(open(path)).get(key)
+    except (OSError, ValueError):
+        tr = None
+    if not tr:
+        return f"no PMC profile for {key} in profiles/pmc_traffic.json"
+    want = shmem_reduce.kernel_source_hash()
+    if tr.get("kernel_src_sha") != want:
+        return (f"profiles/pmc_traffic.json[{key}] was taken from kernel sources {tr.get('kernel_src_sha')}, this "
+                f"tree is {want}: not reported")
+    rec["traffic"] = tr["hbm_bytes_per_launch"]
+    rec["traffic_source"] = tr["source"]
+    return f"PMC passes of this tree's kernels (kernel sources {want})"
+
+
+def persistent_child(rank, world, calls):
+    """N > 1: BASELINE config 5's 64 KiB calls with the opt-in persistent
+    server (SHMEM_PERSISTENT=1), run by one child PE process per rank on the
+    rank's own GPU -- a job of its own (tools/fused_bench.py), started before
+    this process touches the GPU -- so that the opt-in path, never run across
+    GPUs before the driver's 8-GPU node, cannot take the headline line with
+    it: a failure or a hang there becomes an "error" entry. Rank 0's child
+    prints the record (per-call time max over PEs, bit-exact check of every
+    PE's result, calls served vs servers launched)."""
+    import subprocess
+    job = "ps%s-%d" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
+    env = dict(os.environ, SHMEM_PE=str(rank), SHMEM_NPES=str(world), SHMEM_JOB_ID=job,
+               SHMEM_DEVICE=os.environ.get("LOCAL_RANK", str(rank)), SHMEM_PERSISTENT="1",
+               SHMEM_BARRIER_TIMEOUT="60")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+        env.pop(k, None)
+    script = os.path.join(ROOT, "tools", "fused_bench.py")
+    p = subprocess.Popen([sys.executable, script, str(calls), str(64 << 10)], env=env, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    try:
+        out, err = p.communicate(timeout=240)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        p.communicate()
+        return {"error": "timed out after 240 s"}
+    if p.returncode != 0:
+        return {"error": f"PE {rank} rc {p.returncode}: {err[-400:]}"}
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    if rank != 0:
+        return None
+    if not lines:
+        return {"error": "no result line from PE 0"}
+    d = json.loads(lines[-1])
+    leg = d["legs"].get(str(64 << 10), {})
+    leg.update({"opt_in": True, "same_gpu": d.get("same_gpu"), "npes": d.get("npes"),
+                "note": "opt-in persistent server (SHMEM_PERSISTENT=1, shmemx_set_persistent): after the first two "
+                        "calls a resident fused kernel takes each call from a host-coherent mailbox, no launch; "
+                        "measured in a child job of one PE per GPU (tools/fused_bench.py), kernel_avg_us covers "
+                        "only the launched calls"})
+    return leg
 
 
 # ---------------------------------------------------------------------------
@@ -307,9 +381,15 @@ def main():
     S = args.mib << 20
     n = S // 8
 
-    # CPU baseline first, before this process initialises the GPU
+    # N > 1: the opt-in persistent server's small calls, in a child job
+    # (every rank at once, before any of them touches the GPU)
+    small_p_child = None
+    if world > 1 and not args.no_small and not args.host:
+        small_p_child = persistent_child(rank, world, 4096)
+    # CPU baseline, before this process initialises the GPU; at N > 1 the
+    # other ranks wait for rank 0 in the bootstrap (SHMEM_BARRIER_TIMEOUT)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(S, args.gpus, args.cpu_seconds)
     # the fused kernel on 2 PE processes sharing this GPU (children; this
     # process has not touched the GPU yet)
@@ -331,6 +411,16 @@ def main():
         and args.algorithm != "rccl"
     shm.set_algorithm(args.algorithm)
     me, npes = shm.my_pe(), shm.n_pes()
+    # the init-time coherence test of peer-heap reads (runtime.c): on the
+    # driver's 8-GPU node it proves or refutes the acquire protocol the P2P
+    # schedules rely on
+    coherence = None
+    if npes > 1:
+        ran, passed, stale = shm.coherence_selftest()
+        coherence = {"ran": ran, "passed": passed, "stale_without_acquire": stale,
+                     "note": "every PE read each peer's marker through its L2, the peer rewrote it (write-through), "
+                             "and the re-read after mi355_acquire_system must see the new value; "
+                             "stale_without_acquire: a re-read without the acquire returned the old value"}
     if args.host:
         import ctypes
         src, dst = shm.malloc(S), shm.malloc(S)
@@ -373,6 +463,8 @@ def main():
     nk, k_total_ms, k_avg_ms = shm.kernel_timing_stats()
     nag, _, ag_avg_ms = shm.kernel_timing_phase_stats(1)   # N > 1: the all-gather copy
     shm.kernel_timing(False)
+    # what the library ran for these calls: schedule, dominant kernel, bytes
+    info = shm.last_call_info()
 
     # the many-small-bucket regime (BASELINE config 5 shape: 64 KiB per call)
     small_n, small_calls = 8192, 0 if args.no_small else 4096   # BASELINE config 5: 4096 x 64 KiB
@@ -385,6 +477,7 @@ def main():
         steps(small_calls, small_n)
         shm.sync()
         t_small = (time.perf_counter() - ts0) / small_calls
+        small_info = shm.last_call_info()
         shm.barrier_all()
 
     # N = 1: the same calls with the opt-in persistent server (shmemx.h
@@ -514,18 +607,11 @@ def main():
     kernels = None
     if npes == 1 and not args.no_kernels and not args.host:
         kernels = kernel_legs(shm, args.kernel_reps, not args.no_check)
-        traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-        if os.path.exists(traffic_file):
-            try:
-                pmc = json.load(open(traffic_file))
-            except ValueError:
-                pmc = {}
-            for name, leg in kernels.items():
-                tr = pmc.get(f"kernel_{name}") if isinstance(leg, dict) else None
-                if tr:
-                    leg["traffic"] = tr["hbm_bytes_per_launch"]
-                    leg["traffic_over_alg"] = round(tr["hbm_bytes_per_launch"] / leg["alg_bytes_per_launch"], 4)
-                    leg["traffic_source"] = tr["source"]
+        for name, leg in kernels.items():
+            if isinstance(leg, dict):
+                leg["traffic_note"] = traffic_for(leg, f"kernel_{name}", False)
+                if leg.get("traffic"):
+                    leg["traffic_over_alg"] = round(leg["traffic"] / leg["alg_bytes_per_launch"], 4)
 
     # BASELINE config 4 (op coverage): shmem_float_max_to_all and
     # shmem_longlong_and_to_all on 64 MiB per PE, timed like the headline
@@ -566,52 +652,52 @@ def main():
         ops["note"] = ("BASELINE config 4 (op coverage): shmem_float_max_to_all and shmem_longlong_and_to_all, "
                        "64 MiB per PE, GiB/s reduced whole job; longlong words with bits 1 at p = 7/8")
 
-    # dominant kernel and its algorithmic bytes per launch
+    # dominant kernel and its algorithmic bytes per launch, from the schedule
+    # the library reports for the timed calls (shmemx_last_call_info)
+    launches = max(1, info["launches"])
+    alg_bytes = info["alg_bytes"]
+    kname = info["kernel"] or "ncclAllReduce (RCCL's kernels)"
+    kt_s = k_avg_ms * 1e-3 * launches   # the dominant kernel's time per call
+    sched = {"schedule": info["schedule"], "ordered": bool(info["ordered"]), "sources": info["sources"],
+             "outputs": info["outputs"], "peer_sources": info["peer_sources"], "launches_per_call": launches,
+             "bytes_per_buffer": info["bytes_per_buffer"]}
     if npes == 1:
-        kname = "copy_segments<4> (identity fold, PE_size=1)"
-        alg_bytes = 2 * S
-        achieved = alg_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
+        achieved = alg_bytes / kt_s / 1e9 if k_avg_ms > 0 else 0.0
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
-                    "kernel": kname, "alg_bytes_per_launch": alg_bytes, "kernel_avg_us": round(k_avg_ms * 1e3, 2),
-                    "launches_timed": nk, "ms_per_step_with_events": round(t_local_ev / args.steps * 1e3, 4)}
+                    "kernel": kname, "alg_bytes_per_launch": alg_bytes // launches,
+                    "kernel_avg_us": round(k_avg_ms * 1e3, 2),
+                    "launches_timed": nk, "ms_per_step_with_events": round(t_local_ev / args.steps * 1e3, 4),
+                    "call": sched}
     else:
         # N > 1: the reduce-scatter fold reads N-1 of its N shard sources from
         # peers over xGMI, so its bound is the links into this GPU: achieved =
-        # those remote bytes / the fold's duration against (N-1) x 153 GB/s.
-        # Its local-HBM view (all source and output bytes) is kept in `hbm`.
-        shard = S // npes
-        kname = (f"combine_orders_vec<sum,double,{npes}> (reduce-scatter leg: every PE's reference order)"
-                 if npes <= 8 else f"mi355_combine_orders, {npes} sources (one left fold per member)")
+        # those peer bytes / the fold's duration against (N-1) x 153 GB/s. Its
+        # local-HBM view (every source and output byte) is kept in `hbm`.
+        remote = info["peer_bytes"]
+        achieved = remote / kt_s / 1e9 if k_avg_ms > 0 else 0.0
+        peak = (npes - 1) * XGMI_LINK_GBS
+        hbm_gbs = alg_bytes / kt_s / 1e9 if k_avg_ms > 0 else 0.0
         if rccl_fallback:
             kname = "ncclAllReduce (RCCL fallback: P2P self-test failed; the whole exchange, not one leg)"
-        remote = (npes - 1) * shard
-        hbm_bytes = 2 * npes * shard
-        achieved = remote / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
-        peak = (npes - 1) * XGMI_LINK_GBS
-        hbm_gbs = hbm_bytes / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else 0.0
         roofline = {"bound": "xgmi", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
                     "frac": round(achieved / peak, 4), "traffic": None, "kernel": kname,
-                    "alg_bytes_per_launch": remote, "kernel_avg_us": round(k_avg_ms * 1e3, 2),
+                    "alg_bytes_per_launch": remote // launches, "kernel_avg_us": round(k_avg_ms * 1e3, 2),
                     "launches_timed": nk, "ms_per_step_with_events": round(t_local_ev / args.steps * 1e3, 4),
+                    "call": sched,
                     "peak_note": "(N-1) links x 153 GB/s into this GPU (SURVEY 8d); if 153.6 GB/s counts both "
                                  "directions the one-way bound is half: see xgmi.frac_one_direction",
-                    "hbm": {"bytes_per_launch": hbm_bytes, "achieved": round(hbm_gbs, 1), "peak": HBM_PEAK_GBS,
-                            "frac": round(hbm_gbs / HBM_PEAK_GBS, 4),
-                            "note": "the same fold counted as local HBM traffic: N shard sources read + N "
-                                    "outputs (this PE's target shard and N-1 versions) written"}}
+                    "hbm": {"bytes_per_launch": alg_bytes // launches, "achieved": round(hbm_gbs, 1),
+                            "peak": HBM_PEAK_GBS, "frac": round(hbm_gbs / HBM_PEAK_GBS, 4),
+                            "note": "the same fold counted as local HBM traffic: its %d shard sources read + %d "
+                                    "output(s) written (%s)" % (info["sources"], info["outputs"],
+                                                                 "this PE's target shard and the other members' "
+                                                                 "versions" if info["ordered"] else
+                                                                 "this PE's target shard")}}
         if not distinct_gpus:
             roofline["note"] = ("the PEs share ONE GPU (test layout): the 'remote' reads are this GPU's own HBM, "
                                 "so achieved/frac here are not xGMI figures")
-    traffic_file = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(traffic_file) and not args.host:
-        try:
-            tr = json.load(open(traffic_file)).get(f"n{npes}_{args.mib}mib")
-            if tr:
-                roofline["traffic"] = tr["hbm_bytes_per_launch"]
-                roofline["traffic_source"] = tr["source"]
-        except (ValueError, KeyError):
-            pass
+    roofline["traffic_note"] = traffic_for(roofline, f"n{npes}_{args.mib}mib", args.host)
 
     # N > 1: bus bandwidth of the reduce-scatter + all-gather exchange against
     # the full-mesh xGMI bound: each PE moves 2(N-1)/N * S
@@ -620,7 +706,7 @@ def main():
     if npes > 1:
         busbw = 2.0 * (npes - 1) / npes * S / t_step / 1e9
         bound = (npes - 1) * XGMI_LINK_GBS
-        rs_remote = (npes - 1) / npes * S / (k_avg_ms * 1e-3) / 1e9 if k_avg_ms > 0 else None
+        rs_remote = info["peer_bytes"] / (k_avg_ms * 1e-3 * launches) / 1e9 if k_avg_ms > 0 else None
         bound_dir = (npes - 1) * XGMI_LINK_DIR_GBS
         xgmi = {"busbw_GB_s_per_pe": round(busbw, 1), "mesh_bound_GB_s_per_pe": bound,
                 "frac": round(busbw / bound, 4),
@@ -669,13 +755,15 @@ def main():
             "cpu_baseline": cpu,
             "small_call": None if t_small is None else
             {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small * 1e6, 2), "calls": small_calls,
+             "schedule": small_info["schedule"], "kernel": small_info["kernel"],
              "note": "BASELINE config 5 shape: 4096 back-to-back 64 KiB shmem_double_sum_to_all calls, max over PEs"},
-            "small_call_persistent": None if t_small_p is None else
+            "small_call_persistent": small_p_child if world > 1 else None if t_small_p is None else
             {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small_p * 1e6, 2), "calls": small_calls,
-             "served": served1 - served0, "servers_launched": launched1 - launched0,
+             "served": served1 - served0, "servers_launched": launched1 - launched0, "opt_in": True,
              "note": "the same calls with the opt-in persistent server (SHMEM_PERSISTENT): a resident kernel takes each "
                      "call from a host-coherent mailbox instead of a launch; the call ends when the host sees its "
                      "completion flag, as launched ones do (the timed region ends at the last call's return)"},
+            "coherence_selftest": coherence,
             "check": check,
             "op_coverage": ops,
             "kernels": kernels,

@@ -100,6 +100,13 @@ void mi355_time_next_launch (void *start_event, void *stop_event);
  * stream. Pass NULL flag to cancel. */
 void mi355_signal_next_launch (unsigned *count, unsigned *flag, unsigned epoch);
 
+/* Host stub of the kernel this layer launched last from the calling thread
+ * (NULL before the first launch), and its demangled name as rocprofv3
+ * prints it ("void mi355k::copy_segments<4, 1>(mi355k::SegParams<1>)") --
+ * the runtime records which kernel carried a call (shmemx_last_call_info). */
+const void *mi355_last_kernel (void);
+int mi355_kernel_name (const void *kernel, char *buf, size_t len);
+
 /* Launch a one-block kernel whose only job is to carry the armed signal:
  * the host learns that everything queued on `stream` before it is done. */
 int mi355_signal_launch (void *stream);
@@ -258,6 +265,11 @@ int mi355_device_barrier (const MI355FusedArgs *args, void *stream);
  * into out[] (device memory). n <= 1024. */
 int mi355_poke (unsigned long long *const *dst, int n, unsigned long long value, void *stream);
 int mi355_peek (const unsigned long long *const *src, int n, unsigned long long *out, void *stream);
+/* The coherence check: nblocks blocks (<= 256, dealt over the XCDs) each load
+ * the n words with plain, L2-cached loads -- as the folds read peers' buffers
+ * -- into out[b * n + i]. */
+int mi355_peek_cached (const unsigned long long *const *src, int n, unsigned long long *out, int nblocks,
+                       void *stream);
 
 /* Shard i of nshards for n elements of elem_size bytes: the P2P schedule's
  * partition (contiguous, shard starts 256-byte aligned, trailing shards may

@@ -66,6 +66,27 @@ enum shmemx_reduce_order {
 };
 int shmemx_set_reduce_order (int order); /* returns the previous one */
 int shmemx_get_reduce_order (void);
+/* The schedule and the result order are per-PE settings, but they decide
+ * what the members do together: every member of an active set must use the
+ * same algorithm, order and SHMEM_DEVICE_ORDER_SIZE when it calls, or one PE
+ * may take the fused path while another takes the multi-launch one (a hang),
+ * or gather version areas its peers never wrote. Init aborts when the PEs'
+ * environment settings differ; SHMEM_DEBUG=1 also checks every call (below).
+ * With 2 PEs, floating-point sum and product are computed once (a + b is
+ * b + a) and both PEs get the same bits; where both operands are NaNs with
+ * different payloads, the reference's PE 1 would keep its own operand's
+ * payload (x86 SSE returns the first operand's), so the payload -- not the
+ * NaN-ness -- may differ from the reference's there (tests/_compare.py
+ * compares NaN with NaN whatever the payload).
+ *
+ * SHMEM_DEBUG=1: every *_to_all call (host API and stream-ordered) first
+ * exchanges its arguments with the other members of its active set -- op,
+ * type, nreduce, PE_start, logPE_stride, PE_size, the target/source memory
+ * kinds and their symmetric-heap offsets, the algorithm and order settings --
+ * and aborts every PE with a message naming the first field that differs
+ * (the reference's debug build checks init and symmetry,
+ * src/reduce/reduce-op.c:395-398, src/utils/utils.h:74-129). Costs two host
+ * barriers per call. */
 
 /* Persistent fused server (opt-in; env SHMEM_PERSISTENT=1 sets it at init,
  * SHMEM_PERSISTENT_IDLE_US = how long it stays without a call, default 1000):
@@ -106,6 +127,38 @@ void shmemx_kernel_timing_stats (long *launches, double *total_ms, double *avg_m
 /* the same for one phase: 0 = each call's dominant kernel (the fold, or a 1-PE call's copy; what
  * shmemx_kernel_timing_stats reports), 1 = the all-gather copy of the P2P schedule */
 void shmemx_kernel_timing_phase_stats (int phase, long *launches, double *total_ms, double *avg_ms);
+
+/* What this PE's last *_to_all call ran (host API and stream-ordered calls):
+ * the schedule, the dominant kernel -- the reduce-scatter fold of the P2P
+ * schedules, the copy of a 1-PE call, the fused kernel -- and the bytes that
+ * kernel streams, computed from the schedule the library chose, not assumed
+ * by the caller. Returns 0, or -1 before the first call. */
+typedef struct shmemx_call_info {
+    char schedule[64];      /* "p2p", "p2p-rounds", "fused-oneshot", "fused-twoshot", "persistent",
+                             * "identity", "exact", "rccl", "staged", "barrier-only" */
+    char kernel[256];       /* demangled dominant kernel, as rocprofv3 names it ("" for rccl) */
+    int ordered;            /* 1: every member's reference order (version areas written) */
+    int sources, outputs;   /* buffers the dominant kernel reads / writes */
+    int peer_sources;       /* of its sources, how many lie in other PEs' heaps */
+    int launches;           /* dominant-kernel launches in the call (rounds) */
+    unsigned long long bytes_per_buffer;  /* bytes of each source and output, per launch */
+    unsigned long long alg_bytes;         /* (sources + outputs) x bytes_per_buffer, + the fused
+                                           * two-shot's gather (2 (N-1) shards) */
+    unsigned long long peer_bytes;        /* of alg_bytes, read from other PEs' heaps */
+} shmemx_call_info;
+int shmemx_last_call_info (shmemx_call_info *info);
+
+/* The init-time coherence self-test of peer-heap reads (PE_size > 1 jobs):
+ * every PE reads every peer's marker through its L2 (a cached load), each
+ * peer rewrites its marker with a write-through store, and after a barrier
+ * the reader re-reads it once without and once after mi355_acquire_system.
+ * ran: the test ran (peer heaps mapped); passed: the re-read after the
+ * acquire saw every new value on every PE (else the job runs the RCCL
+ * schedule, like a failed mapping); stale_without_acquire: some PE's re-read
+ * WITHOUT the acquire returned an old value (evidence that the acquire the
+ * P2P schedules queue before reading peers' buffers is needed). All three
+ * are the job's (OR / AND over the PEs). */
+void shmemx_coherence_selftest (int *ran, int *passed, int *stale_without_acquire);
 
 /* Bring up the RCCL communicator of the whole job (what SHMEM_REDUCE_ALGORITHM=rccl uses) without
  * aborting when RCCL cannot come up within timeout_s seconds: 0 = ready on this PE, -1 = not. Every PE

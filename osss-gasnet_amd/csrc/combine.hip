@@ -23,9 +23,12 @@
 //   complex prod  the C99 Annex G algorithm of libgcc __muldc3/__mulsc3, which
 //                 is what gcc emits for `a * b` on double/float complex
 //   long double   x87 80-bit extended arithmetic in software (x80.h)
+#include <cxxabi.h>
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
 #include <type_traits>
 
 #include "combine_kernels.h"
@@ -357,6 +360,26 @@ extern "C" void mi355i_take_launch_events(void **start_event, void **stop_event)
     *start_event = t_ev_start;
     *stop_event = t_ev_stop;
     t_ev_start = t_ev_stop = nullptr;
+}
+
+// For fused.hip: its launches count as this layer's last kernel too.
+extern "C" void mi355i_note_launch(const void *kernel) { t_last_kernel = kernel; }
+
+extern "C" const void *mi355_last_kernel(void) { return t_last_kernel; }
+
+// The kernel's demangled name, as rocprofv3 prints it ("void
+// mi355k::copy_segments<4, 1>(mi355k::SegParams<1>)"). Not on the hot path:
+// the runtime keeps the stub pointer per call and resolves it on request.
+extern "C" int mi355_kernel_name(const void *kernel, char *buf, size_t len) {
+    if (kernel == nullptr || buf == nullptr || len == 0) return MI355_E_INVAL;
+    const char *mangled = hipKernelNameRefByPtr(kernel, nullptr);
+    (void)hipGetLastError();
+    if (mangled == nullptr) return MI355_E_INVAL;
+    int status = 0;
+    char *dem = abi::__cxa_demangle(mangled, nullptr, nullptr, &status);
+    snprintf(buf, len, "%s", status == 0 && dem != nullptr ? dem : mangled);
+    free(dem);
+    return 0;
 }
 
 // short <-> int32 for the RCCL schedule (RCCL has no 16-bit integer type):

@@ -16,8 +16,6 @@ namespace mi355k {
 
 using namespace mi355;
 
-using namespace mi355;
-
 constexpr int kBlock = 256;
 constexpr int kMaxSrc = 8;
 
@@ -356,6 +354,8 @@ inline int g_cus[64];
 // mi355_signal_next_launch), consumed by it
 inline thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
 inline thread_local Signal t_sig = {nullptr, nullptr, 0};
+// host stub of the kernel this layer launched last (mi355_last_kernel)
+inline thread_local const void *t_last_kernel = nullptr;
 
 // A host-visible word the host can also write: an armed signal that no kernel
 // will carry (nothing to launch) is fired right here, in stream order.
@@ -374,6 +374,7 @@ int launch(K kernel, dim3 grid, hipStream_t st, P p, bool final = true) {
         p.sig = t_sig;
         t_sig = Signal{nullptr, nullptr, 0};
     }
+    t_last_kernel = (const void *)kernel;
     if (t_ev_start != nullptr || t_ev_stop != nullptr) {
         hipExtLaunchKernelGGL(kernel, grid, dim3(kBlock), 0, st, t_ev_start, t_ev_stop, 0, p);
         t_ev_start = t_ev_stop = nullptr;

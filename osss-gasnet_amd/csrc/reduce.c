@@ -52,6 +52,58 @@ struct aset {
 
 static int aset_pe (const struct aset *s, int i) { return s->start + i * s->stride; }
 
+/* What the call ran (shmemx_last_call_info): called right after the
+ * dominant kernel's launch, so the combine layer's last kernel is it.
+ * sources/outputs buffers of `bytes` each; extra_alg / extra_peer: bytes
+ * beyond those (the fused two-shot's gather). Rounds add launches. */
+static const char *cur_schedule = "none";
+
+static void note_call (int ordered, int sources, int outputs, int peer_sources, unsigned long long bytes,
+                       unsigned long long extra_alg, unsigned long long extra_peer, const void *kernel)
+{
+    shmemi.last.valid = 1;
+    shmemi.last.schedule = cur_schedule;
+    shmemi.last.kernel = kernel;
+    shmemi.last.ordered = ordered;
+    shmemi.last.sources = sources;
+    shmemi.last.outputs = outputs;
+    shmemi.last.peer_sources = peer_sources;
+    shmemi.last.bytes_per_buffer = bytes;
+    shmemi.last.alg_bytes = (unsigned long long) (sources + outputs) * bytes + extra_alg;
+    shmemi.last.peer_bytes = (unsigned long long) peer_sources * bytes + extra_peer;
+    shmemi.last.launches++;
+}
+
+static void begin_call (const char *schedule)
+{
+    cur_schedule = schedule;
+    shmemi.last.valid = 1;
+    shmemi.last.schedule = schedule;
+    shmemi.last.kernel = NULL;
+    shmemi.last.launches = 0;
+    shmemi.last.ordered = shmemi.last.sources = shmemi.last.outputs = shmemi.last.peer_sources = 0;
+    shmemi.last.bytes_per_buffer = shmemi.last.alg_bytes = shmemi.last.peer_bytes = 0;
+}
+
+int shmemx_last_call_info (shmemx_call_info *info)
+{
+    if (info == NULL || !shmemi.last.valid)
+        return -1;
+    memset (info, 0, sizeof *info);
+    snprintf (info->schedule, sizeof info->schedule, "%s", shmemi.last.schedule);
+    if (shmemi.last.kernel != NULL && mi355_kernel_name (shmemi.last.kernel, info->kernel, sizeof info->kernel) != 0)
+        info->kernel[0] = '\0';
+    info->ordered = shmemi.last.ordered;
+    info->sources = shmemi.last.sources;
+    info->outputs = shmemi.last.outputs;
+    info->peer_sources = shmemi.last.peer_sources;
+    info->launches = shmemi.last.launches;
+    info->bytes_per_buffer = shmemi.last.bytes_per_buffer;
+    info->alg_bytes = shmemi.last.alg_bytes;
+    info->peer_bytes = shmemi.last.peer_bytes;
+    return 0;
+}
+
 /* Launch the fold and wait for its completion signal (the kernel's last
  * block writes a host-coherent word; ~4 us sooner than a stream sync). */
 static void combine_wait (int op, int dtype, void *dst, const void *const *srcs, int nsrc, size_t n, int timed)
@@ -269,6 +321,9 @@ static int fold_shard (int op, int dtype, size_t es, size_t dst_off, size_t src_
             dsts[q] = q == s->me ? dst : shmemi_peer_ptr (shmemi.mype, ver_off (chan, s->me, q, slot, dst_off));
         rc = mi355_combine_orders (op, dtype, dsts, spp, s->size, hi - lo, st);
     }
+    if (rc == 0)
+        note_call (ordered, s->size, ordered ? s->size : 1, s->size - 1, (unsigned long long) ((hi - lo) * es), 0, 0,
+                   mi355_last_kernel ());
     if (spp != sp)
         free (spp);
     return rc;
@@ -397,6 +452,7 @@ static void p2p_any (int op, int dtype, size_t es, size_t dst_off, size_t src_of
     SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: P2P shards, %s barriers, %s (%zu elements, %d members%s)",
                   dev ? "device" : "host", ordered ? "every member's reference order" : "PE_start order", n, s->size,
                   ordered && n > round ? ", several rounds" : "");
+    begin_call (dev ? (n > round ? "p2p-rounds" : "p2p") : (n > round ? "p2p-host-rounds" : "p2p-host"));
     size_t b = 0;
     do {
         const size_t cn = n - b < round ? n - b : round;
@@ -433,6 +489,26 @@ static void fused_order (MI355FusedArgs *a, const struct aset *s, int chan)
             a->ver[i] = shmemi_peer_ptr (aset_pe (s, i), shmemi.order_off + (size_t) chan * shmemi.order_chunk);
 }
 
+/* The fused kernel's bytes: one-shot = every member's whole source read
+ * (N - 1 of them from peers), one output; two-shot = the shard of every
+ * member folded into 1 (or, ordered, N) outputs, then the other N - 1 shards
+ * gathered from peers and written here. A one-member "fused" call is the
+ * persistent server's identity copy. */
+static void note_fused (int size, int ordered, int oneshot, size_t n, size_t es, const void *kernel)
+{
+    if (size == 1) {
+        note_call (0, 1, 1, 0, (unsigned long long) (n * es), 0, 0, kernel);
+        return;
+    }
+    if (oneshot) {
+        note_call (ordered, size, 1, size - 1, (unsigned long long) (n * es), 0, 0, kernel);
+        return;
+    }
+    const unsigned long long shard = (unsigned long long) (shard_chunk (n, es, size) * es);
+    note_call (ordered, size, ordered ? size : 1, size - 1, shard, 2ull * (unsigned long long) (size - 1) * shard,
+               (unsigned long long) (size - 1) * shard, kernel);
+}
+
 /* ---------------------------------------------------------------------- */
 /* persistent fused server (opt-in: SHMEM_PERSISTENT=1, shmemx_set_persistent) */
 /* ---------------------------------------------------------------------- */
@@ -451,7 +527,8 @@ static void fused_order (MI355FusedArgs *a, const struct aset *s, int chan)
 static int server_matches (int op, int dtype, const struct aset *s)
 {
     return shmemi.srv.running && shmemi.srv.op == op && shmemi.srv.dtype == dtype && shmemi.srv.start == s->start &&
-           shmemi.srv.stride == s->stride && shmemi.srv.size == s->size;
+           shmemi.srv.stride == s->stride && shmemi.srv.size == s->size &&
+           shmemi.srv.ordered == ordered_pair (op, dtype, s->size);
 }
 
 /* The server has left (EXITED): later servers start past its last seq. */
@@ -572,6 +649,8 @@ static void server_start (int op, int dtype, size_t es, size_t n, int oneshot, c
     shmemi.srv.start = s->start;
     shmemi.srv.stride = s->stride;
     shmemi.srv.size = s->size;
+    shmemi.srv.ordered = a.ordered;
+    shmemi.srv.kernel = mi355_last_kernel ();
     shmemi.srv.grid_elems = n;
     ++shmemi.srv.launched;
     SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "persistent fused server started (%d members, sized for %zu elements)",
@@ -591,15 +670,18 @@ static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t sr
     const double t_call = servable ? shmemi_now () : 0.0;
     if (servable && server_matches (op, dtype, s) && n <= 2 * shmemi.srv.grid_elems) {
         SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: persistent fused server (%zu elements, %d members)", n, s->size);
-        if (server_call (dst_off, src_off, n, shard_chunk (n, es, s->size),
-                         n * es <= shmemi.oneshot_max && dst_off != src_off)) {
+        const int oneshot = n * es <= shmemi.oneshot_max && dst_off != src_off;
+        if (server_call (dst_off, src_off, n, shard_chunk (n, es, s->size), oneshot)) {
             shmemi.srv.last_end = shmemi_now ();
+            begin_call ("persistent");
+            note_fused (s->size, shmemi.srv.ordered, oneshot, n, es, shmemi.srv.kernel);
             return;
         }
     }
     shmemi_server_stop (); /* a different call: the launched grid must fit */
     if (s->size == 1) {
         SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: 1-PE identity, one copy of %zu bytes", n * es);
+        begin_call ("identity");
         copy_local (dst_off, src_off, n * es, 1);
     } else {
         SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: fused one-launch P2P, %s, %s (%zu elements, %d members)%s",
@@ -636,6 +718,8 @@ static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t sr
         if (rc != 0)
             shmemi_fatal ("fused reduction launch failed (op %d, dtype %d, %d PEs, %zu elements): %d", op, dtype,
                           s->size, n, rc);
+        begin_call (a.oneshot ? "fused-oneshot" : "fused-twoshot");
+        note_fused (s->size, a.ordered, a.oneshot, n, es, mi355_last_kernel ());
         if (shmemi_wait_flag (a.epoch) != a.epoch)
             shmemi_fatal ("fused reduction timed out waiting for the other PEs of the active set");
     }
@@ -661,6 +745,8 @@ static void exact_into (int op, int dtype, size_t dst_off, size_t src_off, size_
         if (i != s->me)
             sp[k++] = shmemi_peer_ptr (aset_pe (s, i), src_off);
     combine_wait (op, dtype, shmemi_peer_ptr (shmemi.mype, dst_off), sp, s->size, n, 1);
+    note_call (1, s->size, 1, s->size - 1, (unsigned long long) (n * mi355_dtype_size (dtype)), 0, 0,
+               mi355_last_kernel ());
     free (sp);
 }
 
@@ -671,6 +757,8 @@ static void copy_local (size_t dst_off, size_t src_off, size_t nbytes, int timed
     const void *sv = shmemi_peer_ptr (shmemi.mype, src_off);
     size_t nb = nbytes;
     copy_wait (&d, &sv, &nb, 1, timed ? 0 : -1);
+    if (timed)
+        note_call (0, 1, 1, 0, (unsigned long long) nbytes, 0, 0, mi355_last_kernel ());
 }
 
 /* Reduce n elements at symmetric offsets. Handles aliasing like the
@@ -694,6 +782,7 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
         /* a one-PE fold is the identity: target = source (reduce-op.c:226-229) */
         if (same) {
             SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: 1-PE identity in place, nothing to move");
+            begin_call ("identity");
             return;
         }
         if (!overlap) {
@@ -702,6 +791,7 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
                 return;
             }
             SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: 1-PE identity, one copy of %zu bytes", nbytes);
+            begin_call ("identity");
             copy_local (dst_off, src_off, nbytes, 1);
             return;
         }
@@ -713,6 +803,7 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
         return;
     } else if (exact && !overlap) {
         SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: EXACT reference order, host barriers");
+        begin_call ("exact");
         host_order ();
         shmemi_barrier_set (s->start, s->stride, s->size);
         exact_into (op, dtype, dst_off, src_off, n, s);
@@ -728,6 +819,8 @@ static void reduce_symmetric (int op, int dtype, size_t es, size_t dst_off, size
     const int down = dst_off > src_off;
     SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: overlapping target, %zu chunk(s) through scratch, %s", nchunks,
                   down ? "top down" : "bottom up");
+    if (s->size == 1 || exact)
+        begin_call (exact ? "exact" : "identity");
     for (size_t c = 0; c < nchunks; ++c) {
         const size_t idx = down ? nchunks - 1 - c : c;
         const size_t b = idx * per;
@@ -871,10 +964,12 @@ static int local_direct (int op, int dtype, void *target, const void *source, si
             return 0;
         SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: 1-PE identity, one copy kernel source -> target (%zu bytes)",
                       nbytes);
+        begin_call ("identity");
         if (target != source) {
             void *d = ht;
             size_t nb = nbytes;
             copy_wait (&d, &hs, &nb, 1, -1);
+            note_call (0, 1, 1, 0, (unsigned long long) nbytes, 0, 0, mi355_last_kernel ());
         }
         return 1;
     }
@@ -886,6 +981,37 @@ static int local_direct (int op, int dtype, void *target, const void *source, si
         return 0;
     fused_range (op, dtype, es, b_off, a_off, n, s, hs, ht);
     return 1;
+}
+
+/* SHMEM_DEBUG=1: the members compare their arguments before anything else
+ * of the call happens (runtime.c, shmemi_debug_exchange). */
+static void debug_check (const char *fn, int op, int dtype, const void *target, const void *source, int nreduce,
+                         int PE_start, int logPE_stride, int PE_size)
+{
+    if (PE_size < 2)
+        return;
+    struct shmemi_dbg_rec r;
+    memset (&r, 0, sizeof r);
+    r.op = op;
+    r.dtype = dtype;
+    r.nreduce = nreduce;
+    r.pe_start = PE_start;
+    r.log_stride = logPE_stride;
+    r.pe_size = PE_size;
+    r.tkind = r.skind = -1;
+    if (nreduce > 0) {
+        const size_t nbytes = (size_t) nreduce * mi355_dtype_size (dtype);
+        r.tkind = ptr_kind (target, nbytes);
+        r.skind = ptr_kind (source, nbytes);
+        if (r.tkind == PK_DEV_SYM)
+            r.toff = shmemi_heap_offset (target);
+        if (r.skind == PK_DEV_SYM)
+            r.soff = shmemi_heap_offset (source);
+    }
+    r.algorithm = shmemi.algorithm;
+    r.order = shmemi.order;
+    snprintf (r.fn, sizeof r.fn, "%s", fn);
+    shmemi_debug_exchange (&r, PE_start, 1 << logPE_stride, PE_size);
 }
 
 static void reduce_impl (int op, int dtype, const char *fn, void *target, const void *source,
@@ -912,7 +1038,10 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
 
     const size_t es = mi355_dtype_size (dtype);
     const size_t n = (size_t) nreduce;
+    if (shmemi.debug)
+        debug_check (fn, op, dtype, target, source, nreduce, PE_start, logPE_stride, PE_size);
     if (n == 0) {
+        begin_call ("barrier-only");
         /* both barriers of reduce-op.c:230,266 still run */
         shmemi_barrier_set (s.start, s.stride, s.size);
         shmemi_barrier_set (s.start, s.stride, s.size);
@@ -950,6 +1079,10 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
         shmemi_server_stop ();
         if (shmemi_rccl_allreduce (op, dtype, source, target, n) != 0)
             shmemi_fatal ("%s: ncclAllReduce failed", fn);
+        /* RCCL's own kernels: bytes as a full-mesh exchange would move them */
+        begin_call ("rccl");
+        note_call (0, 1, 1, 0, (unsigned long long) nbytes, 0,
+                   2ull * (unsigned long long) (s.size - 1) * nbytes / (unsigned long long) s.size, NULL);
         return;
     }
     if (kt == PK_DEV_SYM && ks == PK_DEV_SYM) {
@@ -960,7 +1093,9 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
     if (!use_rccl && local_direct (op, dtype, target, source, n, overlap, kt, ks, &s))
         return;
     SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "staged through the scratch buffers (%s)", use_rccl ? "RCCL" : "P2P");
+    begin_call ("staged");
     staged (op, dtype, fn, target, source, n, &s, ks, kt, use_rccl);
+    shmemi.last.schedule = "staged"; /* the kernel fields: the last chunk's reduction */
 }
 
 /* ---------------------------------------------------------------------- */
@@ -1056,14 +1191,19 @@ static void reduce_on_stream (int op, int dtype, const char *fn, void *target, c
         shmemi_fatal ("%s: target and source must lie in the device symmetric heap (shmemx_malloc_device)", fn);
     if (n > 0 && target != source && ranges_overlap ((size_t) target, (size_t) source, nbytes))
         shmemi_fatal ("%s: target and source overlap without being equal", fn);
+    if (shmemi.debug)
+        debug_check (fn, op, dtype, target, source, nreduce, PE_start, logPE_stride, PE_size);
 
     if (n == 0) {
+        begin_call ("barrier-only");
         stream_barrier (fn, &s, st);
     } else if (s.size == 1) {
+        begin_call ("stream-identity");
         if (target != source) {
             void *d = target;
             const void *sv = source;
             stream_copy (fn, &d, &sv, &nbytes, 1, st);
+            note_call (0, 1, 1, 0, (unsigned long long) nbytes, 0, 0, mi355_last_kernel ());
         }
     } else {
         const size_t dst_off = shmemi_heap_offset (target), src_off = shmemi_heap_offset (source);
@@ -1088,11 +1228,14 @@ static void reduce_on_stream (int op, int dtype, const char *fn, void *target, c
             const int rc = mi355_fused_allreduce (&a, st);
             if (rc != 0)
                 shmemi_fatal ("%s: fused reduction launch failed: %d", fn, rc);
+            begin_call (a.oneshot ? "stream-fused-oneshot" : "stream-fused-twoshot");
+            note_fused (s.size, a.ordered, a.oneshot, n, es, mi355_last_kernel ());
         } else {
             void *dsts[MI355_FUSED_MAX_MEMBERS];
             const void *sp[MI355_FUSED_MAX_MEMBERS];
             size_t nb[MI355_FUSED_MAX_MEMBERS];
             const size_t round = ordered ? ordered_round_elems (es, s.size) : n;
+            begin_call (n > round ? "stream-p2p-rounds" : "stream-p2p");
             for (size_t b = 0; b < n; b += round) {
                 const size_t cn = n - b < round ? n - b : round;
                 const size_t d0 = dst_off + b * es, s0 = src_off + b * es;

@@ -26,6 +26,7 @@
 #include <fcntl.h>
 #include <sched.h>
 #include <stdarg.h>
+#include <stddef.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -51,7 +52,7 @@ struct shmemi_hostblk {
 };
 
 #define SEG_MAGIC 0x4d49333535534d45ull /* "MI355SME" */
-#define SEG_VERSION 3
+#define SEG_VERSION 4
 
 static double now_s (void)
 {
@@ -215,7 +216,7 @@ static void bootstrap_attach (void)
     const size_t info = round_up (sizeof (struct shmemi_pe_info) * (size_t) npes, 4096);
     const size_t row = round_up ((size_t) npes, 8);
     const size_t flags = round_up (row * (size_t) npes * sizeof (uint64_t), 4096);
-    const size_t total = hdr + info + flags;
+    const size_t total = hdr + info + 2 * flags; /* barrier counts, SHMEM_DEBUG check counts */
     seg_name (shmemi.seg_name, sizeof shmemi.seg_name);
 
     const double deadline = now_s () + shmemi.barrier_timeout;
@@ -236,6 +237,7 @@ static void bootstrap_attach (void)
         shmemi.seg->info_off = hdr;
         shmemi.seg->flags_off = hdr + info;
         shmemi.seg->flags_row = row;
+        shmemi.seg->dbg_off = hdr + info + flags;
         shmemi.seg->total_size = total;
         atomic_store (&shmemi.seg->magic, SEG_MAGIC);
     } else {
@@ -273,7 +275,8 @@ static void bootstrap_attach (void)
     shmemi.seg_size = total;
     atomic_fetch_add (&shmemi.seg->attached, 1);
     shmemi.bar_count = (uint64_t *) calloc ((size_t) npes, sizeof (uint64_t));
-    if (shmemi.bar_count == NULL)
+    shmemi.dbg_count = (uint64_t *) calloc ((size_t) npes, sizeof (uint64_t));
+    if (shmemi.bar_count == NULL || shmemi.dbg_count == NULL)
         shmemi_fatal ("out of host memory");
 }
 
@@ -282,7 +285,7 @@ static void bootstrap_attach (void)
  * member q, as many arrivals as barriers it has shared with q. A member that
  * races ahead to the next barrier only raises a count that is already due, so
  * no reset round (the reference's second pSync word) is needed. */
-void shmemi_barrier_set (int PE_start, int stride, int PE_size)
+static void barrier_watch (int PE_start, int stride, int PE_size, void (*watch) (int q))
 {
     if (PE_size <= 1 || shmemi.npes <= 1)
         return;
@@ -302,6 +305,8 @@ void shmemi_barrier_set (int PE_start, int stride, int PE_size)
         while (atomic_load_explicit (seg_flag (me, q), memory_order_acquire) < want) {
             if ((++spins & 1023u) == 0) {
                 check_abort ();
+                if (watch != NULL)
+                    watch (q);
                 if (now_s () - t0 > shmemi.barrier_timeout)
                     shmemi_fatal ("barrier timed out after %.0f s waiting for PE %d",
                                   shmemi.barrier_timeout, q);
@@ -312,6 +317,134 @@ void shmemi_barrier_set (int PE_start, int stride, int PE_size)
             }
         }
     }
+}
+
+void shmemi_barrier_set (int PE_start, int stride, int PE_size)
+{
+    barrier_watch (PE_start, stride, PE_size, NULL);
+}
+
+/* ---------------------------------------------------------------------- */
+/* SHMEM_DEBUG=1: collective argument check                                 */
+/* ---------------------------------------------------------------------- */
+/* The reference's debug build checks that the library is initialised and
+ * that target/source are symmetric (src/reduce/reduce-op.c:395-398 ->
+ * src/utils/utils.h:74-129); a member passing a different nreduce, op or
+ * active set is not caught and reads wrong peer offsets or hangs. Here every
+ * member publishes its arguments in the bootstrap segment and counts, per
+ * peer of its active set, the checks it has entered with that peer
+ * (dbgcnt[me][q], like the barrier's pair counts). Members that see the
+ * same count for each other are in the same collective (OpenSHMEM orders the
+ * collectives of overlapping sets), so their records must agree: a member
+ * compares them while it waits in the check's barrier -- which catches a
+ * differing PE_start / stride / size without waiting out the barrier timeout
+ * -- and again once it is through. A closing barrier keeps every record in
+ * place until all members have compared. A mismatch aborts every PE with the
+ * field. */
+static struct shmemi_dbg_rec dbg_mine;
+
+static _Atomic uint64_t *dbg_cnt (int row_pe, int peer)
+{
+    _Atomic uint64_t *base = (_Atomic uint64_t *) ((char *) shmemi.seg + shmemi.seg->dbg_off);
+    return base + (size_t) row_pe * shmemi.seg->flags_row + (size_t) peer;
+}
+
+static void dbg_read (int pe, struct shmemi_dbg_rec *out)
+{
+    struct shmemi_dbg_rec *r = &seg_info (pe)->dbg;
+    for (;;) {
+        const uint32_t s0 = atomic_load_explicit (&r->seq, memory_order_acquire);
+        if (s0 & 1u) {
+            __builtin_ia32_pause ();
+            continue;
+        }
+        memcpy ((char *) out + offsetof (struct shmemi_dbg_rec, op), (const char *) r + offsetof (struct shmemi_dbg_rec, op),
+                sizeof *out - offsetof (struct shmemi_dbg_rec, op));
+        atomic_thread_fence (memory_order_acquire);
+        if (atomic_load_explicit (&r->seq, memory_order_relaxed) == s0)
+            return;
+    }
+}
+
+/* the first field in which b differs from a, or NULL */
+static const char *dbg_diff (const struct shmemi_dbg_rec *a, const struct shmemi_dbg_rec *b, long *va, long *vb)
+{
+#define F(field, name)                                                                                          \
+    if (a->field != b->field) {                                                                                 \
+        *va = (long) a->field;                                                                                  \
+        *vb = (long) b->field;                                                                                  \
+        return name;                                                                                            \
+    }
+    F (pe_start, "PE_start")
+    F (log_stride, "logPE_stride")
+    F (pe_size, "PE_size")
+    F (op, "reduction operator (enum mi355_op)")
+    F (dtype, "element type (enum mi355_dtype)")
+    F (nreduce, "nreduce")
+    F (tkind, "target memory kind (0 host, 1 device symmetric heap, 2 other device memory)")
+    F (skind, "source memory kind (0 host, 1 device symmetric heap, 2 other device memory)")
+    F (toff, "target offset in the device symmetric heap")
+    F (soff, "source offset in the device symmetric heap")
+    F (algorithm, "reduce algorithm (shmemx_set_reduce_algorithm)")
+    F (order, "result order (shmemx_set_reduce_order)")
+#undef F
+    if (strcmp (a->fn, b->fn) != 0) {
+        *va = *vb = 0;
+        return "collective";
+    }
+    return NULL;
+}
+
+/* q's record, if q is inside the check of the same collective as this PE
+ * (the same pair count), compared with this PE's; 1 if compared */
+static int dbg_compare (int q)
+{
+    if (atomic_load_explicit (dbg_cnt (q, shmemi.mype), memory_order_acquire) != shmemi.dbg_count[q])
+        return 0;
+    struct shmemi_dbg_rec theirs;
+    dbg_read (q, &theirs);
+    long va = 0, vb = 0;
+    const char *f = dbg_diff (&dbg_mine, &theirs, &va, &vb);
+    if (f != NULL && strcmp (f, "collective") == 0)
+        shmemi_fatal ("SHMEM_DEBUG: collective mismatch: PE %d called %s, PE %d called %s", shmemi.mype,
+                      dbg_mine.fn, q, theirs.fn);
+    if (f != NULL)
+        shmemi_fatal ("SHMEM_DEBUG: %s: %s is %ld on PE %d but %ld on PE %d (every member of the active set must "
+                      "pass the same arguments)", dbg_mine.fn, f, va, shmemi.mype, vb, q);
+    return 1;
+}
+
+static void dbg_watch (int q) { (void) dbg_compare (q); }
+
+void shmemi_debug_exchange (const struct shmemi_dbg_rec *mine, int PE_start, int stride, int PE_size)
+{
+    if (shmemi.seg == NULL || PE_size < 2)
+        return;
+    struct shmemi_dbg_rec *r = &seg_info (shmemi.mype)->dbg;
+    dbg_mine = *mine;
+    const uint32_t s = atomic_load_explicit (&r->seq, memory_order_relaxed);
+    atomic_store_explicit (&r->seq, s + 1, memory_order_relaxed);
+    atomic_thread_fence (memory_order_release);
+    memcpy ((char *) r + offsetof (struct shmemi_dbg_rec, op), (const char *) mine + offsetof (struct shmemi_dbg_rec, op),
+            sizeof *r - offsetof (struct shmemi_dbg_rec, op));
+    atomic_store_explicit (&r->seq, s + 2, memory_order_release);
+    /* the record first, then the pair counts that make it current for each peer */
+    for (int i = 0; i < PE_size; ++i) {
+        const int q = PE_start + i * stride;
+        if (q != shmemi.mype)
+            atomic_store_explicit (dbg_cnt (shmemi.mype, q), ++shmemi.dbg_count[q], memory_order_release);
+    }
+
+    barrier_watch (PE_start, stride, PE_size, dbg_watch);
+    for (int i = 0; i < PE_size; ++i) {
+        const int q = PE_start + i * stride;
+        if (q != shmemi.mype && !dbg_compare (q))
+            shmemi_fatal ("SHMEM_DEBUG: %s: PE %d passed this call's synchronization from another call (a barrier "
+                          "or a collective over other PEs): the members disagree on the active set (PE_start %d, "
+                          "logPE_stride %d, PE_size %d here)", dbg_mine.fn, q, dbg_mine.pe_start,
+                          dbg_mine.log_stride, dbg_mine.pe_size);
+    }
+    shmemi_barrier_set (PE_start, stride, PE_size); /* every member has compared: records may change */
 }
 
 /* ---------------------------------------------------------------------- */
@@ -484,6 +617,33 @@ static void sigmem_init (void)
     shmemi.peer_sig[shmemi.mype] = shmemi.sigmem;
 }
 
+/* The settings that decide what the members of a collective do together
+ * must agree on every PE (one PE on the fused path and another on the
+ * multi-launch one would wait on each other for ever): abort at init, naming
+ * the environment variable, when a peer's differ. */
+static void settings_check (void)
+{
+    const struct shmemi_settings *a = &seg_info (shmemi.mype)->settings;
+    for (int pe = 0; pe < shmemi.npes; ++pe) {
+        if (pe == shmemi.mype)
+            continue;
+        const struct shmemi_settings *b = &seg_info (pe)->settings;
+#define S(field, env)                                                                                           \
+    if (a->field != b->field)                                                                                   \
+        shmemi_fatal ("%s differs between PEs: %lld here, %lld on PE %d (every PE must use the same value)", env, \
+                      (long long) a->field, (long long) b->field, pe);
+        S (algorithm, "SHMEM_REDUCE_ALGORITHM")
+        S (order, "SHMEM_REDUCE_ORDER")
+        S (debug, "SHMEM_DEBUG")
+        S (order_chunk, "SHMEM_DEVICE_ORDER_SIZE")
+        S (fused_max, "SHMEM_FUSED_MAX_BYTES")
+        S (oneshot_max, "SHMEM_ONESHOT_MAX_BYTES")
+        S (scratch_chunk, "SHMEM_DEVICE_SCRATCH_SIZE")
+        S (user_size, "SHMEM_DEVICE_HEAP_SIZE")
+#undef S
+    }
+}
+
 /* Publish this PE's heap and map every peer's (after the info barrier). */
 static void heap_exchange (void)
 {
@@ -495,8 +655,12 @@ static void heap_exchange (void)
     SHMEMI_HIP (hipIpcGetMemHandle (&me->heap_handle, shmemi.heap));
     SHMEMI_HIP (hipIpcGetMemHandle (&me->sig_handle, shmemi.sigmem));
     me->heap_size = shmemi.heap_size;
+    me->settings = (struct shmemi_settings) {shmemi.algorithm, shmemi.order, shmemi.debug != 0, shmemi.srv.enabled,
+                                             shmemi.order_chunk, shmemi.fused_max, shmemi.oneshot_max,
+                                             shmemi.scratch_chunk, shmemi.user_size};
     __atomic_store_n (&me->published, 1, __ATOMIC_RELEASE);
     shmemi_barrier_set (0, 1, shmemi.npes);
+    settings_check ();
 
     for (int pe = 0; pe < shmemi.npes; ++pe) {
         if (pe == shmemi.mype)
@@ -556,6 +720,69 @@ static void heap_exchange (void)
         shmemi.peer_sig[pe] = (unsigned long long *) p;
     }
     shmemi_barrier_set (0, 1, shmemi.npes);
+}
+
+/* Coherence of peer-heap reads (the contract of a blocking get: it returns
+ * the remote PE's CURRENT data, src/comms/gasnet/comms-inline.h:2224-2238).
+ * A peer GPU's memory is cached in this GPU's L2 without coherence, so a
+ * second read of a buffer a peer rewrote may hit the first read's line; the
+ * P2P schedules queue mi355_acquire_system before such reads.
+ * This checks the protocol on the job's real layout:
+ *   1. every PE reads every peer's marker with plain cached loads, from 32
+ *      blocks (dealt over the 8 XCDs, so every XCD's L2 holds the lines);
+ *   2. barrier; every PE rewrites its own marker with a write-through store;
+ *      barrier;
+ *   3. re-read without an acquire: an old value = stale_without_acquire
+ *      (evidence the acquire is needed; not an error);
+ *   4. mi355_acquire_system, re-read: every block must see every new value.
+ * SHMEM_TEST_IPC_FAIL=stale makes PE 1 report step 4 stale (tests). */
+static void coherence_test (size_t mark_off, int *passed, int *stale)
+{
+    const int np = shmemi.npes, me = shmemi.mype, nb = 32;
+    const unsigned long long newval = 0xC0DE5EE000000000ull;
+    unsigned long long **ptrs = (unsigned long long **) calloc ((size_t) np, sizeof (void *));
+    unsigned long long *host = (unsigned long long *) calloc ((size_t) np * nb, sizeof (unsigned long long));
+    unsigned long long *dev = NULL;
+    if (ptrs == NULL || host == NULL)
+        shmemi_fatal ("out of host memory");
+    SHMEMI_HIP (hipMalloc ((void **) &dev, sizeof (unsigned long long) * (size_t) np * nb));
+    for (int q = 0; q < np; ++q)
+        ptrs[q] = (unsigned long long *) (shmemi.peer_heap[q] + mark_off);
+#define PEEK(what)                                                                                              \
+    do {                                                                                                        \
+        if (mi355_peek_cached ((const unsigned long long *const *) ptrs, np, dev, nb, shmemi.stream) != 0)      \
+            shmemi_fatal ("coherence test: peek launch failed");                                               \
+        SHMEMI_HIP (hipMemcpy (host, dev, sizeof (unsigned long long) * (size_t) np * nb,                       \
+                               hipMemcpyDeviceToHost));                                                         \
+    } while (0)
+    PEEK ("first read");
+    shmemi_barrier_set (0, 1, np);
+    unsigned long long *own = (unsigned long long *) (shmemi.heap + mark_off);
+    if (mi355_poke (&own, 1, newval + (unsigned long long) me, shmemi.stream) != 0)
+        shmemi_fatal ("coherence test: poke launch failed");
+    SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    shmemi_barrier_set (0, 1, np);
+    PEEK ("re-read without acquire");
+    *stale = 0;
+    for (int b = 0; b < nb; ++b)
+        for (int q = 0; q < np; ++q)
+            if (host[(size_t) b * np + q] != newval + (unsigned long long) q)
+                *stale = 1;
+    if (mi355_acquire_system (shmemi.stream) != 0)
+        shmemi_fatal ("coherence test: acquire launch failed");
+    PEEK ("re-read after acquire");
+#undef PEEK
+    *passed = 1;
+    for (int b = 0; b < nb; ++b)
+        for (int q = 0; q < np; ++q)
+            if (host[(size_t) b * np + q] != newval + (unsigned long long) q)
+                *passed = 0;
+    const char *fail = me == 1 ? getenv ("SHMEM_TEST_IPC_FAIL") : NULL;
+    if (fail != NULL && strcmp (fail, "stale") == 0)
+        *passed = 0, *stale = 1;
+    (void) hipFree (dev);
+    free (host);
+    free (ptrs);
 }
 
 /* Interconnect check at init (PE_size > 1): every PE stores a value into
@@ -621,14 +848,37 @@ static void interconnect_selftest (void)
     free (host);
     free (ptrs);
 
+    /* every PE runs the coherence test when every PE has its peers mapped */
     __atomic_store_n (&seg_info (me)->selftest, sig_ok | (heap_ok << 1), __ATOMIC_RELEASE);
     shmemi_barrier_set (0, 1, np);
+    int all_mapped = 1;
+    for (int q = 0; q < np; ++q)
+        all_mapped &= (__atomic_load_n (&seg_info (q)->selftest, __ATOMIC_ACQUIRE) >> 1) & 1;
+    int coh = 0;
+    if (all_mapped) {
+        int passed = 1, stale = 0;
+        coherence_test (mark_off, &passed, &stale);
+        coh = 4 | (passed << 3) | (stale << 4);
+        if (!passed)
+            heap_ok = 0;
+    }
+
+    __atomic_store_n (&seg_info (me)->selftest, sig_ok | (heap_ok << 1) | coh, __ATOMIC_RELEASE);
+    shmemi_barrier_set (0, 1, np);
     int all_sig = 1, all_heap = 1;
+    shmemi.coh_ran = all_mapped;
+    shmemi.coh_passed = all_mapped;
+    shmemi.coh_stale = 0;
     for (int q = 0; q < np; ++q) {
         const int r = __atomic_load_n (&seg_info (q)->selftest, __ATOMIC_ACQUIRE);
         all_sig &= r & 1;
         all_heap &= (r >> 1) & 1;
+        shmemi.coh_passed &= (r >> 3) & 1;
+        shmemi.coh_stale |= (r >> 4) & 1;
     }
+    if (all_mapped && !shmemi.coh_passed && me == 0)
+        fprintf (stderr, "[shmem] warning: a peer heap re-read after a system-scope acquire returned stale data "
+                         "(init coherence test)\n");
     if (!all_sig) {
         if (me == 0)
             fprintf (stderr, "[shmem] warning: peer signal-region stores are not visible; "
@@ -1043,6 +1293,8 @@ void pshmem_finalize (void)
     }
     free (shmemi.bar_count);
     shmemi.bar_count = NULL;
+    free (shmemi.dbg_count);
+    shmemi.dbg_count = NULL;
     shmemi.initialized = 0;
     shmemi_trace_fini ();
 }
@@ -1124,6 +1376,8 @@ int shmemx_set_reduce_algorithm (int algorithm)
     if (algorithm < SHMEMX_REDUCE_AUTO || algorithm > SHMEMX_REDUCE_RCCL)
         shmemi_fatal ("shmemx_set_reduce_algorithm(%d): unknown algorithm", algorithm);
     int old = shmemi.algorithm;
+    if (old != algorithm && shmemi.initialized && shmemi.heap != NULL)
+        shmemi_server_stop (); /* a resident server keeps the schedule it was started for */
     shmemi.algorithm = algorithm;
     return old;
 }
@@ -1135,8 +1389,20 @@ int shmemx_set_reduce_order (int order)
     if (order != SHMEMX_ORDER_REFERENCE && order != SHMEMX_ORDER_PE_START)
         shmemi_fatal ("shmemx_set_reduce_order(%d): unknown order", order);
     int old = shmemi.order;
+    if (old != order && shmemi.initialized && shmemi.heap != NULL)
+        shmemi_server_stop (); /* a resident server keeps the result order it was started with */
     shmemi.order = order;
     return old;
+}
+
+void shmemx_coherence_selftest (int *ran, int *passed, int *stale_without_acquire)
+{
+    if (ran != NULL)
+        *ran = shmemi.coh_ran;
+    if (passed != NULL)
+        *passed = shmemi.coh_passed;
+    if (stale_without_acquire != NULL)
+        *stale_without_acquire = shmemi.coh_stale;
 }
 
 int shmemx_get_reduce_order (void) { return shmemi.order; }

@@ -22,6 +22,26 @@
 #define SHMEMI_ALIGN 256
 
 /* ---- bootstrap segment (POSIX shm, one per job, node-local) ---- */
+
+/* SHMEM_DEBUG=1: one collective's arguments as this PE passed them
+ * (debug_check, reduce.c; shmemi_debug_exchange, runtime.c). Written under a
+ * seqlock (seq odd while being written). */
+struct shmemi_dbg_rec {
+    _Atomic uint32_t seq;
+    int32_t pad0;
+    int32_t op, dtype, nreduce, pe_start, log_stride, pe_size;
+    int32_t tkind, skind;       /* 0 host, 1 device heap, 2 other device memory */
+    int32_t algorithm, order, persistent, pad;
+    uint64_t toff, soff;        /* heap offsets (device heap kinds), else 0 */
+    char fn[48];
+};
+
+/* Settings every PE of a job must share (compared at init). */
+struct shmemi_settings {
+    int32_t algorithm, order, debug, persistent;
+    uint64_t order_chunk, fused_max, oneshot_max, scratch_chunk, user_size;
+};
+
 struct shmemi_pe_info {
     int32_t pid;
     int32_t device;
@@ -30,8 +50,11 @@ struct shmemi_pe_info {
     hipIpcMemHandle_t sig_handle;
     uint64_t heap_size;
     int32_t published;
-    int32_t selftest;           /* bit 0: signal region stores seen, bit 1: heap reads ok */
+    int32_t selftest;           /* bit 0: signal region stores seen, bit 1: heap reads ok,
+                                   bit 2: coherence test ran, bit 3: it passed, bit 4: stale without acquire */
     uint64_t collect_bytes;     /* this PE's contribution to the current shmem_collect */
+    struct shmemi_settings settings;
+    struct shmemi_dbg_rec dbg;
 };
 
 struct shmemi_seg {
@@ -49,6 +72,7 @@ struct shmemi_seg {
     uint64_t info_off;          /* -> struct shmemi_pe_info[npes] */
     uint64_t flags_off;         /* -> _Atomic uint64_t flags[npes][row] */
     uint64_t flags_row;         /* words per row (padded) */
+    uint64_t dbg_off;           /* -> _Atomic uint64_t dbgcnt[npes][row]: SHMEM_DEBUG checks entered, per pair */
     uint64_t total_size;
 };
 
@@ -81,6 +105,7 @@ struct shmemi_state {
     char seg_name[128];
     int seg_unlinked;
     uint64_t *bar_count;        /* [npes]: barriers done with each peer */
+    uint64_t *dbg_count;        /* [npes]: SHMEM_DEBUG collective checks entered with each peer */
 
     /* device symmetric heap: [user | scratch] */
     char *heap;                 /* this PE's base */
@@ -120,6 +145,8 @@ struct shmemi_state {
         double idle_s;          /* SHMEM_PERSISTENT_IDLE_US: the server exits after this long without a call */
         int running;
         int op, dtype, start, stride, size;  /* the calls it serves */
+        int ordered;            /* the result order it was started with (ordered_pair) */
+        const void *kernel;     /* its kernel stub (shmemx_last_call_info) */
         unsigned long long grid_elems;       /* the grid it was sized for */
         unsigned seq;           /* next mailbox seq */
         struct MI355ServerMailbox *mb;       /* host-coherent, device-accessible */
@@ -127,6 +154,19 @@ struct shmemi_state {
         double last_end;        /* when the last fused call returned (burst detection) */
         long served, launched;  /* statistics */
     } srv;
+
+    /* the init-time coherence test of peer-heap reads (job-wide results) */
+    int coh_ran, coh_passed, coh_stale;
+
+    /* what the last *_to_all call ran (shmemx_last_call_info); the kernel
+     * stub is resolved to its name only on request */
+    struct {
+        int valid;
+        const char *schedule;
+        const void *kernel;
+        int ordered, sources, outputs, peer_sources, launches;
+        unsigned long long bytes_per_buffer, alg_bytes, peer_bytes;
+    } last;
 
     /* kernel timing */
     int timing;
@@ -174,6 +214,8 @@ void shmemi_timed_marker (int end);
 int shmemi_rccl_comm (void **comm);
 void shmemi_publish_count (size_t nbytes);
 size_t shmemi_peer_count (int pe);
+/* runtime.c: SHMEM_DEBUG's collective argument exchange over an active set */
+void shmemi_debug_exchange (const struct shmemi_dbg_rec *mine, int PE_start, int stride, int PE_size);
 
 #define SHMEMI_HIP(call) shmemi_hip_check ((call), #call)
 

@@ -6,6 +6,8 @@ OpenSHMEM test program in C would call it. It never computes a reduction
 itself: if the library is missing, loading fails loudly.
 """
 import ctypes
+import glob
+import hashlib
 import os
 
 import numpy as np
@@ -32,6 +34,14 @@ _sz = ctypes.c_size_t
 _i = ctypes.c_int
 
 
+class CallInfo(ctypes.Structure):
+    """shmemx_call_info (include/shmemx.h): what the last *_to_all call ran"""
+    _fields_ = [("schedule", ctypes.c_char * 64), ("kernel", ctypes.c_char * 256), ("ordered", _i),
+                ("sources", _i), ("outputs", _i), ("peer_sources", _i), ("launches", _i),
+                ("bytes_per_buffer", ctypes.c_ulonglong), ("alg_bytes", ctypes.c_ulonglong),
+                ("peer_bytes", ctypes.c_ulonglong)]
+
+
 def load(path=LIB_PATH):
     if not os.path.exists(path):
         raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
@@ -55,6 +65,8 @@ def load(path=LIB_PATH):
         "shmemx_memcpy": ([_vp, _vp, _sz], None), "shmemx_wtime": ([], ctypes.c_double),
         "shmemx_kernel_timing": ([_i], None),
         "shmemx_rccl_init": ([ctypes.c_double], _i),
+        "shmemx_last_call_info": ([ctypes.POINTER(CallInfo)], _i),
+        "shmemx_coherence_selftest": ([ctypes.POINTER(_i)] * 3, None),
         "shmemx_kernel_timing_stats": ([ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_double)], None),
         "shmemx_kernel_timing_phase_stats": ([_i, ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double),
@@ -220,6 +232,22 @@ class Shmem:
         s = (_vp * len(srcs))(*srcs)
         return self.lib.mi355_combine_orders(OPS.index(op), DTYPES.index(dtype), d, s, len(srcs), n, stream)
 
+    def last_call_info(self):
+        """dict of shmemx_last_call_info, or None before the first call"""
+        ci = CallInfo()
+        if self.lib.shmemx_last_call_info(ctypes.byref(ci)) != 0:
+            return None
+        d = {f: getattr(ci, f) for f, _ in CallInfo._fields_}
+        d["schedule"] = ci.schedule.decode()
+        d["kernel"] = ci.kernel.decode()
+        return d
+
+    def coherence_selftest(self):
+        """(ran, passed, stale_without_acquire) of the init-time peer-read coherence test"""
+        a, b, c = _i(), _i(), _i()
+        self.lib.shmemx_coherence_selftest(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return bool(a.value), bool(b.value), bool(c.value)
+
     def kernel_timing(self, enable):
         self.lib.shmemx_kernel_timing(1 if enable else 0)
 
@@ -248,6 +276,23 @@ def bench_loop(path=BENCH_LIB_PATH, name="double_sum"):
     f.argtypes = [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i]
     f.restype = None
     return f
+
+
+def kernel_source_hash():
+    """sha256 (16 hex digits) of everything that decides the kernels' code:
+    csrc/*.hip, csrc/*.h, csrc/Makefile and include/mi355_reduce.h. PMC
+    counter profiles (profiles/pmc_traffic.json) carry the hash of the tree
+    they were taken from; bench.py reports their HBM traffic only for the
+    same hash."""
+    root = os.path.dirname(HERE)
+    files = sorted(glob.glob(os.path.join(HERE, "csrc", "*.hip")) + glob.glob(os.path.join(HERE, "csrc", "*.h")) +
+                   [os.path.join(HERE, "csrc", "Makefile"), os.path.join(root, "include", "mi355_reduce.h")])
+    h = hashlib.sha256()
+    for f in files:
+        h.update(os.path.relpath(f, root).encode())
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 
 
 def shard_bounds(lib, n, elem_size, nshards, i):

@@ -6,7 +6,7 @@ own source first, reduce-op.c:226-264). Every PE runs the same script (the
 parameters come from a seed shared by all PEs, the data from seed + PE).
 
 usage: persistent_worker.py SCRIPT SEED   (identity from SHMEM_PE / SHMEM_NPES)
-  SCRIPT: burst | mixed | idle | race
+  SCRIPT: burst | mixed | idle | race | orderflip | ordered
 Prints one JSON line (calls checked, calls served by a resident server,
 servers launched); exits 1 on the first mismatch.
 """
@@ -136,6 +136,32 @@ elif script == "race":
     idle = float(os.environ.get("SHMEM_PERSISTENT_IDLE_US", "1000")) * 1e-6
     for k in range(10):
         batch("sum", "double", 40, 2048, gap=lambda: idle * 2.0 * prng.random())
+elif script == "orderflip":
+    # the result order switched INSIDE a burst, with no other GPU work between
+    # the calls (a resident server keeps the order it was started with: every
+    # member of a float max must switch together, and shmemx_set_reduce_order
+    # stops the server so the next call starts one with the new order)
+    op, dtype, n = "max", "float", 3000
+    for rnd in range(4):
+        k = 8
+        xs = [[source(op, dtype, n, seed * 31 + rnd * 97 + c, p) for p in range(npes)] for c in range(2 * k)]
+        for c in range(2 * k):
+            shm.put(src_buf + c * 16384, xs[c][me])
+        shm.barrier_all()
+        first = "reference" if rnd % 2 == 0 else "pe_start"
+        second = "pe_start" if first == "reference" else "reference"
+        shm.set_order(first)
+        for c in range(k):
+            shm.to_all(op, dtype, dst_buf + c * 16384, src_buf + c * 16384, n, 0, 0, npes)
+        shm.set_order(second)
+        for c in range(k, 2 * k):
+            shm.to_all(op, dtype, dst_buf + c * 16384, src_buf + c * 16384, n, 0, 0, npes)
+        shm.set_order("reference")
+        for c in range(2 * k):
+            who = me if (first if c < k else second) == "reference" else 0
+            assert_match(shm.get(dst_buf + c * 16384, n, dtype), oracle.reduce_pe(op, dtype, xs[c], who), op, dtype,
+                         f"PE {me} round {rnd} call {c} ({first} then {second})")
+            checked += 1
 elif script == "ordered":
     # the documented contract: GPU work the caller queued on the null stream
     # (a 30 ms kernel, then a device-to-device copy of new data into the

@@ -4,9 +4,14 @@ check, and the roofline / cpu_baseline / op_coverage records. The N = 2 run
 shares the one test GPU and forces the RCCL comparison, which then fails
 (RCCL refuses two ranks on one device): the line must still come out, with
 the comparison marked as skipped and the target re-checked on the default
-schedule."""
+schedule. At N = 2 the line must also carry the same-run CPU baseline (2
+cores), the roofline of the kernel the library's trace says it ran, with the
+bytes recomputed from that schedule, the opt-in persistent leg and the
+coherence self-test."""
 import json
 import os
+import re
+import socket
 import subprocess
 import sys
 
@@ -17,8 +22,14 @@ pytestmark = pytest.mark.gpu
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 
 
-def run(cmd, timeout=240):
-    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+def free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run(cmd, timeout=240, env=None):
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
     assert len(lines) == 1, r.stdout[-3000:]
@@ -50,6 +61,10 @@ def test_bench_one_gpu_line():
     assert cb["one_pe"]["cores"] == 1 and cb["config1"]["us_per_call"] > 0 and cb["host"]["nproc"] >= 1
     assert cb["eight_pe"]["cores"] == 8 and cb["eight_pe"]["value"] > 0 and cb["config5"]["us_per_call"] > 0
     assert d["config"]["bytes_per_pe"] == 256 << 20
+    r = d["roofline"]
+    assert r["kernel"] == "void mi355k::copy_segments<4, 1>(mi355k::SegParams<1>)", r
+    assert r["call"]["schedule"] == "identity" and r["alg_bytes_per_launch"] == 2 * (256 << 20), r
+    assert d["coherence_selftest"] is None
     k = d["kernels"]
     for name in ("fold_k2_double_sum", "fold_k8_double_sum", "rs_shard_n8_double_sum", "fold_k8_float_max",
                  "fold_k8_longlong_and", "rs_shard_n8_float_max"):
@@ -68,11 +83,36 @@ def test_bench_one_gpu_line():
 
 
 @pytest.mark.multipe
-def test_bench_two_ranks_line_with_failed_rccl_comparison():
+def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
+    log = tmp_path / "trace.log"
+    env = dict(os.environ, SHMEM_LOG_LEVELS="REDUCTION", SHMEM_LOG_FILE=str(log))
     d = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
-             "--master-addr", "127.0.0.1", "--master-port", "29563", "bench.py", "--gpus", "2", "--steps", "5",
-             "--warmup", "2", "--force-rccl-compare"])
+             "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", "--steps",
+             "5", "--warmup", "2", "--force-rccl-compare", "--cpu-seconds", "2"], env=env)
     common(d, 2)
-    assert d["cpu_baseline"] is None and d["small_call_persistent"] is None
     assert "error" in d["rccl_compare"], d["rccl_compare"]
     assert d["xgmi"]["busbw_GB_s_per_pe"] > 0
+    # the same-run CPU baseline at N = 2: 2 PE processes on 2 pinned cores
+    cb = d["cpu_baseline"]
+    assert cb["cores"] == 2 and cb["value"] > 0 and cb["kind"] == "port" and cb["host"]["nproc"] >= 2
+    # the roofline kernel is the one the library ran: the trace's schedule
+    # line for the 256 MiB calls says which fold (a 2-member double sum is
+    # order-free: the plain fold, one output, not combine_orders_vec)
+    S = d["config"]["bytes_per_pe"]
+    n = S // 8
+    lines = [ln for ln in open(log).read().splitlines() if "schedule:" in ln and f"({n} elements" in ln]
+    assert lines, "no schedule trace line for the 256 MiB calls"
+    assert all("P2P shards, device barriers, PE_start order" in ln for ln in lines), lines[:3]
+    r = d["roofline"]
+    assert re.fullmatch(r"void mi355k::combine_vec<0, double, 2, \d, \d>\(mi355k::CombineParams\)", r["kernel"]), r
+    shard = S // 2
+    assert r["call"]["schedule"] == "p2p" and r["call"]["sources"] == 2 and r["call"]["outputs"] == 1, r
+    assert r["alg_bytes_per_launch"] == shard and r["hbm"]["bytes_per_launch"] == 3 * shard, r
+    # the opt-in persistent server at N > 1 (a child job of one PE per rank)
+    sp = d["small_call_persistent"]
+    assert "error" not in sp, sp
+    assert sp["opt_in"] and sp["check"].startswith("bit-exact") and sp["served"] >= sp["calls"] - 2, sp
+    assert sp["schedule"] == "persistent" and "fused_server<0, double>" in sp["kernel"], sp
+    # the init coherence test ran on the real layout (here: one GPU) and passed
+    c = d["coherence_selftest"]
+    assert c["ran"] and c["passed"], c

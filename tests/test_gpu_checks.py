@@ -1,0 +1,172 @@
+"""GPU: the job-level checks added in round 3, on PE processes sharing the
+one test GPU.
+
+* the init-time coherence test of peer-heap reads (runtime.c
+  coherence_test): it runs and passes on the real layout; a simulated stale
+  re-read after the acquire (SHMEM_TEST_IPC_FAIL=stale on PE 1) makes every
+  PE fall back to the RCCL schedule cleanly (reference contract: a blocking
+  get returns the peer's current data, comms-inline.h:2224-2238);
+* SHMEM_DEBUG=1's collective argument check (reference debug checks
+  reduce-op.c:395-398, utils.h:74-129): a member passing a different
+  nreduce / PE_size / operator ends the job within seconds, with a message
+  naming the field, instead of reading wrong offsets or waiting out the
+  barrier timeout; matching calls (also disjoint sets at once, and
+  stream-ordered ones) pass;
+* settings that must agree across PEs (SHMEM_REDUCE_ORDER, ...) abort init.
+"""
+import os
+import subprocess
+import sys
+import time
+import uuid
+
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+pytestmark = [pytest.mark.gpu, pytest.mark.multipe]
+
+PRELUDE = ("import sys, os, time\nsys.path[:0] = [%r, %r, %r]\n" % (HERE, os.path.join(ROOT, "osss-gasnet_amd"),
+                                                                     os.path.join(ROOT, "oracle")) +
+           "import numpy as np, shmem_reduce\nshm = shmem_reduce.Shmem(); shm.init()\n"
+           "me, npes = shm.my_pe(), shm.n_pes()\n")
+
+
+def spawn(npes, code, extra=None, per_pe=None, timeout=120):
+    env = dict(os.environ, SHMEM_NPES=str(npes), SHMEM_JOB_ID=uuid.uuid4().hex[:12], SHMEM_DEVICE="0",
+               SHMEM_DEVICE_HEAP_SIZE="32M", SHMEM_DEVICE_SCRATCH_SIZE="3M", SHMEM_BARRIER_TIMEOUT="120")
+    env.update(extra or {})
+    procs = []
+    for pe in range(npes):
+        e = dict(env, SHMEM_PE=str(pe))
+        e.update((per_pe or {}).get(pe, {}))
+        procs.append(subprocess.Popen([sys.executable, "-c", PRELUDE + code], env=e, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    outs = []
+    for p in procs:
+        try:
+            outs.append(p.communicate(timeout=timeout)[0])
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    return [p.returncode for p in procs], outs, time.time()
+
+
+# ---------------------------------------------------------------------------
+# coherence self-test
+# ---------------------------------------------------------------------------
+COH = ("ran, passed, stale = shm.coherence_selftest()\n"
+       "print('COH', int(ran), int(passed), int(stale), 'ALG', shm.lib.shmemx_get_reduce_algorithm(), flush=True)\n"
+       "x = np.random.default_rng(5 + me).random(4099) - 0.5\n"
+       "d = shm.malloc_device(4099 * 8); shm.put(d, x)\n"
+       "shm.to_all('sum', 'double', d, d, 4099, 0, 0, npes)\n"
+       "want = np.random.default_rng(5).random(4099) - 0.5 + (np.random.default_rng(6).random(4099) - 0.5)\n"
+       "print('EXACT', bool((shm.get(d, 4099, 'double') == want).all()), flush=True)\n"
+       "info = shm.last_call_info(); print('SCHED', info['schedule'], flush=True)\n"
+       "shm.finalize()\n")
+
+
+def parse(out, key):
+    return [ln.split()[1:] for ln in out.splitlines() if ln.startswith(key + " ")]
+
+
+def test_coherence_selftest_runs_and_passes():
+    rcs, outs, _ = spawn(2, COH)
+    for rc, out in zip(rcs, outs):
+        assert rc == 0, out[-2000:]
+        coh = parse(out, "COH")[0]
+        assert coh[:2] == ["1", "1"] and coh[3] == "0", out  # ran, passed; P2P (auto) kept
+        assert parse(out, "EXACT")[0] == ["True"] and parse(out, "SCHED")[0] == ["fused-twoshot"], out
+
+
+def test_stale_reread_falls_back_to_rccl():
+    """PE 1 reports its re-read after the acquire stale: every PE learns it at
+    init and runs the RCCL schedule (RCCL joins the two ranks on the one GPU
+    through its socket transport, NCCL_HOSTID per PE, as in
+    test_gpu_multipe.test_rccl_schedule_multi_rank); a 2-PE double sum is
+    a + b either way, so the result stays exact."""
+    per_pe = {pe: {"NCCL_HOSTID": f"shmem-stale-test-pe{pe}"} for pe in range(2)}
+    rcs, outs, _ = spawn(2, COH, extra={"SHMEM_TEST_IPC_FAIL": "stale", "NCCL_SOCKET_IFNAME": "lo",
+                                        "NCCL_IB_DISABLE": "1"}, per_pe=per_pe)
+    for rc, out in zip(rcs, outs):
+        assert rc == 0, out[-2000:]
+        coh = parse(out, "COH")[0]
+        assert coh[:3] == ["1", "0", "1"] and coh[4] == "3", out  # ran, failed, stale; algorithm RCCL
+        assert parse(out, "EXACT")[0] == ["True"] and parse(out, "SCHED")[0] == ["rccl"], out
+    assert "init coherence test" in outs[0]
+
+
+# ---------------------------------------------------------------------------
+# SHMEM_DEBUG=1 collective argument check
+# ---------------------------------------------------------------------------
+def run_mismatch(npes, body):
+    code = ("d = shm.malloc_device(1 << 16)\n"
+            "shm.to_all('sum', 'double', d, d, 100, 0, 0, npes)\n"   # a matching call first
+            "print('T0 %.6f' % time.time(), flush=True)\n" + body)
+    rcs, outs, t_end = spawn(npes, code, extra={"SHMEM_DEBUG": "1", "SHMEM_BARRIER_TIMEOUT": "600"})
+    t0 = min(float(parse(o, "T0")[0][0]) for o in outs if parse(o, "T0"))
+    return rcs, outs, t_end - t0
+
+
+def test_debug_check_names_a_different_nreduce():
+    rcs, outs, dt = run_mismatch(2, "shm.to_all('sum', 'double', d, d, 100 if me == 0 else 99, 0, 0, npes)\n"
+                                    "print('RETURNED', flush=True)\n")
+    assert all(rc != 0 for rc in rcs) and not any("RETURNED" in o for o in outs), outs
+    assert any("nreduce is 100 on PE 0 but 99 on PE 1" in o or "nreduce is 99 on PE 1 but 100 on PE 0" in o
+               for o in outs), outs
+    assert dt < 5.0, dt
+
+
+def test_debug_check_names_a_different_active_set():
+    # PE 0 and PE 1 disagree on PE_size; PE 2 waits in shmem_barrier_all
+    body = ("if me == 2:\n    shm.barrier_all()\n"
+            "else:\n    shm.to_all('max', 'int', d, d, 64, 0, 0, 2 if me == 0 else 3)\n"
+            "print('RETURNED', flush=True)\n")
+    rcs, outs, dt = run_mismatch(3, body)
+    assert all(rc != 0 for rc in rcs) and not any("RETURNED" in o for o in outs), outs
+    assert any("PE_size is" in o for o in outs), outs
+    assert dt < 5.0, dt
+
+
+def test_debug_check_names_a_different_operator():
+    body = ("f = 'sum' if me == 0 else 'max'\nshm.to_all(f, 'double', d, d, 64, 0, 0, npes)\n"
+            "print('RETURNED', flush=True)\n")
+    rcs, outs, dt = run_mismatch(2, body)
+    assert all(rc != 0 for rc in rcs) and not any("RETURNED" in o for o in outs), outs
+    assert any("reduction operator" in o for o in outs), outs
+    assert dt < 5.0, dt
+
+
+def test_debug_check_passes_matching_calls():
+    """Matching calls under SHMEM_DEBUG=1: disjoint active sets at once,
+    strided sets, the whole job, host arrays and stream-ordered calls."""
+    code = ("import oracle\n"
+            "d = shm.malloc_device(1 << 20); s = shm.malloc_device(1 << 20)\n"
+            "ok = True\n"
+            "for rnd in range(20):\n"
+            "    n = 1000 + 37 * rnd\n"
+            "    xs = [np.random.default_rng(rnd * 10 + p).random(n) for p in range(npes)]\n"
+            "    shm.put(s, xs[me]); shm.barrier_all()\n"
+            "    sets = [(0, 0, 2), (2, 0, 2)] if rnd % 3 == 0 else [(me % 2, 1, 2)] if rnd % 3 == 1 else [(0, 0, 4)]\n"
+            "    st = [t for t in sets if me in [t[0] + i * (1 << t[1]) for i in range(t[2])]][0]\n"
+            "    mem = [st[0] + i * (1 << st[1]) for i in range(st[2])]\n"
+            "    if rnd % 4 == 3:\n"
+            "        q = shm.stream_create(); shm.to_all_on_stream('sum', 'double', d, s, n, *st, q)\n"
+            "        shm.stream_sync(q); shm.stream_destroy(q)\n"
+            "    else:\n"
+            "        shm.to_all('sum', 'double', d, s, n, *st)\n"
+            "    got = shm.get(d, n, 'double')\n"
+            "    want = oracle.reduce_pe('sum', 'double', [xs[p] for p in mem], mem.index(me))\n"
+            "    ok &= bool((got.view(np.uint64) == want.view(np.uint64)).all())\n"
+            "print('OK', ok, flush=True)\nshm.finalize()\n")
+    rcs, outs, _ = spawn(4, code, extra={"SHMEM_DEBUG": "1"})
+    for rc, out in zip(rcs, outs):
+        assert rc == 0 and "OK True" in out, out[-2000:]
+
+
+def test_settings_must_agree_at_init():
+    rcs, outs, _ = spawn(2, "print('INIT-RETURNED', flush=True)\nshm.finalize()\n",
+                         per_pe={1: {"SHMEM_REDUCE_ORDER": "pe_start"}})
+    assert all(rc != 0 for rc in rcs) and not any("INIT-RETURNED" in o for o in outs), outs
+    assert any("SHMEM_REDUCE_ORDER differs between PEs" in o for o in outs), outs

@@ -68,6 +68,15 @@ def test_interrupted_bursts():
         assert s["checked"] == 3 * 46 and s["served"] >= 40 and s["launched"] >= 12, s
 
 
+def test_order_switched_inside_a_burst():
+    """shmemx_set_reduce_order between two calls of a burst: the calls after it
+    deliver the new order on every PE (the resident server, started for the
+    old order, is stopped by the switch; server_matches also compares it)."""
+    st = run(2, "orderflip", seed=3)
+    for s in st:
+        assert s["checked"] == 4 * 16 and s["served"] >= 16 and s["launched"] >= 8, s
+
+
 def test_gaps_longer_than_idle():
     st = run(2, "idle", seed=7, extra={"SHMEM_PERSISTENT_IDLE_US": "300"})
     for s in st:

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
-"""One PE of the same-GPU fused-kernel measurement (bench.py's `fused_same_gpu`
-leg, tools/profile_fused.sh). Run as NPES processes with SHMEM_PE / SHMEM_NPES
-/ SHMEM_JOB_ID set and SHMEM_DEVICE=0 (every PE on this GPU).
+"""One PE of the fused-kernel measurement: bench.py's `fused_same_gpu` leg
+(NPES processes with SHMEM_DEVICE=0, every PE on this GPU; also
+tools/profile_fused.sh) and its N > 1 `small_call_persistent` leg (one
+process per rank, each on the rank's GPU, SHMEM_PERSISTENT=1). Run with
+SHMEM_PE / SHMEM_NPES / SHMEM_JOB_ID / SHMEM_DEVICE set.
 
 For each message size, K back-to-back shmem_double_sum_to_all calls from a C
 loop (csrc/bench_loop.c): per-call time (max over PEs), then the same K calls
@@ -47,6 +49,9 @@ def main():
 
     out = {}
     import oracle
+    shared = np.array([sum(shm.lib.shmemx_pe_same_device(q) for q in range(npes) if q != me)], dtype=np.int32)
+    anyshared = np.zeros(1, dtype=np.int32)
+    shm.to_all("max", "int", anyshared.ctypes.data, shared.ctypes.data, 1, 0, 0, npes)
     for nb in sizes:
         n = nb // 8
         x = synth(me, n)
@@ -54,10 +59,13 @@ def main():
         loop(dst, src, n, 0, 0, npes, None, shm._psync_ptr, 20)
         shm.barrier_all()
         shm.sync()
+        served0, launched0 = shm.persistent_stats()
         t0 = time.perf_counter()
         loop(dst, src, n, 0, 0, npes, None, shm._psync_ptr, calls)
         shm.sync()
         t = max_over_pes(time.perf_counter() - t0) / calls
+        served1, launched1 = shm.persistent_stats()
+        info = shm.last_call_info()
         shm.barrier_all()
         shm.kernel_timing(True)
         loop(dst, src, n, 0, 0, npes, None, shm._psync_ptr, calls)
@@ -70,14 +78,15 @@ def main():
         kmax = max_over_pes(kavg)
         out[str(nb)] = {"bytes_per_pe": nb, "calls": calls, "us_per_call": round(t * 1e6, 2),
                         "kernel_avg_us": round(kmax * 1e3, 2), "kernels_timed": nk,
-                        "schedule": "fused one-shot" if nb <= 64 << 10 else "fused reduce-scatter + all-gather",
+                        "schedule": info["schedule"], "kernel": info["kernel"],
+                        "served": served1 - served0, "servers_launched": launched1 - launched0,
                         "check": f"bit-exact vs the reference's per-PE order on every PE, {n} elements each"
                         if bad == 0 else f"MISMATCH {bad} elements (worst PE)"}
         shm.barrier_all()
     shm.free_device(dst)
     shm.free_device(src)
     if me == 0:
-        print(json.dumps({"npes": npes, "same_gpu": True, "legs": out}), flush=True)
+        print(json.dumps({"npes": npes, "same_gpu": bool(anyshared[0]), "legs": out}), flush=True)
     shm.finalize()
 
 
