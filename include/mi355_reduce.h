@@ -228,21 +228,36 @@ int mi355_fused_pull (const MI355PullArgs *args, void *stream);
 #define MI355_SERVER_EXITED 2
 typedef struct MI355ServerMailbox {
     /* host -> device, one 64-byte line the server reads with one load: the
-     * call, then seq_head and seq_tail (release, in that order); a snapshot
-     * counts only when both hold the seq it waits for */
+     * call and its check word, then seq_head and seq_tail (release, in that
+     * order); a snapshot counts only when both hold the seq it waits for AND
+     * its check word matches dwords 1-11 (a torn read of the line -- not
+     * expected from one 64-byte aligned read over PCIe, but not guaranteed
+     * either -- is then retried, not served) */
     unsigned seq_head;                   /* the server serves seq first_seq, first_seq + 1, ... */
     unsigned cmd;                        /* MI355_SERVER_RUN / _QUIT */
     unsigned long long src_off, dst_off; /* byte offsets into every member's symmetric heap */
     unsigned long long n, shard;         /* as MI355FusedArgs */
     unsigned epoch;
     int oneshot;
-    unsigned pad0[3];
+    unsigned check;                      /* mi355_mailbox_check of the line, written with the call */
+    unsigned pad0[2];
     unsigned seq_tail;
     /* device -> host (own line) */
     unsigned state;                      /* MI355_SERVER_RUNNING (set by the host before the launch) / _EXITED */
     unsigned state_seq;                  /* EXITED: the first seq not served */
     unsigned pad1[14];
 } MI355ServerMailbox;
+
+/* The check word: dwords 1-11 of the line (cmd .. oneshot) xor-folded, mixed
+ * with the seq. The server recomputes it from the snapshot it read. */
+static inline unsigned mi355_mailbox_check (const MI355ServerMailbox *mb, unsigned seq)
+{
+    const unsigned *w = (const unsigned *) mb;
+    unsigned x = 0;
+    for (int i = 1; i <= 11; ++i)
+        x ^= w[i];
+    return x ^ (seq * 0x9E3779B1u);
+}
 
 /* Launch the server on `stream` (a stream of its own: it does not finish
  * until QUIT or idle). args: as for mi355_fused_allreduce with src/dst the

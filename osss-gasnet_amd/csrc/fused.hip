@@ -462,14 +462,22 @@ __device__ __forceinline__ void st_sys_u32(unsigned *p, unsigned v) {
 // command, or after idle_ticks without a call) and broadcasts it in the
 // signal region; every other block waits for the broadcast. Both lines are
 // read whole by lanes 0-15 of wave 0 (one 64-byte request) and count when
-// their head and tail words both hold the awaited seq (written last). Every
-// block then holds the call in f[] (LDS). A broadcast seq only advances after
-// the host saw the previous call complete, which needs every block, so no
-// block can miss one.
+// their head and tail words both hold the awaited seq (written last) and the
+// check word (dword 12) matches the call's dwords 1-11 (mi355_mailbox_check):
+// a snapshot torn between an old and a new call is read again. Every block
+// then holds the call in f[] (LDS). A broadcast seq only advances after the
+// host saw the previous call complete, which needs every block, so no block
+// can miss one.
 __device__ __forceinline__ bool line_has(const unsigned *line, unsigned seq, unsigned &v) {
-    v = ld_sys_u32(line + (threadIdx.x & 15));
-    const unsigned head = __shfl(v, 0), tail = __shfl(v, 15);
-    return head == seq && tail == seq;
+    const unsigned lane = threadIdx.x & 15;
+    v = ld_sys_u32(line + lane);
+    unsigned x = lane >= 1 && lane <= 11 ? v : 0u;
+    x ^= __shfl_xor(x, 8, 16);
+    x ^= __shfl_xor(x, 4, 16);
+    x ^= __shfl_xor(x, 2, 16);
+    x ^= __shfl_xor(x, 1, 16);
+    const unsigned head = __shfl(v, 0), tail = __shfl(v, 15), check = __shfl(v, 12);
+    return head == seq && tail == seq && check == (__shfl(x, 0) ^ (seq * 0x9E3779B1u));
 }
 
 __device__ void server_next(const MI355FusedArgs &a, MI355ServerMailbox *mb, unsigned seq,
@@ -494,6 +502,14 @@ __device__ void server_next(const MI355FusedArgs &a, MI355ServerMailbox *mb, uns
                 __builtin_amdgcn_s_sleep(2);
             }
             if (idle && lane == 1) v = MI355_SERVER_QUIT;  // dword 1: cmd
+            if (idle) {  // the broadcast's check word covers the QUIT
+                unsigned x = lane >= 1 && lane <= 11 ? v : 0u;
+                x ^= __shfl_xor(x, 8, 16);
+                x ^= __shfl_xor(x, 4, 16);
+                x ^= __shfl_xor(x, 2, 16);
+                x ^= __shfl_xor(x, 1, 16);
+                if (lane == 12) v = __shfl(x, 0) ^ (seq * 0x9E3779B1u);
+            }
             // broadcast: the call (dwords 1-14), then head and tail
             if (lane >= 1 && lane < 15) st_sys_u32(slot + lane, v);
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");

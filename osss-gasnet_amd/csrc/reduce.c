@@ -565,6 +565,7 @@ void shmemi_server_stop (void)
     if (__atomic_load_n (&mb->state, __ATOMIC_ACQUIRE) != MI355_SERVER_EXITED) {
         mb->cmd = MI355_SERVER_QUIT;
         const unsigned seq = shmemi.srv.seq++;
+        mb->check = mi355_mailbox_check (mb, seq);
         __atomic_store_n (&mb->seq_head, seq, __ATOMIC_RELEASE);
         __atomic_store_n (&mb->seq_tail, seq, __ATOMIC_RELEASE);
         server_wait_exited ();
@@ -586,6 +587,7 @@ static int server_call (size_t dst_off, size_t src_off, size_t n, size_t shard, 
     mb->oneshot = oneshot;
     mb->cmd = MI355_SERVER_RUN;
     const unsigned seq = shmemi.srv.seq++;
+    mb->check = mi355_mailbox_check (mb, seq);
     __atomic_store_n (&mb->seq_head, seq, __ATOMIC_RELEASE);
     __atomic_store_n (&mb->seq_tail, seq, __ATOMIC_RELEASE);
     const double t0 = shmemi_now ();
@@ -1018,8 +1020,6 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
                          int nreduce, int PE_start, int logPE_stride, int PE_size, long *pSync)
 {
     shmemi_init_check (fn);
-    if (shmemi.heap == NULL)
-        shmemi_fatal ("%s: no GPU: this library reduces on the GPU only (SHMEM_BOOTSTRAP_ONLY set?)", fn);
     if (logPE_stride < 0 || logPE_stride > 30 || PE_size < 1 || PE_start < 0 ||
         PE_start + (long) (PE_size - 1) * (1L << logPE_stride) >= shmemi.npes)
         shmemi_fatal ("%s: active set (PE_start %d, logPE_stride %d, PE_size %d) outside the %d PEs",
@@ -1042,11 +1042,13 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
         debug_check (fn, op, dtype, target, source, nreduce, PE_start, logPE_stride, PE_size);
     if (n == 0) {
         begin_call ("barrier-only");
-        /* both barriers of reduce-op.c:230,266 still run */
+        /* both barriers of reduce-op.c:230,266 still run (host only: no GPU work) */
         shmemi_barrier_set (s.start, s.stride, s.size);
         shmemi_barrier_set (s.start, s.stride, s.size);
         return;
     }
+    if (shmemi.heap == NULL)
+        shmemi_fatal ("%s: no GPU: this library reduces on the GPU only (SHMEM_BOOTSTRAP_ONLY set?)", fn);
     if (target == NULL || source == NULL)
         shmemi_fatal ("%s: NULL target or source", fn);
     const size_t nbytes = n * es;

@@ -70,6 +70,7 @@ static void server_quit_nowait (void)
 {
     if (shmemi.srv.running && shmemi.srv.mb != NULL) {
         shmemi.srv.mb->cmd = MI355_SERVER_QUIT;
+        shmemi.srv.mb->check = mi355_mailbox_check (shmemi.srv.mb, shmemi.srv.seq);
         __atomic_store_n (&shmemi.srv.mb->seq_head, shmemi.srv.seq, __ATOMIC_RELEASE);
         __atomic_store_n (&shmemi.srv.mb->seq_tail, shmemi.srv.seq, __ATOMIC_RELEASE);
         shmemi.srv.running = 0;
@@ -621,6 +622,14 @@ static void sigmem_init (void)
  * must agree on every PE (one PE on the fused path and another on the
  * multi-launch one would wait on each other for ever): abort at init, naming
  * the environment variable, when a peer's differ. */
+static void settings_publish (void)
+{
+    seg_info (shmemi.mype)->settings =
+        (struct shmemi_settings) {shmemi.algorithm, shmemi.order, shmemi.debug != 0, shmemi.srv.enabled,
+                                  shmemi.order_chunk, shmemi.fused_max, shmemi.oneshot_max, shmemi.scratch_chunk,
+                                  shmemi.user_size};
+}
+
 static void settings_check (void)
 {
     const struct shmemi_settings *a = &seg_info (shmemi.mype)->settings;
@@ -655,9 +664,7 @@ static void heap_exchange (void)
     SHMEMI_HIP (hipIpcGetMemHandle (&me->heap_handle, shmemi.heap));
     SHMEMI_HIP (hipIpcGetMemHandle (&me->sig_handle, shmemi.sigmem));
     me->heap_size = shmemi.heap_size;
-    me->settings = (struct shmemi_settings) {shmemi.algorithm, shmemi.order, shmemi.debug != 0, shmemi.srv.enabled,
-                                             shmemi.order_chunk, shmemi.fused_max, shmemi.oneshot_max,
-                                             shmemi.scratch_chunk, shmemi.user_size};
+    settings_publish ();
     __atomic_store_n (&me->published, 1, __ATOMIC_RELEASE);
     shmemi_barrier_set (0, 1, shmemi.npes);
     settings_check ();
@@ -1124,7 +1131,9 @@ void pshmem_init (void)
         shmemi.device = -1;
         if (shmemi.npes > 1) {
             bootstrap_attach ();
+            settings_publish ();
             shmemi_barrier_set (0, 1, shmemi.npes);
+            settings_check ();
             if (shmemi.mype == 0) {
                 shm_unlink (shmemi.seg_name);
                 shmemi.seg_unlinked = 1;

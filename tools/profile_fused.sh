@@ -27,6 +27,10 @@ run_pair () {  # $1 = pass name, rest = rocprofv3 options
 run_pair trace --kernel-trace --stats || exit 1
 run_pair fetch --pmc FETCH_SIZE || exit 1
 run_pair write --pmc WRITE_SIZE || exit 1
+# VMEM read instructions per dispatch: the fold's loads are known, the rest
+# are flag polls (one wave instruction each, one small uncached request):
+# separates the fetch bytes of polling from the sources'
+run_pair vmem --pmc SQ_INSTS_VMEM_RD SQ_WAVES || exit 1
 cp "$(find "$OUT/trace" -name '*kernel_stats.csv' -print -quit)" "$DST/rocprof_kernel_stats_fused_pe0.csv"
 grep '^{' "$OUT/trace.pe0.log" > "$DST/fused_bench_under_rocprof.json" || true
 for sz in 65536 1048576; do :; done
@@ -34,15 +38,18 @@ python3 - "$OUT" "$DST" <<'PY'
 import csv, glob, json, os, sys
 out, dst = sys.argv[1], sys.argv[2]
 res = {}
-for counter, d in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+for counter, d in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write"), ("SQ_INSTS_VMEM_RD", "vmem"),
+                   ("SQ_WAVES", "vmem")):
     f = glob.glob(os.path.join(out, d, "**", "*counter_collection.csv"), recursive=True)[0]
     per = {}
     for r in csv.DictReader(open(f)):
         if "fused_allreduce<0, double>" in r["Kernel_Name"] and r["Counter_Name"] == counter:
-            per.setdefault(int(r["Grid_Size"]), []).append(float(r["Counter_Value"]) * 1024)
+            scale = 1024 if counter.endswith("_SIZE") else 1
+            per.setdefault(int(r["Grid_Size"]), []).append(float(r["Counter_Value"]) * scale)
     for g, v in per.items():
         v.sort()
-        res.setdefault(str(g), {})[counter] = {"median_bytes": v[len(v) // 2], "dispatches": len(v)}
+        key = "median_bytes" if counter.endswith("_SIZE") else "median"
+        res.setdefault(str(g), {})[counter] = {key: v[len(v) // 2], "dispatches": len(v)}
 json.dump({"kernel": "fused_allreduce<sum,double> on PE 0 of 2 sharing the GPU, keyed by grid size (threads)",
            "by_grid": res, "note": "FETCH_SIZE raw (double it for wide streaming reads, MI355X_MICROARCH.md); "
            "the one-shot fold reads both PEs' whole sources, the two-shot reads both shards and the peer's shard"},
