@@ -403,6 +403,10 @@ def main():
     # a PE that never arrives ends the bench within two minutes with the
     # library's diagnostic (the library default, 600 s, suits long jobs)
     os.environ.setdefault("SHMEM_BARRIER_TIMEOUT", "120")
+    # N > 1: ranks 1.. wait at init for rank 0, which first times the CPU
+    # baseline (and, like every rank, waits for its persistent-leg child, at
+    # most 240 s): the bootstrap wait covers both
+    os.environ.setdefault("SHMEM_BOOTSTRAP_TIMEOUT", "600")
     shm = shmem_reduce.Shmem()
     shm.init()
     # the init self-test found peer heap reads broken: the library runs the

@@ -502,13 +502,14 @@ __device__ void server_next(const MI355FusedArgs &a, MI355ServerMailbox *mb, uns
                 __builtin_amdgcn_s_sleep(2);
             }
             if (idle && lane == 1) v = MI355_SERVER_QUIT;  // dword 1: cmd
-            if (idle) {  // the broadcast's check word covers the QUIT
+            if (idle) {  // the broadcast's check word covers the QUIT (every lane shuffles: uniform)
                 unsigned x = lane >= 1 && lane <= 11 ? v : 0u;
                 x ^= __shfl_xor(x, 8, 16);
                 x ^= __shfl_xor(x, 4, 16);
                 x ^= __shfl_xor(x, 2, 16);
                 x ^= __shfl_xor(x, 1, 16);
-                if (lane == 12) v = __shfl(x, 0) ^ (seq * 0x9E3779B1u);
+                const unsigned check = __shfl(x, 0) ^ (seq * 0x9E3779B1u);
+                if (lane == 12) v = check;
             }
             // broadcast: the call (dwords 1-14), then head and tail
             if (lane >= 1 && lane < 15) st_sys_u32(slot + lane, v);

@@ -220,7 +220,10 @@ static void bootstrap_attach (void)
     const size_t total = hdr + info + 2 * flags; /* barrier counts, SHMEM_DEBUG check counts */
     seg_name (shmemi.seg_name, sizeof shmemi.seg_name);
 
-    const double deadline = now_s () + shmemi.barrier_timeout;
+    /* SHMEM_BOOTSTRAP_TIMEOUT: how long a PE waits for PE 0 to create the
+     * segment (a launcher may start PE 0 late; default: the barrier timeout) */
+    static const char *bt_env[] = {"SHMEM_BOOTSTRAP_TIMEOUT", NULL};
+    const double deadline = now_s () + (double) env_long (bt_env, (long) shmemi.barrier_timeout);
     if (shmemi.mype == 0) {
         shm_unlink (shmemi.seg_name); /* stale leftover of a crashed job */
         int fd = shm_open (shmemi.seg_name, O_CREAT | O_EXCL | O_RDWR, 0600);

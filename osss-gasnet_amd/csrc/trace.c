@@ -118,7 +118,6 @@ void shmemi_trace_show_info (void)
     static const char *const vars[][2] = {
         {"{SHMEM,SMA}_VERSION", "print the library version (INIT trace)"},
         {"{SHMEM,SMA}_INFO", "print this list"},
-        {"SHMEM_DEBUG", "check pSync holds SHMEM_SYNC_VALUE on entry"},
         {"SHMEM_LOG_LEVELS", "trace levels to enable (names separated by , : ; or \"all\")"},
         {"SHMEM_LOG_FILE", "append trace lines to this file instead of stderr"},
         {"SHMEM_PE, SHMEM_NPES", "PE identity (else RANK/WORLD_SIZE, OMPI_COMM_WORLD_*, PMI_*)"},
@@ -136,6 +135,10 @@ void shmemi_trace_show_info (void)
         {"SHMEM_FUSED_MAX_BYTES", "largest message for the one-launch fused reduction (default 1M)"},
         {"SHMEM_ONESHOT_MAX_BYTES", "largest fused message folded one-shot, not reduce-scatter + all-gather (default 64K)"},
         {"SHMEM_BARRIER_TIMEOUT", "seconds before a barrier wait aborts the job (default 600)"},
+        {"SHMEM_BOOTSTRAP_TIMEOUT", "seconds a PE waits at init for PE 0 to create the job's segment (default: "
+                                    "SHMEM_BARRIER_TIMEOUT)"},
+        {"SHMEM_DEBUG", "1: check pSync and exchange every collective's arguments between its members, aborting "
+                        "with the first differing field"},
         {"SHMEM_ENTRY_SYNC", "1: every call starts with hipDeviceSynchronize"},
         {"SHMEM_PEER_ACQUIRE", "1/0: system-scope L2 acquire before reading peers' buffers (default: on if a peer is on another GPU)"},
     };

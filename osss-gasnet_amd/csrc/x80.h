@@ -55,26 +55,39 @@ __device__ __forceinline__ u128 sub(u128 a, u128 b) {
     return r;
 }
 __device__ __forceinline__ bool lt(u128 a, u128 b) {
-    return a.hi < b.hi || (a.hi == b.hi && a.lo < b.lo);
+    return (a.hi < b.hi) | ((a.hi == b.hi) & (a.lo < b.lo));
 }
-__device__ __forceinline__ u128 shl(u128 a, int s) {  // 0 <= s < 128
-    if (s == 0) return a;
-    if (s >= 64) return mk(a.lo << (s - 64), 0);
-    return mk((a.hi << s) | (a.lo >> (64 - s)), a.lo << s);
+// Everything below is straight-line code (selects, no branches): the
+// general path runs with whole waves, and its earlier branchy form -- early
+// returns per encoding class, shifts with `if` per range -- gave
+// nondeterministic one- and two-ulp errors on gfx950 in a kernel that ran it
+// on every lane (tools/x80_lane_probe.hip: ~0.7 % of 3-operand x87 products
+// of random encodings, varying from run to run, while the straight-line fast
+// path matched the host x87 on every element).
+__device__ __forceinline__ int clz64(uint64_t x) { return x == 0 ? 64 : __builtin_clzll(x); }
+// a >> s, a << s and the bits of a below position s, for s in [0, 255]
+__device__ __forceinline__ u128 shr(u128 a, int s) {
+    const int k = s & 63;
+    const uint64_t hk = a.hi >> k, lk = a.lo >> k;
+    const uint64_t in = (a.hi << 1) << (63 - k);  // a.hi << (64 - k); 0 for k = 0
+    const bool ge64 = s >= 64, ge128 = s >= 128;
+    return mk(ge64 ? 0 : hk, ge128 ? 0 : ge64 ? hk : (lk | in));
 }
-__device__ __forceinline__ u128 shr(u128 a, int s) {  // 0 <= s < 128
-    if (s == 0) return a;
-    if (s >= 64) return mk(0, a.hi >> (s - 64));
-    return mk(a.hi >> s, (a.lo >> s) | (a.hi << (64 - s)));
+__device__ __forceinline__ u128 shl(u128 a, int s) {
+    const int k = s & 63;
+    const uint64_t hk = a.hi << k, lk = a.lo << k;
+    const uint64_t in = (a.lo >> 1) >> (63 - k);  // a.lo >> (64 - k); 0 for k = 0
+    const bool ge64 = s >= 64, ge128 = s >= 128;
+    return mk(ge128 ? 0 : ge64 ? lk : (hk | in), ge64 ? 0 : lk);
 }
-// Bits of a below bit position s (s in [1,128]).
 __device__ __forceinline__ u128 low_bits(u128 a, int s) {
-    if (s >= 128) return a;
-    if (s >= 64) return mk(a.hi & ((s == 64) ? 0 : ((~0ull) >> (128 - s))), a.lo);
-    return mk(0, a.lo & ((~0ull) >> (64 - s)));
+    const int k = s & 63;
+    const uint64_t m = (~0ull >> 1) >> (63 - k);  // the low k bits
+    const bool ge64 = s >= 64, ge128 = s >= 128;
+    return mk(ge128 ? a.hi : ge64 ? (a.hi & m) : 0, ge64 ? a.lo : (a.lo & m));
 }
-__device__ __forceinline__ int msb(u128 a) {  // a != 0
-    return a.hi ? 127 - __builtin_clzll(a.hi) : 63 - __builtin_clzll(a.lo);
+__device__ __forceinline__ int msb(u128 a) {  // -1 for 0
+    return a.hi != 0 ? 127 - clz64(a.hi) : 63 - clz64(a.lo);
 }
 
 __device__ __forceinline__ int efield(const x80 &a) { return a.se & 0x7FFF; }
@@ -126,12 +139,9 @@ __device__ __forceinline__ x80 quiet(x80 a) {
 // NaN result of an operation with at least one NaN operand.
 __device__ __forceinline__ x80 nan_result(const x80 &a, const x80 &b) {
     const bool na = is_nan(a), nb = is_nan(b);
-    if (na && nb) {
-        const uint64_t ma = a.m | 0x4000000000000000ull, mb = b.m | 0x4000000000000000ull;
-        if (ma != mb) return quiet(pick(ma > mb, a, b));
-        return quiet(pick(sign(a) == 0, a, b));
-    }
-    return quiet(pick(na, a, b));
+    const uint64_t ma = a.m | 0x4000000000000000ull, mb = b.m | 0x4000000000000000ull;
+    const bool take_a = (na & nb) ? (ma != mb ? ma > mb : sign(a) == 0) : na;
+    return quiet(pick(take_a, a, b));
 }
 
 __device__ __forceinline__ int exp_of(const x80 &a) {  // value = m * 2^E
@@ -140,49 +150,32 @@ __device__ __forceinline__ int exp_of(const x80 &a) {  // value = m * 2^E
 }
 
 // Round W * 2^Ew (+ sticky fraction below W's last bit) to 64 bits, RNE,
-// with gradual underflow and overflow to infinity.
+// with gradual underflow and overflow to infinity. W != 0 on the lanes
+// whose result is used (callers select a special result for the others).
 __device__ __forceinline__ x80 round_pack(int s, u128 W, int Ew, bool sticky, const x80 &padsrc) {
     const int L = msb(W);
     int E = Ew + L - 63;  // exponent with the leading bit at position 63
     int shift = L - 63;
-    if (E < kEmin) {
-        shift += kEmin - E;
-        E = kEmin;
-    }
-    uint64_t m;
-    if (shift <= 0) {
-        m = shl(W, -shift).lo;  // exact (sticky bits, if any, are < half an ulp: round down)
-    } else {
-        u128 rem;
-        if (shift >= 128) {
-            m = 0;
-            rem = W;
-        } else {
-            m = shr(W, shift).lo;
-            rem = low_bits(W, shift);
-        }
-        bool up;
-        if (shift > 128) {
-            up = false;  // everything is below half an ulp
-        } else {
-            const u128 half = shl(mk(0, 1), shift - 1);
-            if (lt(half, rem)) up = true;
-            else if (lt(rem, half)) up = false;
-            else up = sticky || (m & 1);  // tie: to even unless something lies beyond
-        }
-        if (up) {
-            m += 1;
-            if (m == 0) {  // carried out of 64 bits
-                m = 0x8000000000000000ull;
-                E += 1;
-            }
-        }
-    }
-    if (m == 0) return make(s, 0, 0, padsrc);
-    if ((m >> 63) == 0) return make(s, 0, m, padsrc);  // denormal (E == kEmin)
+    const bool under = E < kEmin;
+    shift += under ? kEmin - E : 0;
+    E = under ? kEmin : E;
+    // shift <= 0: exact (W < 2^64 there; sticky bits, if any, are below half an ulp)
+    const uint64_t m_exact = W.lo << ((shift < 0 ? -shift : 0) & 63);
+    // shift > 0: the bits shifted out decide; beyond 128 everything is below half an ulp
+    const int rs = shift <= 0 ? 0 : shift > 255 ? 255 : shift;
+    const u128 rem = low_bits(W, rs);
+    const u128 half = shl(mk(0, 1), rs > 0 ? rs - 1 : 0);
+    uint64_t m = shift > 0 ? shr(W, rs).lo : m_exact;
+    const bool tie = (rem.hi == half.hi) & (rem.lo == half.lo);
+    const bool up = (shift > 0) & (rs <= 128) & (lt(half, rem) | (tie & (sticky | ((m & 1) != 0))));
+    m += up ? 1 : 0;
+    const bool wrap = up & (m == 0);  // carried out of 64 bits
+    m = wrap ? 0x8000000000000000ull : m;
+    E += wrap ? 1 : 0;
     const int ef = E + kEOff;
-    if (ef >= kEmaxField) return make(s, kEmaxField, 0x8000000000000000ull, padsrc);
-    return make(s, ef, m, padsrc);
+    const bool zero = m == 0, denormal = (m >> 63) == 0;  // denormal: E == kEmin
+    const bool ovf = !denormal & (ef >= kEmaxField);
+    return make(s, (zero | denormal) ? 0 : ovf ? kEmaxField : ef, zero ? 0 : ovf ? 0x8000000000000000ull : m, padsrc);
 }
 
 // Round-to-nearest-even of a 64-bit significand m with the 64 bits below it
@@ -206,9 +199,10 @@ __device__ __forceinline__ bool fast_operand(const x80 &a) {
 
 // The fast paths run when every active lane of the wave can take them (one
 // vote, a uniform branch); otherwise the whole wave takes the general path.
-// (Diverging per lane between the two paths gave nondeterministic one-ulp
-// errors in the general path's results on gfx950 -- test_longdouble_
-// random_encodings -- so the choice is per wave.)
+// (Round 2 attributed nondeterministic one-ulp errors to lanes diverging
+// between the two paths; round 3 found them in the then-branchy general path
+// itself, which is now straight-line. The vote stays: it keeps the common
+// case to the fast path's instructions only.)
 __device__ __forceinline__ bool add_fast(const x80 &a, const x80 &b, x80 &r) {
     // One straight-line path for effective addition and subtraction (every
     // choice a select; a branchy form diverged per lane on the operands'
@@ -253,43 +247,33 @@ __device__ __forceinline__ bool add_fast(const x80 &a, const x80 &b, x80 &r) {
     return ok;
 }
 
+// The general paths: every encoding class, straight-line -- the finite
+// result is computed for every lane and the special cases (in the 387's
+// priority: unsupported encoding, NaN, infinity, zeros) replace it by selects.
 __device__ __forceinline__ x80 add_general(const x80 &a, const x80 &b) {
-    if (unsupported(a) || unsupported(b)) return indefinite(a);
-    if (is_nan(a) || is_nan(b)) return nan_result(a, b);
     const int sa = sign(a), sb = sign(b);
-    if (is_inf(a) || is_inf(b)) {
-        if (is_inf(a) && is_inf(b) && sa != sb) return indefinite(a);
-        return pick(is_inf(a), a, make(sb, kEmaxField, 0x8000000000000000ull, a));
-    }
-    if (is_zero(a) && is_zero(b)) return make(sa & sb, 0, 0, a);
-    // order by magnitude: A >= B
+    const int ia = is_inf(a), ib = is_inf(b), na = is_nan(a), nb = is_nan(b);  // ints: evaluated without branches
+    const int ua = unsupported(a), ub = unsupported(b), za = is_zero(a), zb = is_zero(b);
+    // finite: order by magnitude, A >= B; align B under A with a sticky bit
     const int ea = exp_of(a), eb = exp_of(b);
-    const bool a_big = (ea > eb) || (ea == eb && a.m >= b.m);
+    const bool a_big = (ea > eb) | ((ea == eb) & (a.m >= b.m));
     const int EA = a_big ? ea : eb, EB = a_big ? eb : ea;
     const uint64_t MA = a_big ? a.m : b.m, MB = a_big ? b.m : a.m;
     const int sA = a_big ? sa : sb, sB = a_big ? sb : sa;
-    const u128 WA = shl(mk(0, MA), 62);
-    u128 WB = shl(mk(0, MB), 62);
-    bool sticky = false;
-    const int d = EA - EB;
-    if (d > 0) {
-        if (d >= 128) {
-            sticky = !is0(WB);
-            WB = mk(0, 0);
-        } else {
-            sticky = !is0(low_bits(WB, d));
-            WB = shr(WB, d);
-        }
-    }
-    u128 W;
-    if (sA == sB) {
-        W = add(WA, WB);
-    } else {
-        W = sub(WA, WB);
-        if (sticky) W = sub(W, mk(0, 1));
-    }
-    if (is0(W) && !sticky) return make(0, 0, 0, a);  // exact cancellation: +0
-    return round_pack(sA, W, EA - 62, sticky, a);
+    const u128 WA = shl(mk(0, MA), 62), WB0 = shl(mk(0, MB), 62);  // 2 guard bits above, 62 below
+    const int d = EA - EB > 255 ? 255 : EA - EB;
+    const int sticky = !is0(low_bits(WB0, d));
+    const u128 WB = shr(WB0, d);
+    const u128 dif = sub(WA, WB);
+    const u128 W = sA == sB ? add(WA, WB) : sticky ? sub(dif, mk(0, 1)) : dif;
+    x80 r = round_pack(sA, W, EA - 62, sticky, a);
+    const int cancel = is0(W);
+    r = pick(cancel & !sticky, make(0, 0, 0, a), r);                          // exact cancellation: +0
+    r = pick(za & zb, make(sa & sb, 0, 0, a), r);
+    const x80 inf_r = pick(ia, a, make(sb, kEmaxField, 0x8000000000000000ull, a));
+    r = pick(ia | ib, pick(ia & ib & (sa != sb), indefinite(a), inf_r), r);  // inf - inf: invalid
+    r = pick(na | nb, nan_result(a, b), r);
+    return pick(ua | ub, indefinite(a), r);
 }
 
 __device__ __forceinline__ x80 add(const x80 &a, const x80 &b) {
@@ -319,17 +303,16 @@ __device__ __forceinline__ bool mul_fast(const x80 &a, const x80 &b, x80 &r) {
 }
 
 __device__ __forceinline__ x80 mul_general(const x80 &a, const x80 &b) {
-    if (unsupported(a) || unsupported(b)) return indefinite(a);
-    if (is_nan(a) || is_nan(b)) return nan_result(a, b);
     const int s = sign(a) ^ sign(b);
-    const bool ia = is_inf(a), ib = is_inf(b);
-    if (ia || ib) {
-        if (is_zero(a) || is_zero(b)) return indefinite(a);
-        return make(s, kEmaxField, 0x8000000000000000ull, a);
-    }
-    if (is_zero(a) || is_zero(b)) return make(s, 0, 0, a);
+    const int za = is_zero(a), zb = is_zero(b), ia = is_inf(a), ib = is_inf(b);  // ints: no branches
+    const int na = is_nan(a), nb = is_nan(b), ua = unsupported(a), ub = unsupported(b);
     const u128 P = mk(__umul64hi(a.m, b.m), a.m * b.m);
-    return round_pack(s, P, exp_of(a) + exp_of(b), false, a);
+    x80 r = round_pack(s, P, exp_of(a) + exp_of(b), false, a);
+    r = pick(za | zb, make(s, 0, 0, a), r);
+    const x80 inf_r = pick(za | zb, indefinite(a), make(s, kEmaxField, 0x8000000000000000ull, a));  // 0 x inf
+    r = pick(ia | ib, inf_r, r);
+    r = pick(na | nb, nan_result(a, b), r);
+    return pick(ua | ub, indefinite(a), r);
 }
 
 __device__ __forceinline__ x80 mul(const x80 &a, const x80 &b) {

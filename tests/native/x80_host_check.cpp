@@ -115,5 +115,27 @@ int main(int argc, char **argv) {
         }
     }
     printf("compare: %ld pairs, %ld mismatches\n", nc, badc);
-    return bad != 0 || badc != 0;
+    // the general paths (x80d::add_general / mul_general, straight-line) on
+    // operands of every encoding class, against the host's x87 + and *
+    long ng = 0, badg = 0;
+    for (long i = 0; i < per; ++i) {
+        const int e0 = 1 + (int)(g() % 0x7FFE);
+        x80 a = any(e0), b = any(g() % 2 ? e0 + (int)(g() % 140) - 70 : 1 + (int)(g() % 0x7FFE));
+        if (b.se == 0 && b.m == 0 && g() % 2) b = a;
+        long double la, lb;
+        memset(&la, 0, sizeof la);
+        memset(&lb, 0, sizeof lb);
+        memcpy(&la, &a, 10);
+        memcpy(&lb, &b, 10);
+        volatile long double s = la + lb, p = la * lb;
+        ++ng;
+        if (!same(x80d::add_general(a, b), s) || !same(x80d::mul_general(a, b), p)) {
+            if (badg < 5)
+                printf("general mismatch: %04x %016llx, %04x %016llx\n", a.se, (unsigned long long)a.m, b.se,
+                       (unsigned long long)b.m);
+            ++badg;
+        }
+    }
+    printf("general: %ld pairs, %ld mismatches\n", ng, badg);
+    return bad != 0 || badc != 0 || badg != 0;
 }

@@ -76,7 +76,7 @@ def test_coherence_selftest_runs_and_passes():
     for rc, out in zip(rcs, outs):
         assert rc == 0, out[-2000:]
         coh = parse(out, "COH")[0]
-        assert coh[:2] == ["1", "1"] and coh[3] == "0", out  # ran, passed; P2P (auto) kept
+        assert coh[:2] == ["1", "1"] and coh[4] == "0", out  # ran, passed; P2P (auto) kept
         assert parse(out, "EXACT")[0] == ["True"] and parse(out, "SCHED")[0] == ["fused-twoshot"], out
 
 

@@ -23,3 +23,4 @@ def test_x80_matches_host_x87(tmp_path):
     assert out.returncode == 0, out.stdout + out.stderr
     assert "3000000 pairs, 0 mismatches" in out.stdout, out.stdout
     assert "compare: 500000 pairs, 0 mismatches" in out.stdout, out.stdout
+    assert "general: 500000 pairs, 0 mismatches" in out.stdout, out.stdout

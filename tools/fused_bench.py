@@ -62,10 +62,10 @@ def main():
         served0, launched0 = shm.persistent_stats()
         t0 = time.perf_counter()
         loop(dst, src, n, 0, 0, npes, None, shm._psync_ptr, calls)
+        info = shm.last_call_info()  # before max_over_pes (a reduction of its own)
         shm.sync()
         t = max_over_pes(time.perf_counter() - t0) / calls
         served1, launched1 = shm.persistent_stats()
-        info = shm.last_call_info()
         shm.barrier_all()
         shm.kernel_timing(True)
         loop(dst, src, n, 0, 0, npes, None, shm._psync_ptr, calls)
