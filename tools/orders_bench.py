@@ -5,7 +5,7 @@ shape of an N-PE call on 256 MiB per PE (N sources of 256/N MiB; orders
 writes N outputs, the fold one). Kernel time from HIP event stamps (median of
 reps). Measurement tool: prints one JSON line per (type, N).
 
-usage: orders_bench.py [reps]
+usage: orders_bench.py [reps] [dtype,dtype,...]
 """
 import ctypes
 import json
@@ -19,6 +19,7 @@ sys.path.insert(0, os.path.join(ROOT, "osss-gasnet_amd"))
 import shmem_reduce  # noqa: E402
 
 reps = int(sys.argv[1]) if len(sys.argv) > 1 else 20
+only = sys.argv[2].split(",") if len(sys.argv) > 2 else None
 S = 256 << 20
 os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(2 * S + (64 << 20)))
 os.environ.setdefault("SHMEM_DEVICE_SCRATCH_SIZE", "3M")
@@ -61,6 +62,8 @@ def timed(launch):
 
 for op, dtype in [("sum", "double"), ("sum", "float"), ("max", "float"), ("min", "double"), ("prod", "complexd"),
                   ("sum", "complexf"), ("sum", "longdouble"), ("prod", "longdouble"), ("max", "longdouble")]:
+    if only and dtype not in only:
+        continue
     es = np.dtype(shmem_reduce.NP[dtype]).itemsize
     fill(dtype)
     for npes in (2, 4, 8):
