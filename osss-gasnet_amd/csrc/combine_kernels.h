@@ -402,6 +402,31 @@ inline int device_cus() {
 // kBlocksPerCU resident blocks per CU (grid-stride covers the rest).
 constexpr int kBlocksPerCU = 8;
 
+// Blocks of `fn` one CU holds at once (occupancy API, cached per kernel).
+// A grid-stride launch larger than what is resident runs in rounds, the last
+// one partly empty. The VALU-bound x87 folds cap their grids at this (the
+// every-member x87 sum at 8 sources: 80 VGPRs, 6 blocks per CU instead of
+// the 8 asked: 271 -> 263 us at 8 x 32 MiB, profiles/r03/orders_grid_cap.jsonl).
+// The HBM-bound folds do not: capped at their residency (the 8-source fold
+// holds 152 VGPRs, 3 blocks per CU) they ran 1-4 % slower -- the queued
+// blocks refill CUs as others finish.
+inline int resident_blocks(const void *fn) {
+    static const void *keys[512];
+    static int vals[512];
+    static int used = 0;
+    for (int i = 0; i < used; ++i)
+        if (keys[i] == fn) return vals[i];
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBlock, 0) != hipSuccess || n < 1) n = 1;
+    (void)hipGetLastError();
+    if (used < 512) {
+        keys[used] = fn;
+        vals[used] = n;
+        ++used;
+    }
+    return n;
+}
+
 inline unsigned grid_for(uint64_t units_per_block_pass, uint64_t units, int blocks_per_cu = kBlocksPerCU) {
     uint64_t want = (units + units_per_block_pass - 1) / units_per_block_pass;
     uint64_t cap = (uint64_t)device_cus() * blocks_per_cu;
@@ -446,6 +471,7 @@ template <int OP, int NSRC, typename T> struct OrdersShape {
     static constexpr bool cplx = std::is_same<T, cplxf>::value || std::is_same<T, cplxd>::value;
     static constexpr bool sel = (OP == MI355_OP_MIN || OP == MI355_OP_MAX) && NSRC >= 5;
     using S = Shape<NSRC, T>;
+    static constexpr bool alu_heavy = S::alu_heavy;
     // 3-4 sources with compare-select chains or complex products: the sum's
     // shape there (one block per CU) leaves too few waves to hide their ALU
     // latency; eight blocks per CU
@@ -500,8 +526,12 @@ int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, b
         using S = Shape<NSRC, T>;
         p.nvec = n / V;
         p.tail = (uint32_t)(n % V);
-        const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, S::blocks_per_cu);
-        return launch(combine_vec<OP, T, NSRC, S::unroll, S::policy>, dim3(grid), st, p, final);
+        auto k = combine_vec<OP, T, NSRC, S::unroll, S::policy>;
+        const int bpc = !S::alu_heavy || S::blocks_per_cu < resident_blocks((const void *)k)
+                            ? S::blocks_per_cu
+                            : resident_blocks((const void *)k);
+        const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, bpc);
+        return launch(k, dim3(grid), st, p, final);
     }
     p.nvec = n;
     p.tail = 0;
@@ -534,11 +564,15 @@ int launch_orders_fixed(void *const *dsts, const void *const *srcs, size_t n, hi
         using S = OrdersShape<OP, NSRC, T>;
         p.nvec = n / V;
         p.tail = (uint32_t)(n % V);
-        const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, S::blocks_per_cu);
         bool all = true;
         for (int k = 0; k < NSRC; ++k) all = all && dsts[k] != nullptr;
-        if (all) return launch(combine_orders_vec<OP, T, NSRC, S::unroll, S::policy, true>, dim3(grid), st, p);
-        return launch(combine_orders_vec<OP, T, NSRC, S::unroll, S::policy, false>, dim3(grid), st, p);
+        auto k = all ? combine_orders_vec<OP, T, NSRC, S::unroll, S::policy, true>
+                     : combine_orders_vec<OP, T, NSRC, S::unroll, S::policy, false>;
+        const int bpc = !S::alu_heavy || S::blocks_per_cu < resident_blocks((const void *)k)
+                            ? S::blocks_per_cu
+                            : resident_blocks((const void *)k);
+        const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, bpc);
+        return launch(k, dim3(grid), st, p);
     }
     p.nvec = n;
     p.tail = 0;

@@ -186,9 +186,9 @@ __device__ __forceinline__ bool round_up(uint64_t m, uint64_t rem, bool sticky) 
 }
 
 // Fast path of add/mul: both operands normal with exponent fields in
-// [1, kFastMax], so every result is normal or an exact zero and no rounding
-// can overflow; the rest (zeros, denormals, infinities, NaNs, unsupported
-// encodings, near-overflow exponents, alignment shifts beyond 64 bits,
+// [1, kFastMax], so no rounding can overflow; the rest (zeros, denormals,
+// infinities, NaNs, unsupported encodings, near-overflow exponents,
+// alignment shifts beyond 63 bits, differences whose high 64 bits cancel,
 // results that would be denormal) takes the general path. Both paths round
 // the exact result once, so they agree bit for bit where both apply.
 constexpr int kFastMax = kEmaxField - 3;
@@ -204,46 +204,51 @@ __device__ __forceinline__ bool fast_operand(const x80 &a) {
 // itself, which is now straight-line. The vote stays: it keeps the common
 // case to the fast path's instructions only.)
 __device__ __forceinline__ bool add_fast(const x80 &a, const x80 &b, x80 &r) {
-    // One straight-line path for effective addition and subtraction (every
-    // choice a select; a branchy form diverged per lane on the operands'
-    // signs, carries and cancellations, and the every-member fold ran both
-    // sides of every branch): B aligned under A = MA:0 in 128 bits, exactly;
-    // A + B, or A + (~B + 1) when the signs differ (A >= B, so no borrow out);
-    // then one normalization: right by one on a carry out of the addition,
-    // left by the leading zeros after a subtraction; one rounding.
-    const int ea = efield(a), eb = efield(b);
-    const bool a_big = (ea > eb) | ((ea == eb) & (a.m >= b.m));
-    const int EA = a_big ? ea : eb;
-    const int d = a_big ? ea - eb : eb - ea;
+    // Straight-line: every choice a select. B (the smaller magnitude) is
+    // aligned under A = MA:0 as Bh:Bl (exact: the fast path takes alignment
+    // shifts up to 63); A + B or A - B in 128 bits; one normalization (right
+    // by one on a carry out of the addition, left by the leading zeros of the
+    // high word after a subtraction -- a difference whose high word cancels
+    // entirely takes the general path); one round to nearest even, as a carry
+    // out of an addition. Operands normal with fields in [1, kFastMax] and a
+    // normal result, else not ok.
+    const int ea = a.se & 0x7FFF, eb = b.se & 0x7FFF;
+    const int d = ea - eb;
+    const bool a_big = (d > 0) | ((d == 0) & (a.m >= b.m));
     const uint64_t MA = a_big ? a.m : b.m, MB = a_big ? b.m : a.m;
-    const int sa = sign(a), sb = sign(b);
-    const int sA = a_big ? sa : sb;
-    const bool sub = sa != sb;
-    const int dd = d < 64 ? d : 64;
-    const uint64_t Bh = dd == 64 ? 0 : MB >> (dd & 63);
-    const uint64_t Bl = dd == 0 ? 0 : MB << ((64 - dd) & 63);  // dd = 64: MB << 0 = MB
+    const int EA = ea > eb ? ea : eb;
+    const int dd = d < 0 ? -d : d;
+    const int k = dd < 63 ? dd : 63;
+    const uint64_t Bh = MB >> k;
+    const uint64_t Bl = (MB << 1) << (63 - k);  // MB << (64 - k): the bits shifted out; 0 for k = 0
+    const bool sub = ((a.se ^ b.se) & 0x8000) != 0;
+    // A + B: hi:lo = MA + Bh : Bl, carry out of hi; A - B: MA:0 - Bh:Bl
+    const uint64_t sum_hi = MA + Bh;
+    const bool carry = !sub & (sum_hi < MA);
     const uint64_t lo = sub ? 0 - Bl : Bl;
-    const uint64_t hi = MA + (sub ? ~Bh + (Bl == 0 ? 1 : 0) : Bh);
-    const bool carry = !sub & (hi < MA);
-    const bool zero = sub & (hi == 0) & (lo == 0);  // exact cancellation: +0
-    // leading zeros of hi:lo after a subtraction (0 after an addition)
-    const int lz = !sub ? 0 : hi != 0 ? __builtin_clzll(hi) : 64 + (lo != 0 ? __builtin_clzll(lo) : 63);
-    const int l = lz & 63;
-    // hi:lo << lz (lz in [0, 127]) or >> 1 (carry: the 129th bit comes back in at the top)
-    const uint64_t sh_hi = lz >= 64 ? lo << l : l == 0 ? hi : (hi << l) | (lo >> (64 - l));
-    const uint64_t sh_lo = lz >= 64 ? 0 : lo << l;
-    const uint64_t nhi = carry ? (hi >> 1) | 0x8000000000000000ull : sh_hi;
-    const uint64_t nlo = carry ? (lo >> 1) | (hi << 63) : sh_lo;
-    const bool sticky = carry & ((lo & 1) != 0);
+    const uint64_t hi = sub ? MA - Bh - (Bl != 0 ? 1 : 0) : sum_hi;
+    const int lz = sub ? __builtin_clzll(hi | 1) : 0;  // hi == 0: not ok below
+    // both normalizations computed, then selected (pinned in registers: left to
+    // itself the compiler sinks each into a divergent branch of its own)
+    uint64_t rh = (hi >> 1) | 0x8000000000000000ull, rl = (lo >> 1) | (hi << 63);
+    uint64_t lh = (hi << lz) | ((lo >> 1) >> (63 - lz)), ll = lo << lz;
+    asm volatile("" : "+v"(rh), "+v"(rl), "+v"(lh), "+v"(ll));
+    const uint64_t nhi = carry ? rh : lh;
+    const uint64_t nlo = carry ? rl : ll;
+    const uint64_t sticky = carry ? (lo & 1) : 0;
     int E = EA + (carry ? 1 : 0) - lz;
-    const bool up = round_up(nhi, nlo, sticky);
+    // round to nearest even: above half an ulp, or at half with a sticky bit or an odd last bit
+    const bool up = round_up(nhi, nlo, sticky != 0);
     uint64_t m = nhi + (up ? 1 : 0);
-    const bool wrap = up & (m == 0);
+    const bool wrap = m == 0;  // nhi = ~0 rounded up
     m = wrap ? 0x8000000000000000ull : m;
     E += wrap ? 1 : 0;
-    const int fa = fast_operand(a), fb = fast_operand(b);  // ints: evaluated without branches
-    const bool ok = fa & fb & (d <= 64) & (zero | (E >= 1));
-    r = zero ? make(0, 0, 0, a) : make(sA, E, m, a);
+    const unsigned fa = (unsigned)(ea - 1) < (unsigned)kFastMax && (a.m >> 63) != 0;
+    const unsigned fb = (unsigned)(eb - 1) < (unsigned)kFastMax && (b.m >> 63) != 0;
+    const bool ok = fa & fb & (dd <= 63) & (hi != 0) & ((unsigned)(E - 1) < (unsigned)kFastMax);
+    r = a;
+    r.m = m;
+    r.se = (uint16_t)(((a_big ? a.se : b.se) & 0x8000) | E);
     return ok;
 }
 
