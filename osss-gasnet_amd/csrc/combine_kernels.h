@@ -230,24 +230,75 @@ __device__ __forceinline__ void x80_orders_vector(const OrdersParams &p, uint64_
     // Member 1's order (s1, s0, s2, ...) gives member 0's value (s0, s1, s2,
     // ...): x87 + and * commute, NaN and signed-zero rules included, and the
     // rest of the two chains is the same -- one chain fewer per element.
+    // Fast chains, unrolled over the members (operands picked at compile
+    // time), on the unpacked form of x80.h's add_fast_u/mul_fast_u: the
+    // sources' domain is checked once (x80d::chain_operand: exponents that
+    // keep every step in range), each step checks only its alignment,
+    // cancellation and rounding, and
+    // one wave vote decides for all the element's chains: every lane stayed
+    // in the fast domain, or the whole wave redoes the chains on the general
+    // path (the same x87 results either way; the choice is wave-uniform).
+    x80d::xu u[NSRC], res[NSRC];
+    int ok = 1;
+#pragma unroll
+    for (int k = 0; k < NSRC; ++k) {
+        u[k] = x80d::unpack(v[k]);
+        ok &= x80d::chain_operand<OP, NSRC - 1>(v[k]);
+    }
+#pragma unroll
+    for (int q = 0; q < NSRC; ++q) {
+        if (q == 1) {
+            res[1] = res[0];
+            continue;
+        }
+        x80d::xu a = u[q];
+        // one chain after the other: interleaved by the scheduler, the
+        // chains' select masks outgrow the SGPRs and spill to VGPR lanes
+        if (q > 0) asm volatile("" : "+v"(a.m) : "v"(res[q - 1].m));
+#pragma unroll
+        for (int j = 0; j + 1 < NSRC; ++j) {
+            x80d::xu r;
+            ok &= OP == MI355_OP_SUM ? x80d::add_fast_u<false>(a, u[j < q ? j : j + 1], r)
+                                     : x80d::mul_fast_u<false>(a, u[j < q ? j : j + 1], r);
+            a = r;
+        }
+        res[q] = a;
+        asm volatile("" : "+v"(ok));  // a VGPR, not lane masks kept (and spilled) across the chains
+    }
+    if (__all(ok)) {
+#pragma unroll
+        for (int q = 0; q < NSRC; ++q) {
+            if (!ALL && p.dst[q] == nullptr) continue;
+            Pack<x80> o;
+            o.e[0] = x80d::pack(res[q], v[q]);
+            st16_fold((u32x4 *)p.dst[q] + i, o.v);
+        }
+        return;
+    }
     x80 first = v[0];
     bool have_first = false;
 #pragma unroll 1
     for (int q = 0; q < NSRC; ++q) {
         if (!ALL && p.dst[q] == nullptr) continue;
         x80 acc = v[0];
+#pragma unroll
+        for (int k = 1; k < NSRC; ++k) acc = x80d::pick(q == k, v[k], acc);
+        const x80 own = acc;
         if (q == 1 && have_first) {
             acc = first;
         } else {
 #pragma unroll
-            for (int k = 1; k < NSRC; ++k) acc = x80d::pick(q == k, v[k], acc);
-#pragma unroll
-            for (int j = 0; j + 1 < NSRC; ++j) acc = apply<OP>(acc, x80d::pick(j < q, v[j], v[j + 1]));
+            for (int j = 0; j + 1 < NSRC; ++j) {
+                const x80 b = x80d::pick(j < q, v[j], v[j + 1]);
+                acc = OP == MI355_OP_SUM ? x80d::add_general(acc, b) : x80d::mul_general(acc, b);
+            }
             if (q == 0) {
                 first = acc;
                 have_first = true;
             }
         }
+#pragma unroll
+        for (int w = 0; w < 3; ++w) acc.pad[w] = own.pad[w];  // the padding of the member's own slot
         Pack<x80> o;
         o.e[0] = acc;
         st16_fold((u32x4 *)p.dst[q] + i, o.v);

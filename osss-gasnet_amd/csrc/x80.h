@@ -188,9 +188,10 @@ __device__ __forceinline__ bool round_up(uint64_t m, uint64_t rem, bool sticky) 
 // Fast path of add/mul: both operands normal with exponent fields in
 // [1, kFastMax], so no rounding can overflow; the rest (zeros, denormals,
 // infinities, NaNs, unsupported encodings, near-overflow exponents,
-// alignment shifts beyond 63 bits, differences whose high 64 bits cancel,
-// results that would be denormal) takes the general path. Both paths round
-// the exact result once, so they agree bit for bit where both apply.
+// exponent differences of 63-65, differences that cancel more than 64 bits,
+// round ups that wrap the significand, results that would be denormal) takes
+// the general path. Both paths round the exact result once, so they agree
+// bit for bit where both apply.
 constexpr int kFastMax = kEmaxField - 3;
 __device__ __forceinline__ bool fast_operand(const x80 &a) {
     const int e = efield(a);
@@ -203,53 +204,98 @@ __device__ __forceinline__ bool fast_operand(const x80 &a) {
 // between the two paths; round 3 found them in the then-branchy general path
 // itself, which is now straight-line. The vote stays: it keeps the common
 // case to the fast path's instructions only.)
-__device__ __forceinline__ bool add_fast(const x80 &a, const x80 &b, x80 &r) {
-    // Straight-line: every choice a select. B (the smaller magnitude) is
-    // aligned under A = MA:0 as Bh:Bl (exact: the fast path takes alignment
-    // shifts up to 63); A + B or A - B in 128 bits; one normalization (right
-    // by one on a carry out of the addition, left by the leading zeros of the
-    // high word after a subtraction -- a difference whose high word cancels
-    // entirely takes the general path); one round to nearest even, as a carry
-    // out of an addition. Operands normal with fields in [1, kFastMax] and a
-    // normal result, else not ok.
-    const int ea = a.se & 0x7FFF, eb = b.se & 0x7FFF;
-    const int d = ea - eb;
+// A value of the fast paths' domain, unpacked: significand, exponent field,
+// sign as a mask (0 or -1). A chain of operations (the every-member fold)
+// keeps its accumulator in this form and packs once at the end.
+struct xu {
+    uint64_t m;
+    int e;
+    int s;
+};
+__device__ __forceinline__ xu unpack(const x80 &a) {
+    return xu{a.m, a.se & 0x7FFF, (int)(int16_t)a.se >> 15};
+}
+__device__ __forceinline__ x80 pack(const xu &u, const x80 &padsrc) {
+    x80 r = padsrc;  // the padding bytes of the slot the result goes to
+    r.m = u.m;
+    r.se = (uint16_t)((u.s & 0x8000) | u.e);
+    return r;
+}
+
+// nhi rounded to nearest even by the bits below it, nlo: up when nlo is
+// above half, or at half with nhi odd -- (nlo | (nhi & 1)) > half, the carry
+// out of its sum with half - 1, added into nhi by the same carry chain.
+__device__ __forceinline__ uint64_t round_even(uint64_t nhi, uint64_t nlo) {
+    const unsigned __int128 N = ((unsigned __int128)nhi << 64) | (nlo | (nhi & 1));
+    return (uint64_t)((N + 0x7FFFFFFFFFFFFFFFull) >> 64);
+}
+
+// The operations of a chain of up to STEPS of them whose operands pass
+// chain_operand<OP, STEPS> stay in the fast path's exponent range without a
+// check per step. Sums: fields in [kChainLo, kFastMax - STEPS]; a sum's field
+// exceeds the larger operand's by at most 1, and a difference's falls at most
+// 61 below it (add_fast_u: at most 63 leading zeros in the high word, two
+// bits of headroom). Products: unbiased exponents within +-L, L =
+// (kFastMax - kBias - STEPS) / (STEPS + 1); a product's unbiased exponent is
+// the operands' sum plus 0 or 1.
+constexpr int kChainLo = 64;
+template <int OP, int STEPS>
+__device__ __forceinline__ bool chain_operand(const x80 &a) {
+    const int e = efield(a);
+    if constexpr (OP == 0) {
+        return (e >= kChainLo) & (e <= kFastMax - STEPS) & jbit(a);
+    } else {
+        constexpr int L = (kFastMax - kBias - STEPS) / (STEPS + 1);
+        return ((unsigned)(e - (kBias - L)) <= 2u * L) & jbit(a);
+    }
+}
+
+// a + b for operands of the fast domain (the caller checks them:
+// fast_operand); true when the result is in it too (RANGE: including its
+// exponent range; false: the caller bounds it, chain_operand).
+template <bool RANGE = true>
+__device__ __forceinline__ bool add_fast_u(const xu &a, const xu &b, xu &r) {
+    // Straight-line, in a 128-bit frame with two bits of headroom: A (the
+    // larger magnitude) at bits 125..62, B aligned below it by the exponent
+    // difference dd -- exact for dd <= 62; for dd >= 66 B is under a quarter
+    // ulp of A and only its sign matters to the rounding, so it becomes a
+    // sticky 1 at bit 0 (dd 63-65: general path). A + B cannot carry out of
+    // the frame, and its high word has at least one leading zero; one left
+    // shift by them normalizes the sum or difference (a difference whose high
+    // word cancels entirely takes the general path), one round to nearest
+    // even (a round up that wraps the significand takes the general path).
+    const int d = a.e - b.e;
     const bool a_big = (d > 0) | ((d == 0) & (a.m >= b.m));
     const uint64_t MA = a_big ? a.m : b.m, MB = a_big ? b.m : a.m;
-    const int EA = ea > eb ? ea : eb;
+    const int EA = a.e > b.e ? a.e : b.e;
     const int dd = d < 0 ? -d : d;
-    const int k = dd < 63 ? dd : 63;
-    const uint64_t Bh = MB >> k;
-    const uint64_t Bl = (MB << 1) << (63 - k);  // MB << (64 - k): the bits shifted out; 0 for k = 0
-    const bool sub = ((a.se ^ b.se) & 0x8000) != 0;
-    // A + B: hi:lo = MA + Bh : Bl, carry out of hi; A - B: MA:0 - Bh:Bl
-    const uint64_t sum_hi = MA + Bh;
-    const bool carry = !sub & (sum_hi < MA);
-    const uint64_t lo = sub ? 0 - Bl : Bl;
-    const uint64_t hi = sub ? MA - Bh - (Bl != 0 ? 1 : 0) : sum_hi;
-    const int lz = sub ? __builtin_clzll(hi | 1) : 0;  // hi == 0: not ok below
-    // both normalizations computed, then selected (pinned in registers: left to
-    // itself the compiler sinks each into a divergent branch of its own)
-    uint64_t rh = (hi >> 1) | 0x8000000000000000ull, rl = (lo >> 1) | (hi << 63);
-    uint64_t lh = (hi << lz) | ((lo >> 1) >> (63 - lz)), ll = lo << lz;
-    asm volatile("" : "+v"(rh), "+v"(rl), "+v"(lh), "+v"(ll));
-    const uint64_t nhi = carry ? rh : lh;
-    const uint64_t nlo = carry ? rl : ll;
-    const uint64_t sticky = carry ? (lo & 1) : 0;
-    int E = EA + (carry ? 1 : 0) - lz;
-    // round to nearest even: above half an ulp, or at half with a sticky bit or an odd last bit
-    const bool up = round_up(nhi, nlo, sticky != 0);
-    uint64_t m = nhi + (up ? 1 : 0);
-    const bool wrap = m == 0;  // nhi = ~0 rounded up
-    m = wrap ? 0x8000000000000000ull : m;
-    E += wrap ? 1 : 0;
-    const unsigned fa = (unsigned)(ea - 1) < (unsigned)kFastMax && (a.m >> 63) != 0;
-    const unsigned fb = (unsigned)(eb - 1) < (unsigned)kFastMax && (b.m >> 63) != 0;
-    const bool ok = fa & fb & (dd <= 63) & (hi != 0) & ((unsigned)(E - 1) < (unsigned)kFastMax);
-    r = a;
+    const int k = dd < 62 ? dd : 62;
+    // A - B = A + ~B + 1: the sign difference as a mask and a carry in
+    const uint32_t M32 = (uint32_t)(a.s ^ b.s);
+    const uint64_t M = ((uint64_t)M32 << 32) | M32;
+    const unsigned __int128 A = (unsigned __int128)MA << 62;
+    const unsigned __int128 B = ((unsigned __int128)((MB >> 2) >> k) << 64) | (dd >= 66 ? 1 : MB << (62 - k));
+    const unsigned __int128 R = A + (B ^ (((unsigned __int128)M << 64) | M)) + (M & 1);
+    const uint64_t Rh = (uint64_t)(R >> 64), Rl = (uint64_t)R;
+    const int lz = __builtin_clzg(Rh, 64);  // Rh == 0: not ok below
+    __builtin_assume(lz >= 1);
+    const uint64_t nhi = (Rh << lz) | (Rl >> (64 - lz)), nlo = Rl << lz;
+    const uint64_t m = round_even(nhi, nlo);
+    const int E = EA + 2 - lz;
     r.m = m;
-    r.se = (uint16_t)(((a_big ? a.se : b.se) & 0x8000) | E);
+    r.e = E;
+    r.s = a_big ? a.s : b.s;
+    const bool ok = ((dd <= 62) | (dd >= 66)) & (Rh != 0) & (m != 0);
+    if constexpr (RANGE) return ok & ((unsigned)(E - 1) < (unsigned)kFastMax);
     return ok;
+}
+
+__device__ __forceinline__ bool add_fast(const x80 &a, const x80 &b, x80 &r) {
+    xu u;
+    const int ok = add_fast_u(unpack(a), unpack(b), u);  // ints: evaluated without branches
+    const int fa = fast_operand(a), fb = fast_operand(b);
+    r = pack(u, a);
+    return ok & fa & fb;
 }
 
 // The general paths: every encoding class, straight-line -- the finite
@@ -288,23 +334,31 @@ __device__ __forceinline__ x80 add(const x80 &a, const x80 &b) {
     return add_general(a, b);
 }
 
-__device__ __forceinline__ bool mul_fast(const x80 &a, const x80 &b, x80 &r) {
-    // straight-line like add_fast: the 128-bit product's leading bit is at
-    // 127 or 126 (one conditional left shift, as a select), one rounding
-    const int E = efield(a) + efield(b) - kBias + 1;  // biased exponent, leading bit at 127
+template <bool RANGE = true>
+__device__ __forceinline__ bool mul_fast_u(const xu &a, const xu &b, xu &r) {
+    // straight-line like add_fast_u: the 128-bit product's leading bit is at
+    // 127 or 126 (one conditional left shift, as a select), one rounding (a
+    // round up that wraps the significand takes the general path)
+    const int E = a.e + b.e - kBias + 1;  // biased exponent, leading bit at 127
     const uint64_t hi = __umul64hi(a.m, b.m), lo = a.m * b.m;
     const bool low = (hi >> 63) == 0;  // leading bit at 126
     const uint64_t nhi = low ? (hi << 1) | (lo >> 63) : hi;
     const uint64_t nlo = low ? lo << 1 : lo;
-    int Ef = E - (low ? 1 : 0);
-    const bool up = round_up(nhi, nlo, false);
-    uint64_t m = nhi + (up ? 1 : 0);
-    const bool wrap = up & (m == 0);
-    m = wrap ? 0x8000000000000000ull : m;
-    Ef += wrap ? 1 : 0;
-    const int fa = fast_operand(a), fb = fast_operand(b);  // ints: evaluated without branches
-    r = make(sign(a) ^ sign(b), Ef, m, a);
-    return fa & fb & (E >= 2) & (E <= kFastMax);
+    const uint64_t m = round_even(nhi, nlo);
+    r.m = m;
+    r.e = E - (low ? 1 : 0);
+    r.s = a.s ^ b.s;
+    const bool ok = m != 0;
+    if constexpr (RANGE) return ok & (E >= 2) & (E <= kFastMax);
+    return ok;
+}
+
+__device__ __forceinline__ bool mul_fast(const x80 &a, const x80 &b, x80 &r) {
+    xu u;
+    const int ok = mul_fast_u(unpack(a), unpack(b), u);  // ints: evaluated without branches
+    const int fa = fast_operand(a), fb = fast_operand(b);
+    r = pack(u, a);
+    return ok & fa & fb;
 }
 
 __device__ __forceinline__ x80 mul_general(const x80 &a, const x80 &b) {

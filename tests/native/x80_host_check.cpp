@@ -3,7 +3,10 @@
 // against the host's own x87 `long double` + and * (what the reference's
 // reduce-op.c:99 element functions execute), on pairs aimed at both of its
 // paths and the boundaries between them: exponent differences 0-3 and 0-70,
-// fields near 1 and near the top, exact and near cancellation, random fields.
+// fields near 1 and near the top, exact and near cancellation, random fields,
+// powers of two and all-ones significands against operands 60-73 fields
+// below (the fast add's sticky operand), significands that round up to a
+// carry (the wrap).
 // Built and run by tests/test_x80_host.py (CPU). usage: x80_host_check [pairs per case]
 #include <stdint.h>
 #include <stdio.h>
@@ -15,6 +18,8 @@
 #define __device__
 #define __forceinline__ inline
 #define __all(x) (x)
+#define __builtin_clzg(x, z) ((x) != 0 ? __builtin_clzll(x) : (z))
+#define __builtin_assume(c) ((void)0)
 static inline uint64_t __umul64hi(uint64_t a, uint64_t b) { return (uint64_t)(((unsigned __int128)a * b) >> 64); }
 #include "x80.h"
 
@@ -35,7 +40,7 @@ int main(int argc, char **argv) {
         r.se = (uint16_t)((s << 15) | e);
         return r;
     };
-    for (int round = 0; round < 6; ++round)
+    for (int round = 0; round < 8; ++round)
         for (long i = 0; i < per; ++i) {
             int ea, eb;
             switch (round) {
@@ -44,7 +49,9 @@ int main(int argc, char **argv) {
             case 2: ea = 1 + (int)(g() % 80); eb = 1 + (int)(g() % 80); break;
             case 3: ea = 0x7FF8 + (int)(g() % 7); eb = 0x3F80 + (int)(g() % 256); break;
             case 4: ea = 1 + (int)(g() % 0x7FFE); eb = 1 + (int)(g() % 0x7FFE); break;
-            default: ea = 16383 + (int)(g() % 5); eb = ea; break;
+            case 5: ea = 16383 + (int)(g() % 5); eb = ea; break;
+            case 6: ea = 16000 + (int)(g() % 800); eb = ea - 60 - (int)(g() % 14); break;
+            default: ea = 16383 + (int)(g() % 3); eb = ea - (int)(g() % 3); break;
             }
             if (eb < 1) eb = 1;
             if (eb > 0x7FFE) eb = 0x7FFE;
@@ -52,6 +59,11 @@ int main(int argc, char **argv) {
             if (round == 5) {  // b = -a with the low significand bits perturbed
                 b.m = (a.m ^ (g() & 0xFFF)) | (1ull << 63);
                 b.se = a.se ^ 0x8000;
+            }
+            if (round == 6) a.m = g() & 1 ? 1ull << 63 : ~0ull;
+            if (round == 7) {  // all-ones high bits: sums and products that round up to 2^64
+                a.m |= ~0ull << (g() % 20);
+                b.m |= ~0ull << (g() % 20);
             }
             long double la, lb;
             memset(&la, 0, sizeof la);

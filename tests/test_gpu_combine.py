@@ -199,6 +199,61 @@ def test_combine_orders_x87_minmax_sparse_specials(shm, dev, op, nsrc):
     dev.free()
 
 
+@pytest.mark.parametrize("case", ["near", "bounds", "sparse"])
+@pytest.mark.parametrize("op", ["sum", "prod"])
+@pytest.mark.parametrize("nsrc", [2, 3, 5, 8])
+def test_combine_orders_x87_chains(shm, dev, op, nsrc, case):
+    """The every-member x87 sum/product (combine_kernels.h x80_orders_vector):
+    every member's chain in the fast form, one wave vote, the general chains
+    for the whole wave otherwise; every member against the host x87 in the
+    reference's order (reduce-op.c:99 element function, one rounding per
+    operation).
+      near    exponent fields 16383 +- 70: the fast chains throughout
+      bounds  the fast form's edges: fields at and around x80.h kChainLo and
+              kFastMax - steps (sums), +-L around the bias (products),
+              exponent differences 58-70 (exact alignment up to 62, general
+              63-65, a dropped operand from 66), all-ones significands (round
+              ups that wrap), operands that cancel to their last bits
+      sparse  near, with a few zeros, denormals, infinities and NaNs planted:
+              both kinds of waves in one launch"""
+    rng = np.random.default_rng(1000 * nsrc + 10 * len(op) + len(case))
+    n = 120000
+    steps = nsrc - 1
+    srcs = []
+    for k in range(nsrc):
+        e = 16383 + rng.integers(-70, 71, n)
+        m = rng.integers(0, 2**64, n, dtype=np.uint64, endpoint=False) | np.uint64(1 << 63)
+        if case == "bounds":
+            pick = rng.integers(0, 6, n)
+            lim = (0x7FFF - 3 - 16383 - steps) // (steps + 1)
+            e = np.where(pick == 0, 62 + rng.integers(0, 6, n), e)
+            e = np.where(pick == 1, 0x7FFC - steps + rng.integers(-3, 3, n), e)
+            e = np.where(pick == 2, 16383 + np.where(rng.random(n) < 0.5, -lim, lim) + rng.integers(-2, 3, n), e)
+            e = np.where(pick == 3, 16383 - (k % 2) * rng.integers(58, 71, n), e)
+            m = np.where(pick == 4, m | (~np.uint64(0) << rng.integers(0, 12, n).astype(np.uint64)), m)
+            e = np.clip(e, 1, 0x7FFE)
+        x = _x80(rng, n, e, m=m)
+        if case == "bounds" and k == 1:  # member 1 nearly cancels member 0 on a sixth of the elements
+            c = rng.random(n) < 1 / 6
+            raw0, raw1 = srcs[0].view(np.uint8).reshape(n, 16), x.view(np.uint8).reshape(n, 16)
+            m0 = raw0[:, 0:8].copy().view(np.uint64).reshape(n) ^ rng.integers(0, 1 << 10, n, dtype=np.uint64)
+            se0 = raw0[:, 8:10].copy().view(np.uint16).reshape(n) ^ np.uint16(0x8000)
+            raw1[c, 0:8] = (m0 | np.uint64(1 << 63))[c].view(np.uint8).reshape(-1, 8)
+            raw1[c, 8:10] = se0[c].view(np.uint8).reshape(-1, 2)
+        if case == "sparse":
+            pos = rng.integers(0, n, 12)
+            x[pos[:3]] = np.longdouble(0.0)
+            x[pos[3:6]] = np.finfo(np.longdouble).tiny / 16
+            x[pos[6:9]] = np.longdouble(np.inf) if k % 2 else -np.longdouble(np.inf)
+            x[pos[9:]] = np.longdouble(np.nan)
+        srcs.append(x)
+    want = oracle.reduce_all(op, "longdouble", srcs)
+    got = gpu_orders(shm, dev, op, "longdouble", srcs)
+    for q, g in got.items():
+        assert_match(g, want[q], op, "longdouble", ctx=f"{case} nsrc={nsrc} member {q}")
+    dev.free()
+
+
 @pytest.mark.parametrize("op,dtype", [("sum", "double"), ("xor", "int"), ("max", "float"), ("prod", "complexf"),
                                       ("min", "longdouble"), ("sum", "short")])
 @pytest.mark.parametrize("nsrc", [1, 2, 5, 8, 9, 12, 17])
