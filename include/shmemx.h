@@ -25,6 +25,21 @@ void shmemx_free_device (void *ptr);
 /* 1 if ptr lies in this PE's device symmetric heap. */
 int shmemx_is_device_symmetric (const void *ptr);
 
+/* Device buffers outside the heap (hipMalloc, a framework's tensors) as
+ * *_to_all target/source with PE_size > 1: the members export the
+ * allocations holding them (IPC), map each other's for the call and reduce
+ * in place of staging them through scratch -- one host barrier per call for
+ * the exchange, no copies. Applies when every member passes device memory
+ * of the same kinds (heap / not heap) for target and for source, 16-byte
+ * aligned, target == source or disjoint, and every allocation can be
+ * exported (hipMalloc yes, virtual-memory hipMemCreate no); otherwise every
+ * member stages, as with SHMEM_EXTERNAL_MAP=0. Mapped allocations stay open
+ * for later calls (at most SHMEM_EXTERNAL_MAP_CACHE, default 64; they keep
+ * the peer's memory alive after it frees it): flush closes them all on this
+ * PE; stats = allocations mapped now, opened and closed since init. */
+void shmemx_external_map_flush (void);
+void shmemx_external_map_stats (long *mapped, long *opened, long *closed);
+
 /* Cross-PE schedule for *_to_all (env SHMEM_REDUCE_ALGORITHM sets the
  * default at init):
  *   SHMEMX_REDUCE_AUTO  = P2P shard schedule (below)

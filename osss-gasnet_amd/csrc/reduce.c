@@ -668,7 +668,8 @@ static void copy_local (size_t dst_off, size_t src_off, size_t nbytes, int timed
 static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
                          const struct aset *s, const void *host_src, void *host_dst)
 {
-    const int servable = shmemi.srv.enabled && host_src == NULL && host_dst == NULL;
+    const int servable = shmemi.srv.enabled && host_src == NULL && host_dst == NULL && dst_off < SHMEMI_EXT_TARGET &&
+                         src_off < SHMEMI_EXT_TARGET; /* it addresses the members' heaps */
     const double t_call = servable ? shmemi_now () : 0.0;
     if (servable && server_matches (op, dtype, s) && n <= 2 * shmemi.srv.grid_elems) {
         SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: persistent fused server (%zu elements, %d members)", n, s->size);
@@ -854,7 +855,7 @@ int shmemi_rccl_supported (int op, int dtype);
 /* ---------------------------------------------------------------------- */
 /* entry                                                                   */
 /* ---------------------------------------------------------------------- */
-enum { PK_HOST = 0, PK_DEV_SYM = 1, PK_DEV_OTHER = 2 };
+enum { PK_HOST = SHMEMI_PK_HOST, PK_DEV_SYM = SHMEMI_PK_DEV_SYM, PK_DEV_OTHER = SHMEMI_PK_DEV_OTHER };
 
 static int ptr_kind (const void *p, size_t nbytes)
 {
@@ -1090,6 +1091,22 @@ static void reduce_impl (int op, int dtype, const char *fn, void *target, const 
     if (kt == PK_DEV_SYM && ks == PK_DEV_SYM) {
         reduce_symmetric (op, dtype, es, shmemi_heap_offset (target), shmemi_heap_offset (source), n, &s);
         return;
+    }
+    /* device buffers outside the heap (a framework's tensors): the members
+     * map each other's allocations for this call and run the heap schedules
+     * on them, or, when one of them cannot, all stage (extmap.c) */
+    if (s.size > 1 && !use_rccl) {
+        size_t toff, soff;
+        if (shmemi_ext_begin (fn, target, source, nbytes, kt, ks, s.start, s.stride, s.size, &toff, &soff)) {
+            SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "device buffers outside the heap mapped by the peers for this call");
+            caller_order_pending = 1; /* peers read this PE's buffers directly */
+            reduce_symmetric (op, dtype, es, toff, soff, n, &s);
+            shmemi_ext_end ();
+            static char name[80];
+            snprintf (name, sizeof name, "mapped-%s", shmemi.last.schedule);
+            shmemi.last.schedule = name;
+            return;
+        }
     }
 
     if (!use_rccl && local_direct (op, dtype, target, source, n, overlap, kt, ks, &s))

@@ -52,7 +52,7 @@ struct shmemi_hostblk {
 };
 
 #define SEG_MAGIC 0x4d49333535534d45ull /* "MI355SME" */
-#define SEG_VERSION 4
+#define SEG_VERSION 5
 
 static double now_s (void)
 {
@@ -180,6 +180,8 @@ static struct shmemi_pe_info *seg_info (int pe)
 {
     return (struct shmemi_pe_info *) ((char *) shmemi.seg + shmemi.seg->info_off) + pe;
 }
+
+struct shmemi_pe_info *shmemi_seg_info (int pe) { return seg_info (pe); }
 
 static _Atomic uint64_t *seg_flag (int row_pe, int from_pe)
 {
@@ -328,6 +330,22 @@ void shmemi_barrier_set (int PE_start, int stride, int PE_size)
     barrier_watch (PE_start, stride, PE_size, NULL);
 }
 
+/* This PE's arrival at a barrier of the set without the wait: the members
+ * that wait see it (extmap.c: a PE that will stage anyway publishes its
+ * record and goes on). Keeps the pair counts as a full barrier does. */
+void shmemi_barrier_arrive (int PE_start, int stride, int PE_size)
+{
+    if (PE_size <= 1 || shmemi.npes <= 1)
+        return;
+    for (int i = 0; i < PE_size; ++i) {
+        const int q = PE_start + i * stride;
+        if (q != shmemi.mype) {
+            atomic_fetch_add_explicit (seg_flag (q, shmemi.mype), 1, memory_order_release);
+            ++shmemi.bar_count[q];
+        }
+    }
+}
+
 /* ---------------------------------------------------------------------- */
 /* SHMEM_DEBUG=1: collective argument check                                 */
 /* ---------------------------------------------------------------------- */
@@ -466,6 +484,8 @@ size_t shmemi_heap_offset (const void *p) { return (size_t) ((const char *) p - 
 
 void *shmemi_peer_ptr (int pe, size_t off)
 {
+    if (__builtin_expect (off >= SHMEMI_EXT_TARGET, 0))
+        return shmemi_ext_ptr (pe, off); /* a device buffer outside the heap, mapped for this call (extmap.c) */
     if (__builtin_expect (shmemi.peer_heap[pe] == NULL, 0))
         shmemi_fatal ("PE %d's device heap is not mapped here (IPC mapping failed at init): only the RCCL "
                       "schedule can reach it", pe);
@@ -629,7 +649,7 @@ static void settings_publish (void)
 {
     seg_info (shmemi.mype)->settings =
         (struct shmemi_settings) {shmemi.algorithm, shmemi.order, shmemi.debug != 0, shmemi.srv.enabled,
-                                  shmemi.order_chunk, shmemi.fused_max, shmemi.oneshot_max, shmemi.scratch_chunk,
+                                  shmemi.ext_map, 0, shmemi.order_chunk, shmemi.fused_max, shmemi.oneshot_max, shmemi.scratch_chunk,
                                   shmemi.user_size};
 }
 
@@ -647,6 +667,7 @@ static void settings_check (void)
         S (algorithm, "SHMEM_REDUCE_ALGORITHM")
         S (order, "SHMEM_REDUCE_ORDER")
         S (debug, "SHMEM_DEBUG")
+        S (ext_map, "SHMEM_EXTERNAL_MAP")
         S (order_chunk, "SHMEM_DEVICE_ORDER_SIZE")
         S (fused_max, "SHMEM_FUSED_MAX_BYTES")
         S (oneshot_max, "SHMEM_ONESHOT_MAX_BYTES")
@@ -1124,6 +1145,8 @@ void pshmem_init (void)
     shmemi.debug = (int) env_long (dbg_env, 0);
     static const char *es_env[] = {"SHMEM_ENTRY_SYNC", NULL};
     shmemi.entry_sync = (int) env_long (es_env, 0);
+    static const char *em_env[] = {"SHMEM_EXTERNAL_MAP", NULL};
+    shmemi.ext_map = env_long (em_env, 1) != 0;
     shmemi.algorithm = parse_algorithm (getenv ("SHMEM_REDUCE_ALGORITHM"));
     shmemi.order = parse_order (getenv ("SHMEM_REDUCE_ORDER"));
 
@@ -1237,6 +1260,7 @@ void pshmem_finalize (void)
         extern void shmemi_rccl_destroy (void);
         shmemi_rccl_destroy ();
     }
+    shmemi_ext_finalize (); /* peers' buffers mapped by calls (extmap.c) */
     if (shmemi.peer_heap != NULL) {
         for (int pe = 0; pe < shmemi.npes; ++pe) {
             if (pe != shmemi.mype && shmemi.peer_heap[pe] != NULL)

@@ -38,8 +38,19 @@ struct shmemi_dbg_rec {
 
 /* Settings every PE of a job must share (compared at init). */
 struct shmemi_settings {
-    int32_t algorithm, order, debug, persistent;
+    int32_t algorithm, order, debug, persistent, ext_map, pad;
     uint64_t order_chunk, fused_max, oneshot_max, scratch_chunk, user_size;
+};
+
+/* One *_to_all call's device buffers outside the symmetric heap, as this PE
+ * passed them (extmap.c): the IPC export of the allocation holding each and
+ * the offset in it, or the heap offset of a symmetric one. */
+struct shmemi_ext_rec {
+    int32_t ok;                 /* both buffers can be shared with the peers */
+    int32_t same;               /* target == source */
+    int32_t tkind, skind;       /* 1 device heap, 2 other device memory */
+    hipIpcMemHandle_t th, sh;
+    uint64_t toff, soff;
 };
 
 struct shmemi_pe_info {
@@ -55,6 +66,7 @@ struct shmemi_pe_info {
     uint64_t collect_bytes;     /* this PE's contribution to the current shmem_collect */
     struct shmemi_settings settings;
     struct shmemi_dbg_rec dbg;
+    struct shmemi_ext_rec ext;
 };
 
 struct shmemi_seg {
@@ -98,6 +110,7 @@ struct shmemi_state {
     int p2p_broken;             /* init self-test: peer heap reads failed */
     int peer_acquire;           /* queue mi355_acquire_system before reads of peers' buffers */
     int local_pes;              /* PEs on this GPU (this one included): co-residency share of the fused grids */
+    int ext_map;                /* SHMEM_EXTERNAL_MAP: peers map device buffers outside the heap (extmap.c) */
 
     /* bootstrap */
     struct shmemi_seg *seg;
@@ -183,6 +196,7 @@ void shmemi_fatal (const char *fmt, ...) __attribute__ ((noreturn, format (print
 void shmemi_init_check (const char *fn);
 void shmemi_hip_check (hipError_t e, const char *what);
 void shmemi_barrier_set (int PE_start, int stride, int PE_size);
+void shmemi_barrier_arrive (int PE_start, int stride, int PE_size);
 int shmemi_in_device_heap (const void *p, size_t nbytes);
 size_t shmemi_heap_offset (const void *p);
 void *shmemi_peer_ptr (int pe, size_t off);
@@ -216,6 +230,20 @@ void shmemi_publish_count (size_t nbytes);
 size_t shmemi_peer_count (int pe);
 /* runtime.c: SHMEM_DEBUG's collective argument exchange over an active set */
 void shmemi_debug_exchange (const struct shmemi_dbg_rec *mine, int PE_start, int stride, int PE_size);
+struct shmemi_pe_info *shmemi_seg_info (int pe);
+
+/* extmap.c: device buffers outside the symmetric heap reached by the peers
+ * through IPC mappings of their allocations. A call that maps them addresses
+ * them with the virtual offsets SHMEMI_EXT_TARGET / SHMEMI_EXT_SOURCE (plus
+ * the byte offset into the buffer), which shmemi_peer_ptr resolves per PE. */
+#define SHMEMI_EXT_TARGET ((size_t) 1 << 60)
+#define SHMEMI_EXT_SOURCE ((size_t) 3 << 59)
+enum { SHMEMI_PK_HOST = 0, SHMEMI_PK_DEV_SYM = 1, SHMEMI_PK_DEV_OTHER = 2 };
+int shmemi_ext_begin (const char *fn, void *target, const void *source, size_t nbytes, int kt, int ks, int PE_start,
+                      int stride, int PE_size, size_t *toff, size_t *soff);
+void shmemi_ext_end (void);
+void *shmemi_ext_ptr (int pe, size_t off);
+void shmemi_ext_finalize (void);
 
 #define SHMEMI_HIP(call) shmemi_hip_check ((call), #call)
 

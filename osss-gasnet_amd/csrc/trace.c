@@ -140,6 +140,9 @@ void shmemi_trace_show_info (void)
         {"SHMEM_DEBUG", "1: check pSync and exchange every collective's arguments between its members, aborting "
                         "with the first differing field"},
         {"SHMEM_ENTRY_SYNC", "1: every call starts with hipDeviceSynchronize"},
+        {"SHMEM_EXTERNAL_MAP", "1 (default) / 0: peers map device buffers outside the heap for a call instead of "
+                               "staging them through scratch"},
+        {"SHMEM_EXTERNAL_MAP_CACHE", "peers' mapped allocations kept open (default 64, least recently used closed)"},
         {"SHMEM_PEER_ACQUIRE", "1/0: system-scope L2 acquire before reading peers' buffers (default: on if a peer is on another GPU)"},
     };
     shmemi_trace_emit (SHMEMI_LOG_INFO, "environment variables understood by this build:");

@@ -60,6 +60,8 @@ def load(path=LIB_PATH):
         "shmemx_set_reduce_order": ([_i], _i), "shmemx_get_reduce_order": ([], _i),
         "shmemx_set_persistent": ([_i], _i),
         "shmemx_persistent_stats": ([ctypes.POINTER(ctypes.c_long)] * 2, None),
+        "shmemx_external_map_stats": ([ctypes.POINTER(ctypes.c_long)] * 3, None),
+        "shmemx_external_map_flush": ([], None),
         "shmemx_device_id": ([], _i), "shmemx_device_synchronize": ([], None),
         "shmemx_peer_link": ([_i, ctypes.POINTER(_i), ctypes.POINTER(_i)], _i),
         "shmemx_memcpy": ([_vp, _vp, _sz], None), "shmemx_wtime": ([], ctypes.c_double),
@@ -146,6 +148,13 @@ class Shmem:
         a, b = ctypes.c_long(), ctypes.c_long()
         self.lib.shmemx_persistent_stats(ctypes.byref(a), ctypes.byref(b))
         return a.value, b.value
+
+    def external_map_stats(self):
+        """(peers' allocations mapped now, opened, closed since init): device
+        buffers outside the heap that calls mapped (shmemx.h)"""
+        a, b, c = ctypes.c_long(), ctypes.c_long(), ctypes.c_long()
+        self.lib.shmemx_external_map_stats(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        return a.value, b.value, c.value
 
     def sync(self):
         self.lib.shmemx_device_synchronize()

@@ -256,8 +256,8 @@ def main():
     ha, hb = shm.malloc(maxb), shm.malloc(maxb)
     hip = ctypes.CDLL("libamdhip64.so")
     pa, pb = ctypes.c_void_p(), ctypes.c_void_p()
-    assert hip.hipMalloc(ctypes.byref(pa), ctypes.c_size_t(maxb)) == 0
-    assert hip.hipMalloc(ctypes.byref(pb), ctypes.c_size_t(maxb)) == 0
+    assert hip.hipMalloc(ctypes.byref(pa), ctypes.c_size_t(maxb + 4096)) == 0
+    assert hip.hipMalloc(ctypes.byref(pb), ctypes.c_size_t(maxb + 4096)) == 0
     priv_a, priv_b = pa.value, pb.value
     results = {}
     for c in spec["cases"]:
@@ -305,6 +305,24 @@ def main():
                 src, dst = priv_a, priv_b
             else:
                 src, dst = ha, hb
+        elif mode == "devmap_inplace":   # one hipMalloc buffer, target == source
+            src = dst = priv_a
+        elif mode == "devmap_offset":    # each PE's buffers at other offsets into its allocations
+            src, dst = priv_a + 64 * (me + 1), priv_b + 32 * me
+        elif mode == "devmap_symtarget":  # target in the symmetric heap, source a hipMalloc buffer
+            src, dst = priv_a, db
+        elif mode == "devmap_unaligned_pe1":  # PE 1's pair 8 bytes off 16-byte alignment: every PE stages
+            src, dst = (priv_a + 8, priv_b + 8) if me == 1 else (priv_a, priv_b)
+        elif mode == "devmap_realloc":   # fresh allocations before the call (the peers' cached mappings go stale)
+            hip.hipFree(pa)
+            hip.hipFree(pb)
+            keep = ctypes.c_void_p()   # so the new ones need not land on the old addresses
+            assert hip.hipMalloc(ctypes.byref(keep), ctypes.c_size_t(4096 * (1 + c["id"] % 3))) == 0
+            assert hip.hipMalloc(ctypes.byref(pa), ctypes.c_size_t(maxb + 4096)) == 0
+            assert hip.hipMalloc(ctypes.byref(pb), ctypes.c_size_t(maxb + 4096)) == 0
+            hip.hipFree(keep)
+            priv_a, priv_b = pa.value, pb.value
+            src, dst = priv_a, priv_b
         elif mode == "host_mixed":
             # even PEs: page-locked shmem_malloc arrays (one-launch in-kernel
             # staging for small n); odd PEs: plain numpy arrays (staged copies)
@@ -355,6 +373,9 @@ def main():
             results[str(c["id"])] = out
         else:
             results[str(c["id"])] = shm.get(dst, n, dtype) if n else np.zeros(0, dtype=shmem_reduce.NP[dtype])
+        if n and c.get("api") != "fortran":
+            results[str(c["id"]) + "_schedule"] = np.array([shm.last_call_info()["schedule"]])
+    results["external_map_stats"] = np.array(shm.external_map_stats())
     hip.hipFree(pa)
     hip.hipFree(pb)
     shm.free(hb)

@@ -395,6 +395,66 @@ def test_non_symmetric_device_buffers(tmp_path):
     check(results, cases)
 
 
+MAPPED_PAIRS = [("sum", "double"), ("max", "float"), ("and", "longlong"), ("prod", "complexd"),
+                ("sum", "longdouble"), ("min", "short")]
+
+
+def test_external_device_buffers_mapped(tmp_path):
+    """hipMalloc buffers at 3 PEs: the members map each other's allocations for
+    the call (extmap.c) and run the heap schedules on them -- fused one-shot,
+    two-shot and the multi-launch shards -- in place, at per-PE offsets into
+    the allocations and with the target in the heap; every PE's result is the
+    reference's for it, the schedule says "mapped-", and the peers' mappings
+    are opened once and reused."""
+    cases = []
+    cid = 0
+    for mode in ("devother", "devmap_inplace", "devmap_offset", "devmap_symtarget"):
+        for n in (515, 8192, 60000, 300000):
+            cases += make_cases(MAPPED_PAIRS, n, [[0, 0, 3]], mode, "p2p", cid)
+            cid += 100
+    cases += make_cases(MAPPED_PAIRS[:3], 5000, [[0, 1, 2]], "devother", "p2p", cid)  # strided set {0, 2}
+    results = run_pes(3, cases, tmp_path, extra_env={"SHMEM_DEVICE_SCRATCH_SIZE": "3M"})
+    check(results, cases)
+    for c in cases:
+        for s in c["sets"]:
+            for pe in members(*s):
+                sched = str(results[pe][str(c["id"]) + "_schedule"][0])
+                assert sched.startswith("mapped-"), f"case {c['id']} {c['mode']} PE {pe}: schedule {sched}"
+    for pe in range(3):
+        mapped, opened, closed = (int(v) for v in results[pe]["external_map_stats"])
+        # two hipMalloc allocations per peer, each opened once for all the calls
+        assert opened <= 4 and closed == 0 and mapped == opened, (pe, mapped, opened, closed)
+
+
+def test_external_device_buffers_fallbacks(tmp_path):
+    """Where one member cannot share its buffers (PE 1 8 bytes off 16-byte
+    alignment) every member stages and the results stay exact; buffers
+    re-allocated before every call get new handles (no stale mapping); a
+    cache of one mapping closes and reopens as the calls alternate."""
+    cases = []
+    cases += make_cases(MAPPED_PAIRS, 5000, [[0, 0, 3]], "devmap_unaligned_pe1", "p2p", 0)
+    cases += make_cases(MAPPED_PAIRS, 70000, [[0, 0, 3]], "devmap_unaligned_pe1", "p2p", 100)
+    cases += make_cases(MAPPED_PAIRS * 2, 3000, [[0, 0, 3]], "devmap_realloc", "p2p", 200)
+    cases += make_cases(MAPPED_PAIRS, 40000, [[0, 0, 3]], "devother", "p2p", 300)
+    results = run_pes(3, cases, tmp_path, extra_env={"SHMEM_DEVICE_SCRATCH_SIZE": "3M",
+                                                     "SHMEM_EXTERNAL_MAP_CACHE": "1"})
+    check(results, cases)
+    for c in cases:
+        for pe in range(3):
+            sched = str(results[pe][str(c["id"]) + "_schedule"][0])
+            assert sched.startswith("mapped-") == (c["mode"] != "devmap_unaligned_pe1"), (c["id"], pe, sched)
+    for pe in range(3):
+        mapped, opened, closed = (int(v) for v in results[pe]["external_map_stats"])
+        assert opened >= 2 * 12 and closed >= opened - 4, (pe, mapped, opened, closed)
+    # mapping off: the same calls staged
+    off = make_cases(MAPPED_PAIRS, 70000, [[0, 0, 3]], "devother", "p2p", 400)
+    results = run_pes(3, off, tmp_path, extra_env={"SHMEM_DEVICE_SCRATCH_SIZE": "3M", "SHMEM_EXTERNAL_MAP": "0"})
+    check(results, off)
+    for c in off:
+        assert not str(results[0][str(c["id"]) + "_schedule"][0]).startswith("mapped-")
+        assert tuple(int(v) for v in results[0]["external_map_stats"]) == (0, 0, 0)
+
+
 def test_signal_region_mapping_failure_falls_back(tmp_path):
     """One PE cannot map the peers' signal regions (SHMEM_TEST_IPC_FAIL=sig
     on PE 1): init must not abort; every PE agrees to run without device-side
