@@ -366,6 +366,8 @@ def main():
     ap.add_argument("--no-kernels", action="store_true",
                     help="N = 1: skip the kernel legs (the fold kernels timed alone: k = 2 / 8 sources of "
                          "256 MiB, config 3 / 4's per-GPU reduce-scatter shapes)")
+    ap.add_argument("--no-external", action="store_true",
+                    help="N > 1: skip the leg on plain hipMalloc buffers (outside the symmetric heap)")
     ap.add_argument("--kernel-reps", type=int, default=50)
     ap.add_argument("--no-fused", action="store_true",
                     help="N = 1: skip the fused-kernel leg (2 PE processes sharing this GPU, 64 KiB and 1 MiB calls)")
@@ -656,6 +658,49 @@ def main():
         ops["note"] = ("BASELINE config 4 (op coverage): shmem_float_max_to_all and shmem_longlong_and_to_all, "
                        "64 MiB per PE, GiB/s reduced whole job; longlong words with bits 1 at p = 7/8")
 
+    # N > 1: the same call on plain hipMalloc buffers (a framework's tensors,
+    # outside the symmetric heap): the members map each other's allocations
+    # for the call (csrc/extmap.c) instead of staging them through scratch
+    external = None
+    if npes > 1 and not args.host and not args.no_external and not rccl_fallback:
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        bufs = [ctypes.c_void_p(), ctypes.c_void_p()]
+        if all(hip.hipMalloc(ctypes.byref(b), ctypes.c_size_t(S)) == 0 for b in bufs):
+            esrc, edst = bufs[0].value, bufs[1].value
+            shm.put(esrc, synth(me, np.arange(n, dtype=np.uint64)))  # the op-coverage leg rewrote src
+            k = max(5, args.steps // 4)
+            loop(edst, esrc, n, 0, 0, npes, None, shm._psync_ptr, 3)
+            shm.barrier_all()
+            shm.sync()
+            te0 = time.perf_counter()
+            loop(edst, esrc, n, 0, 0, npes, None, shm._psync_ptr, k)
+            shm.sync()
+            t_ext_local = time.perf_counter() - te0
+            einfo = shm.last_call_info()   # before max_over_pes: its own call replaces it
+            t_ext = max_over_pes(t_ext_local) / k
+            ck = "skipped"
+            if not args.no_check:
+                import oracle
+                idx = np.unique(np.random.default_rng(50 + me).integers(0, n, 1 << 14)).astype(np.uint64)
+                got = shm.get(edst, n, "double")[idx.astype(np.int64)]
+                want = oracle.reduce_pe("sum", "double", [synth(p, idx) for p in range(npes)], me)
+                bad = int(max_over_pes(int((got.view(np.uint64) != want.view(np.uint64)).sum())))
+                ck = "bit-exact, %d samples" % len(idx) if bad == 0 else "MISMATCH %d samples" % bad
+            shm.barrier_all()
+            mapped, opened, closed = shm.external_map_stats()
+            external = {"bytes_per_pe": S, "steps": k, "us_per_call": round(t_ext * 1e6, 2),
+                        "value": round(npes * S / t_ext / GIB, 2), "over_heap_buffers": round(t_ext / t_step, 3),
+                        "schedule": einfo["schedule"], "mappings_opened": opened, "check": ck,
+                        "note": "the headline call on plain hipMalloc buffers (outside the symmetric heap): "
+                                "the members map each other's allocations for the call (IPC, cached) instead "
+                                "of staging them through scratch (SHMEM_EXTERNAL_MAP)"}
+        else:
+            external = {"error": "hipMalloc of the two buffers failed"}
+        for b in bufs:
+            if b.value:
+                hip.hipFree(b)
+
     # dominant kernel and its algorithmic bytes per launch, from the schedule
     # the library reports for the timed calls (shmemx_last_call_info)
     launches = max(1, info["launches"])
@@ -770,6 +815,7 @@ def main():
             "coherence_selftest": coherence,
             "check": check,
             "op_coverage": ops,
+            "external_buffers": external,
             "kernels": kernels,
             "fused_same_gpu": fused,
             "fused_same_gpu_persistent": fused_p,

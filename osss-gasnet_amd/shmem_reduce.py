@@ -23,6 +23,9 @@ NP = {
     "float": np.float32, "double": np.float64, "longdouble": np.longdouble,
     "complexf": np.complex64, "complexd": np.complex128,
 }
+# torch dtype name -> the shmem type whose C type has its layout (LP64: long = long long = int64)
+TORCH_DTYPES = {"int16": "short", "int32": "int", "int64": "long", "float32": "float", "float64": "double",
+                "complex64": "complexf", "complex128": "complexd"}
 ALGORITHMS = {"auto": 0, "p2p": 1, "exact": 2, "rccl": 3}          # enum shmemx_reduce_algorithm
 ORDERS = {"reference": 0, "pe_start": 1}                            # enum shmemx_reduce_order
 SHMEM_REDUCE_SYNC_SIZE = 128
@@ -177,6 +180,22 @@ class Shmem:
         if pSync is None:
             pSync = self._psync_ptr
         self._reduction(op, dtype)(target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync)
+
+    def to_all_tensors(self, op, target, source, PE_start=0, logPE_stride=0, PE_size=None):
+        """shmem_<T>_<op>_to_all on two contiguous device tensors of one dtype
+        (T from the tensor's dtype; long double has no torch dtype). They need
+        not come from the symmetric heap: at PE_size > 1 the members map each
+        other's allocations for the call (shmemx.h, extmap.c). Blocking, like
+        the C call: on return `target` holds this PE's result."""
+        if target.dtype != source.dtype or target.numel() != source.numel():
+            raise ValueError("target and source must have the same dtype and number of elements")
+        if not (target.is_contiguous() and source.is_contiguous()) or target.device.type != "cuda" \
+                or source.device.type != "cuda":
+            raise ValueError("target and source must be contiguous GPU tensors")
+        dtype = TORCH_DTYPES.get(str(source.dtype).replace("torch.", ""))
+        if dtype is None:
+            raise TypeError(f"no shmem_*_to_all for {source.dtype}")
+        self.to_all(op, dtype, target.data_ptr(), source.data_ptr(), source.numel(), PE_start, logPE_stride, PE_size)
 
     def _stream_reduction(self, op, dtype):
         key = ("stream", op, dtype)

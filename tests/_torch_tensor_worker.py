@@ -54,6 +54,18 @@ def main():
         got = dst.cpu().numpy()
         want = oracle.reduce_pe(op, dtype, srcs, me)
         assert_match(got, want, op, dtype, ctx=f"PE {me} {op}/{dtype} {kind}:")
+    # the tensor form of the call (shmem_reduce.Shmem.to_all_tensors)
+    for k, (op, tdt) in enumerate([("sum", torch.float64), ("min", torch.int16), ("xor", torch.int64),
+                                   ("prod", torch.complex64), ("max", torch.float32), ("or", torch.int32)]):
+        name = shmem_reduce.TORCH_DTYPES[str(tdt).replace("torch.", "")]
+        n = 10007 + 999 * k
+        srcs = [source(op, name, n, 1700 + k, pe) for pe in range(npes)]
+        x = torch.from_numpy(srcs[me]).cuda()
+        out = torch.empty_like(x)
+        shm.to_all_tensors(op, out, x)
+        assert shm.last_call_info()["schedule"].startswith("mapped-")
+        assert_match(out.cpu().numpy(), oracle.reduce_pe(op, name, srcs, me), op, name,
+                     ctx=f"PE {me} to_all_tensors {op}/{tdt}:")
     shm.barrier_all()
     print(json.dumps({"pe": me, "schedules": scheds, "map_stats": shm.external_map_stats()}), flush=True)
     shm.finalize()

@@ -116,3 +116,6 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
     # the init coherence test ran on the real layout (here: one GPU) and passed
     c = d["coherence_selftest"]
     assert c["ran"] and c["passed"], c
+    # the same call on plain hipMalloc buffers: mapped by the peers, not staged
+    e = d["external_buffers"]
+    assert e["schedule"] == "mapped-p2p" and e["check"].startswith("bit-exact") and e["mappings_opened"] >= 1, e
