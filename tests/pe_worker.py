@@ -260,6 +260,7 @@ def main():
     assert hip.hipMalloc(ctypes.byref(pb), ctypes.c_size_t(maxb + 4096)) == 0
     priv_a, priv_b = pa.value, pb.value
     results = {}
+    fds_start = len(os.listdir("/proc/self/fd"))
     for c in spec["cases"]:
         if c.get("kind") == "config":
             run_config(shm, c, me, results)
@@ -376,6 +377,7 @@ def main():
         if n and c.get("api") != "fortran":
             results[str(c["id"]) + "_schedule"] = np.array([shm.last_call_info()["schedule"]])
     results["external_map_stats"] = np.array(shm.external_map_stats())
+    results["fd_count"] = np.array([fds_start, len(os.listdir("/proc/self/fd"))])
     hip.hipFree(pa)
     hip.hipFree(pb)
     shm.free(hb)

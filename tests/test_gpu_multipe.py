@@ -424,6 +424,9 @@ def test_external_device_buffers_mapped(tmp_path):
         mapped, opened, closed = (int(v) for v in results[pe]["external_map_stats"])
         # two hipMalloc allocations per peer, each opened once for all the calls
         assert opened <= 4 and closed == 0 and mapped == opened, (pe, mapped, opened, closed)
+        # exports are cached per allocation: no file descriptor per call
+        fd0, fd1 = (int(v) for v in results[pe]["fd_count"])
+        assert fd1 - fd0 <= 8, (pe, fd0, fd1)
 
 
 def test_external_device_buffers_fallbacks(tmp_path):
