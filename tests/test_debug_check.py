@@ -113,3 +113,20 @@ def test_settings_must_agree(tmp_path):
     outs = [o for _, o in res]
     assert all(rc != 0 for rc, _ in res) and not any("INIT-RETURNED" in o for o in outs), outs
     assert any("SHMEM_REDUCE_ORDER differs between PEs" in o for o in outs), outs
+
+
+def test_external_map_setting_must_agree(tmp_path):
+    """SHMEM_EXTERNAL_MAP decides whether a member joins the per-call record
+    exchange for device buffers outside the heap (csrc/extmap.c): PEs that
+    differ would wait on each other for ever, so init aborts naming it."""
+    import os
+    body = """
+    print('INIT-RETURNED', flush=True)
+    shm.finalize()
+    """
+    with open(os.path.join(str(tmp_path), "sitecustomize.py"), "w") as f:
+        f.write("import os\nif os.environ.get('SHMEM_PE') == '1': os.environ['SHMEM_EXTERNAL_MAP'] = '0'\n")
+    res = spawn(2, body, tmp_path, extra={"PYTHONPATH": str(tmp_path)})
+    outs = [o for _, o in res]
+    assert all(rc != 0 for rc, _ in res) and not any("INIT-RETURNED" in o for o in outs), outs
+    assert any("SHMEM_EXTERNAL_MAP differs between PEs" in o for o in outs), outs
