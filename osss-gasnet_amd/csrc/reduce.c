@@ -875,7 +875,11 @@ static int ptr_kind (const void *p, size_t nbytes)
  * chunk k-1 (stream out) run while chunk k is reduced: with host buffers the
  * two PCIe directions then work at the same time.
  *   A0/A1 = halves of scratch A (sources), B0/B1 = halves of scratch B (results)
- * PE_size == 1 is the identity: each chunk goes in to A and straight back out. */
+ * PE_size == 1 is the identity: each chunk goes in to A and straight back out.
+ * A target that overlaps the source from above is walked top down (memmove
+ * order, like the reference's temporary target, reduce-op.c:174-215): the
+ * copy-out of a chunk then only writes source bytes already copied in, while
+ * the copy-in of the next chunk (below) runs beside it. */
 static void staged (int op, int dtype, const char *fn, void *target, const void *source, size_t n,
                     const struct aset *s, int ks, int kt, int use_rccl)
 {
@@ -889,30 +893,34 @@ static void staged (int op, int dtype, const char *fn, void *target, const void 
     const hipMemcpyKind in_kind = ks == PK_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice;
     const hipMemcpyKind out_kind = kt == PK_HOST ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
     const int identity = s->size == 1;
+    const int down = (const char *) target > (const char *) source &&
+                     (const char *) target < (const char *) source + n * es;
 
-#define CHUNK_N(k) (n - (k) * per < per ? n - (k) * per : per)
+#define CHUNK_ID(k) (down ? nchunks - 1 - (k) : (k)) /* the k-th chunk processed */
+#define CHUNK_N(c) (n - (c) * per < per ? n - (c) * per : per)
     for (size_t k = 0; k < nchunks + 1; ++k) {
-        /* copy-in of chunk k (issued one chunk ahead of its reduction) */
+        /* copy-in of the k-th chunk (issued one chunk ahead of its reduction) */
         if (k < nchunks) {
             const int j = (int) (k & 1);
-            if (k >= 2) /* A[j] was last read by the copy-out (identity) or reduction of chunk k-2 */
+            const size_t c = CHUNK_ID (k);
+            if (k >= 2) /* A[j] was last read by the copy-out (identity) or reduction of the (k-2)-th chunk */
                 SHMEMI_HIP (hipStreamWaitEvent (shmemi.stream_in, shmemi.ev_out[j], 0));
-            SHMEMI_HIP (hipMemcpyAsync (shmemi.heap + a_off[j], (const char *) source + k * per * es,
-                                        CHUNK_N (k) * es, in_kind, shmemi.stream_in));
+            SHMEMI_HIP (hipMemcpyAsync (shmemi.heap + a_off[j], (const char *) source + c * per * es,
+                                        CHUNK_N (c) * es, in_kind, shmemi.stream_in));
             SHMEMI_HIP (hipEventRecord (shmemi.ev_in[j], shmemi.stream_in));
         }
         if (k == 0)
             continue;
-        /* reduce and copy out chunk c = k - 1 */
-        const size_t c = k - 1;
-        const int j = (int) (c & 1);
+        /* reduce and copy out the (k-1)-th chunk */
+        const size_t q = k - 1, c = CHUNK_ID (q);
+        const int j = (int) (q & 1);
         const size_t cn = CHUNK_N (c);
         size_t out_off = a_off[j];
         if (identity) {
             SHMEMI_HIP (hipStreamWaitEvent (shmemi.stream_out, shmemi.ev_in[j], 0));
         } else {
             SHMEMI_HIP (hipEventSynchronize (shmemi.ev_in[j])); /* peers read A[j] after the barrier */
-            if (c >= 2) /* B[j] is still being copied out for chunk c-2 */
+            if (q >= 2) /* B[j] is still being copied out for the (q-2)-th chunk */
                 SHMEMI_HIP (hipStreamWaitEvent (shmemi.stream, shmemi.ev_out[j], 0));
             out_off = b_off[j];
             if (use_rccl) {
@@ -927,6 +935,7 @@ static void staged (int op, int dtype, const char *fn, void *target, const void 
         SHMEMI_HIP (hipEventRecord (shmemi.ev_out[j], shmemi.stream_out));
     }
 #undef CHUNK_N
+#undef CHUNK_ID
     SHMEMI_HIP (hipStreamSynchronize (shmemi.stream_out));
     SHMEMI_HIP (hipStreamSynchronize (shmemi.stream_in));
 }
@@ -1010,6 +1019,9 @@ static void debug_check (const char *fn, int op, int dtype, const void *target, 
             r.toff = shmemi_heap_offset (target);
         if (r.skind == PK_DEV_SYM)
             r.soff = shmemi_heap_offset (source);
+        /* the staging path walks its chunks in an order the members share */
+        const char *t = (const char *) target, *sr = (const char *) source;
+        r.overlap = t == sr ? 1 : t > sr && t < sr + nbytes ? 2 : sr > t && sr < t + nbytes ? 3 : 0;
     }
     r.algorithm = shmemi.algorithm;
     r.order = shmemi.order;

@@ -409,6 +409,7 @@ static const char *dbg_diff (const struct shmemi_dbg_rec *a, const struct shmemi
     F (soff, "source offset in the device symmetric heap")
     F (algorithm, "reduce algorithm (shmemx_set_reduce_algorithm)")
     F (order, "result order (shmemx_set_reduce_order)")
+    F (overlap, "target/source relation (0 disjoint, 1 the same buffer, 2 target overlapping above source, 3 below)")
 #undef F
     if (strcmp (a->fn, b->fn) != 0) {
         *va = *vb = 0;

@@ -31,7 +31,8 @@ struct shmemi_dbg_rec {
     int32_t pad0;
     int32_t op, dtype, nreduce, pe_start, log_stride, pe_size;
     int32_t tkind, skind;       /* 0 host, 1 device heap, 2 other device memory */
-    int32_t algorithm, order, persistent, pad;
+    int32_t algorithm, order, persistent;
+    int32_t overlap;            /* target vs source: 0 disjoint, 1 same, 2 overlapping above, 3 below */
     uint64_t toff, soff;        /* heap offsets (device heap kinds), else 0 */
     char fn[48];
 };

@@ -306,6 +306,14 @@ def main():
                 src, dst = priv_a, priv_b
             else:
                 src, dst = ha, hb
+        elif mode == "host_overlap_up":      # page-locked host arrays, target 5 elements above source
+            src, dst = ha, ha + 5 * es
+        elif mode == "host_overlap_down":    # target 5 elements below source
+            src, dst = ha + 5 * es, ha
+        elif mode == "devother_overlap_up":  # hipMalloc buffer, target 5 elements above source
+            src, dst = priv_a, priv_a + 5 * es
+        elif mode == "devother_overlap_down":
+            src, dst = priv_a + 5 * es, priv_a
         elif mode == "devmap_inplace":   # one hipMalloc buffer, target == source
             src = dst = priv_a
         elif mode == "devmap_offset":    # each PE's buffers at other offsets into its allocations

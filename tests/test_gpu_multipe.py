@@ -458,6 +458,23 @@ def test_external_device_buffers_fallbacks(tmp_path):
         assert tuple(int(v) for v in results[0]["external_map_stats"]) == (0, 0, 0)
 
 
+@pytest.mark.parametrize("npes", [1, 2])
+def test_overlapping_buffers_outside_the_heap(tmp_path, npes):
+    """Target 5 elements above / below source in host arrays and in hipMalloc
+    memory, over several scratch chunks: the result is the fold of the
+    original sources (the reference's temporary target, reduce-op.c:174-215),
+    whatever order the staging copies run in."""
+    cases = []
+    cid = 0
+    for mode in ("host_overlap_up", "host_overlap_down", "devother_overlap_up", "devother_overlap_down"):
+        for n in (1000, 300000):
+            cases += make_cases([("sum", "double"), ("max", "int"), ("xor", "short")], n, [[0, 0, npes]], mode,
+                                "p2p", cid)
+            cid += 100
+    results = run_pes(npes, cases, tmp_path, extra_env={"SHMEM_DEVICE_SCRATCH_SIZE": "3M"})
+    check(results, cases)
+
+
 def test_signal_region_mapping_failure_falls_back(tmp_path):
     """One PE cannot map the peers' signal regions (SHMEM_TEST_IPC_FAIL=sig
     on PE 1): init must not abort; every PE agrees to run without device-side
