@@ -413,6 +413,8 @@ def test_external_device_buffers_mapped(tmp_path):
             cases += make_cases(MAPPED_PAIRS, n, [[0, 0, 3]], mode, "p2p", cid)
             cid += 100
     cases += make_cases(MAPPED_PAIRS[:3], 5000, [[0, 1, 2]], "devother", "p2p", cid)  # strided set {0, 2}
+    cases += make_cases(MAPPED_PAIRS, 20000, [[0, 0, 3]], "devother", "exact", cid + 100)  # EXACT schedule
+    cases += make_cases(MAPPED_PAIRS, 200000, [[0, 0, 3]], "devmap_offset", "p2p", cid + 200, order="pe_start")
     results = run_pes(3, cases, tmp_path, extra_env={"SHMEM_DEVICE_SCRATCH_SIZE": "3M"})
     check(results, cases)
     for c in cases:
