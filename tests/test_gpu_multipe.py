@@ -477,6 +477,30 @@ def test_overlapping_buffers_outside_the_heap(tmp_path, npes):
     check(results, cases)
 
 
+def test_random_sequence_stress_outside_heap(tmp_path):
+    """200 back-to-back reductions on buffers outside the heap -- hipMalloc
+    memory mapped by the peers (whole, at per-PE offsets, in place, heap
+    target, one PE unaligned), host arrays, overlapping targets -- with random
+    op/type, size and active set, including two disjoint sets at once: the
+    per-call record exchange and the staging paths stay in step."""
+    rng = np.random.default_rng(2027)
+    sets_choices = [[[0, 0, 4]], [[0, 1, 2], [1, 1, 2]], [[1, 0, 3]], [[0, 0, 2], [2, 0, 2]]]
+    modes = ["devother", "devmap_offset", "devmap_inplace", "devmap_symtarget", "devmap_unaligned_pe1", "host",
+             "devother_mixed", "host_overlap_up", "devother_overlap_up", "devother_overlap_down", "dev"]
+    cases = []
+    for cid in range(200):
+        op, dtype = oracle.PAIRS[rng.integers(len(oracle.PAIRS))]
+        n = int(rng.choice([0, 1, 7, 1000, 8192, 40000, 150000, 300000]))
+        cases.append({"id": cid, "op": op, "dtype": dtype, "n": n, "sets": sets_choices[rng.integers(4)],
+                      "mode": str(rng.choice(modes)), "algorithm": str(rng.choice(["p2p", "p2p", "exact"])),
+                      "seed": 9000 + cid})
+    results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_DEVICE_HEAP_SIZE": "64M",
+                                                     "SHMEM_DEVICE_SCRATCH_SIZE": "3M",
+                                                     "SHMEM_DEVICE_ORDER_SIZE": "256K",
+                                                     "SHMEM_EXTERNAL_MAP_CACHE": "3"})
+    check(results, cases)
+
+
 def test_signal_region_mapping_failure_falls_back(tmp_path):
     """One PE cannot map the peers' signal regions (SHMEM_TEST_IPC_FAIL=sig
     on PE 1): init must not abort; every PE agrees to run without device-side
