@@ -925,6 +925,7 @@ static void interconnect_selftest (void)
         shmemi.algorithm = SHMEMX_REDUCE_RCCL;
         shmemi.p2p_broken = 1;
         shmemi.fused_max = 0; /* its kernels read the peers' heaps too: every PE takes the same path */
+        shmemi.ext_map = 0;   /* peers' other allocations would be mapped the same way (extmap.c) */
     }
     shmemi_barrier_set (0, 1, np);
 }
