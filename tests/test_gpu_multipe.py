@@ -477,12 +477,14 @@ def test_overlapping_buffers_outside_the_heap(tmp_path, npes):
     check(results, cases)
 
 
-def test_random_sequence_stress_outside_heap(tmp_path):
+@pytest.mark.parametrize("persistent", ["0", "1"], ids=["launched", "persistent-server"])
+def test_random_sequence_stress_outside_heap(tmp_path, persistent):
     """200 back-to-back reductions on buffers outside the heap -- hipMalloc
     memory mapped by the peers (whole, at per-PE offsets, in place, heap
     target, one PE unaligned), host arrays, overlapping targets -- with random
     op/type, size and active set, including two disjoint sets at once: the
-    per-call record exchange and the staging paths stay in step."""
+    per-call record exchange and the staging paths stay in step; with the
+    opt-in persistent server too (heap calls served, the others stop it)."""
     rng = np.random.default_rng(2027)
     sets_choices = [[[0, 0, 4]], [[0, 1, 2], [1, 1, 2]], [[1, 0, 3]], [[0, 0, 2], [2, 0, 2]]]
     modes = ["devother", "devmap_offset", "devmap_inplace", "devmap_symtarget", "devmap_unaligned_pe1", "host",
@@ -497,7 +499,8 @@ def test_random_sequence_stress_outside_heap(tmp_path):
     results = run_pes(4, cases, tmp_path, extra_env={"SHMEM_DEVICE_HEAP_SIZE": "64M",
                                                      "SHMEM_DEVICE_SCRATCH_SIZE": "3M",
                                                      "SHMEM_DEVICE_ORDER_SIZE": "256K",
-                                                     "SHMEM_EXTERNAL_MAP_CACHE": "3"})
+                                                     "SHMEM_EXTERNAL_MAP_CACHE": "3",
+                                                     "SHMEM_PERSISTENT": persistent})
     check(results, cases)
 
 
