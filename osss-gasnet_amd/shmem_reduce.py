@@ -197,6 +197,30 @@ class Shmem:
             raise TypeError(f"no shmem_*_to_all for {source.dtype}")
         self.to_all(op, dtype, target.data_ptr(), source.data_ptr(), source.numel(), PE_start, logPE_stride, PE_size)
 
+    def heap_tensor(self, n, dtype):
+        """A 1-D torch tensor of n elements of torch dtype `dtype` in the
+        device symmetric heap (collective, like shmemx_malloc_device): the
+        buffer the stream-ordered, graph-capturable reductions take. The tensor
+        does not own the memory: free it with free_device(t.data_ptr()) once
+        no tensor or queued work uses it."""
+        import torch
+        name = TORCH_DTYPES.get(str(dtype).replace("torch.", ""))
+        if name is None:
+            raise TypeError(f"no shmem_*_to_all for {dtype}")
+        np_dt = np.dtype(NP[name])
+        ptr = self.malloc_device(max(1, n) * np_dt.itemsize)
+        if not ptr:
+            raise MemoryError("device symmetric heap exhausted")
+
+        class _HeapBuffer:
+            __cuda_array_interface__ = {"shape": (n,), "typestr": np_dt.str, "data": (ptr, False), "version": 3,
+                                        "strides": None}
+
+        t = torch.as_tensor(_HeapBuffer(), device=f"cuda:{self.lib.shmemx_device_id()}")
+        if t.data_ptr() != ptr:
+            raise RuntimeError("torch copied the heap buffer instead of wrapping it")
+        return t
+
     def _stream_reduction(self, op, dtype):
         key = ("stream", op, dtype)
         f = self._fns.get(key)
