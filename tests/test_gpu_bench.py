@@ -51,6 +51,9 @@ def common(d, n):
     for name in ("float_max", "longlong_and"):
         assert d["op_coverage"][name]["check"].startswith("bit-exact"), d["op_coverage"]
     assert d["small_call"]["us_per_call"] > 0
+    g = d["small_call_graph"]
+    assert g["us_per_call"] > 0 and g["check"].startswith("bit-exact") and g["calls"] == 4096, g
+    assert g["schedule"] == ("stream-identity" if n == 1 else "stream-fused-oneshot"), g
 
 
 def test_bench_one_gpu_line():
