@@ -174,9 +174,9 @@ def traffic_for(rec, key, host):
     """HBM bytes per launch from the PMC passes committed in
     profiles/pmc_traffic.json (tools/pmc_traffic.py: FETCH_SIZE x 2 +
     WRITE_SIZE, gfx950 correction), put into rec["traffic"] only when the
-    entry was profiled from kernel sources with the hash of this tree
-    (shmem_reduce.kernel_source_hash); otherwise traffic stays null and the
-    returned note says why."""
+    entry was profiled from this library's machine code (hash of its gfx950
+    code objects, shmem_reduce.kernel_code_hash); otherwise traffic stays null
+    and the returned note says why."""
     if host:
         return "host-staged run: no PMC profile"
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
@@ -186,13 +186,13 @@ def traffic_for(rec, key, host):
         tr = None
     if not tr:
         return f"no PMC profile for {key} in profiles/pmc_traffic.json"
-    want = shmem_reduce.kernel_source_hash()
-    if tr.get("kernel_src_sha") != want:
-        return (f"profiles/pmc_traffic.json[{key}] was taken from kernel sources {tr.get('kernel_src_sha')}, this "
-                f"tree is {want}: not reported")
+    want = shmem_reduce.kernel_code_hash()
+    if tr.get("kernel_code_sha") != want:
+        return (f"profiles/pmc_traffic.json[{key}] was taken from kernel code {tr.get('kernel_code_sha')}, this "
+                f"library's is {want}: not reported")
     rec["traffic"] = tr["hbm_bytes_per_launch"]
     rec["traffic_source"] = tr["source"]
-    return f"PMC passes of this tree's kernels (kernel sources {want})"
+    return f"PMC passes of this library's kernels (gfx950 code objects {want})"
 
 
 def persistent_child(rank, world, calls):

@@ -6,7 +6,6 @@ OpenSHMEM test program in C would call it. It never computes a reduction
 itself: if the library is missing, loading fails loudly.
 """
 import ctypes
-import glob
 import hashlib
 import os
 
@@ -330,21 +329,25 @@ def bench_loop(path=BENCH_LIB_PATH, name="double_sum"):
     return f
 
 
-def kernel_source_hash():
-    """sha256 (16 hex digits) of everything that decides the kernels' code:
-    csrc/*.hip, csrc/*.h, csrc/Makefile and include/mi355_reduce.h. PMC
-    counter profiles (profiles/pmc_traffic.json) carry the hash of the tree
-    they were taken from; bench.py reports their HBM traffic only for the
-    same hash."""
-    root = os.path.dirname(HERE)
-    files = sorted(glob.glob(os.path.join(HERE, "csrc", "*.hip")) + glob.glob(os.path.join(HERE, "csrc", "*.h")) +
-                   [os.path.join(HERE, "csrc", "Makefile"), os.path.join(root, "include", "mi355_reduce.h")])
-    h = hashlib.sha256()
-    for f in files:
-        h.update(os.path.relpath(f, root).encode())
-        with open(f, "rb") as fh:
-            h.update(fh.read())
-    return h.hexdigest()[:16]
+def kernel_code_hash(path=LIB_PATH):
+    """sha256 (16 hex digits) of the gfx950 code objects the library carries
+    (its .hip_fatbin ELF section): the machine code PMC counter profiles
+    describe. Host-only changes leave it unchanged; any change to a kernel,
+    a kernel header or the device compile flags changes it (the build is
+    deterministic: rebuilding the same sources gives the same bytes).
+    profiles/pmc_traffic.json records it per entry and bench.py reports an
+    entry's HBM traffic only for a library with the same hash."""
+    import struct
+    with open(path, "rb") as f:
+        b = f.read()
+    shoff = struct.unpack_from("<Q", b, 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, 0x3A)
+    secs = [struct.unpack_from("<IIQQQQ", b, shoff + i * shentsize) for i in range(shnum)]
+    stroff = secs[shstrndx][4]
+    for name, _typ, _flags, _addr, off, size in secs:
+        if b[stroff + name:b.index(b"\0", stroff + name)] == b".hip_fatbin":
+            return hashlib.sha256(b[off:off + size]).hexdigest()[:16]
+    raise RuntimeError(f"{path} has no .hip_fatbin section")
 
 
 def shard_bounds(lib, n, elem_size, nshards, i):

@@ -90,3 +90,12 @@ def test_constants_match_reference_values():
     assert "#define SHMEM_REDUCE_SYNC_SIZE          (256L / SHMEM_INTERNAL_F2C_SCALE)" in text
     assert "#define SHMEM_REDUCE_MIN_WRKDATA_SIZE   (128L / SHMEM_INTERNAL_F2C_SCALE)" in text
     assert "#define SHMEM_SYNC_VALUE (-1L)" in text
+
+
+def test_kernel_code_hash_reads_the_fatbin():
+    """bench.py ties PMC traffic to the library's gfx950 code objects
+    (shmem_reduce.kernel_code_hash, the .hip_fatbin section): present, and
+    the same value on every read."""
+    import shmem_reduce
+    h = shmem_reduce.kernel_code_hash()
+    assert len(h) == 16 and int(h, 16) >= 0 and h == shmem_reduce.kernel_code_hash()

@@ -4,9 +4,9 @@ bytes per launch of the bench's dominant kernel, with the gfx950 correction
 of MI355X_MICROARCH.md (HBM section): FETCH_SIZE counts half the bytes of a
 wide (16 B/lane) coalesced streaming read, so it is doubled; WRITE_SIZE is
 exact for 16-B streaming stores. Both counters are in KB (1024 B). Each
-entry records the hash of the kernel sources it was taken from
-(shmem_reduce.kernel_source_hash): bench.py reports an entry's traffic only
-for a tree with the same hash.
+entry records the hash of the gfx950 code objects it was taken from
+(shmem_reduce.kernel_code_hash): bench.py reports an entry's traffic only
+for a library with the same machine code.
 
 usage: pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR MIN_GRID KEY [out.json]
 """
@@ -17,7 +17,7 @@ import os
 import sys
 
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "osss-gasnet_amd"))
-import shmem_reduce  # noqa: E402  (kernel_source_hash only; nothing is loaded)
+import shmem_reduce  # noqa: E402  (kernel_code_hash only; the library is read, not loaded)
 
 
 def per_dispatch(d, counter, kname, min_grid):
@@ -43,7 +43,7 @@ def main():
     write = sorted(w)[len(w) // 2] * 1024
     res = {"fetch_size_bytes_raw": fetch, "write_size_bytes": write,
            "hbm_bytes_per_launch": 2 * fetch + write,
-           "kernel_src_sha": shmem_reduce.kernel_source_hash(),
+           "kernel_code_sha": shmem_reduce.kernel_code_hash(),
            "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), median of {len(f)}/{len(w)} "
                      f"dispatches of {kname}; FETCH_SIZE x2 (gfx950 wide-read correction)"}
     print(json.dumps({key: res}, indent=1))
