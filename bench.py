@@ -550,7 +550,7 @@ def main():
     # SHMEM_REDUCE_ALGORITHM=rccl) for comparison with the P2P schedule; the
     # headline value stays the default schedule's
     t_rccl_local = None
-    distinct_gpus = False
+    distinct_gpus = shared_gpu = False
     if npes > 1:
         # RCCL refuses two ranks on one device: compare only with one GPU per
         # PE. Same GPU = same PCI bus id (not the HIP ordinal, which is 0 on
@@ -559,7 +559,8 @@ def main():
                           dtype=np.int32)
         anyshared = np.zeros(1, dtype=np.int32)
         shm.to_all("max", "int", anyshared.ctypes.data, shared.ctypes.data, 1, 0, 0, npes)
-        distinct_gpus = int(anyshared[0]) == 0 or args.force_rccl_compare
+        shared_gpu = int(anyshared[0]) != 0
+        distinct_gpus = not shared_gpu or args.force_rccl_compare
     rccl_ok = False
     # RCCL prints a version banner on stdout at communicator creation; keep
     # stdout to the one JSON line by pointing fd 1 at stderr meanwhile
@@ -792,9 +793,18 @@ def main():
                                                                  "this PE's target shard and the other members' "
                                                                  "versions" if info["ordered"] else
                                                                  "this PE's target shard")}}
-        if not distinct_gpus:
-            roofline["note"] = ("the PEs share ONE GPU (test layout): the 'remote' reads are this GPU's own HBM, "
-                                "so achieved/frac here are not xGMI figures")
+        if shared_gpu:
+            # PEs sharing ONE GPU (test layout): the 'remote' reads are this
+            # GPU's own HBM, so the bound is HBM; the link view is kept aside
+            xv = {k: roofline.pop(k) for k in ("bound", "achieved", "peak", "frac", "alg_bytes_per_launch",
+                                               "peak_note")}
+            h = roofline.pop("hbm")
+            roofline = {"bound": "hbm", "achieved": h["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": h["frac"], "traffic": None, "alg_bytes_per_launch": h["bytes_per_launch"],
+                        **roofline, "hbm_note": h["note"], "xgmi_view": xv,
+                        "note": "the PEs share ONE GPU (test layout): every 'remote' read is this GPU's own HBM, "
+                                "so the fold is HBM-bound here; xgmi_view is what the line reports with one GPU "
+                                "per PE (not a link rate here)"}
     roofline["traffic_note"] = traffic_for(roofline, f"n{npes}_{args.mib}mib", args.host)
 
     # N > 1: bus bandwidth of the reduce-scatter + all-gather exchange against
@@ -823,7 +833,7 @@ def main():
             if shm.lib.shmemx_peer_link(q, ctypes.byref(lt), ctypes.byref(hp)) == 0:
                 links[str(q)] = {"type": {4: "xgmi", 2: "pcie"}.get(lt.value, str(lt.value)), "hops": hp.value}
         xgmi["links_from_pe0"] = links or None
-        if not distinct_gpus:
+        if shared_gpu:
             xgmi["note"] = ("the PEs share ONE GPU (test layout): peer 'xGMI' reads are local HBM reads, so "
                             "these figures are not xGMI rates")
 

@@ -44,10 +44,12 @@ def common(d, n):
     if n == 1:
         assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] < 1.2 and r["achieved"] > 0
     else:
-        # N > 1: the reduce-scatter fold's remote reads against the links into the GPU
-        assert r["bound"] == "xgmi" and r["peak"] == (n - 1) * 153.0 and r["achieved"] > 0
-        assert r["alg_bytes_per_launch"] == (n - 1) * (d["config"]["bytes_per_pe"] // n)
-        assert r["hbm"]["peak"] == 8000.0 and r["hbm"]["achieved"] > 0
+        # N > 1: the reduce-scatter fold's remote reads against the links into the GPU; here
+        # (PEs sharing the test GPU) its local-HBM view, the link view kept aside
+        x = r["xgmi_view"]
+        assert x["bound"] == "xgmi" and x["peak"] == (n - 1) * 153.0 and x["achieved"] > 0
+        assert x["alg_bytes_per_launch"] == (n - 1) * (d["config"]["bytes_per_pe"] // n)
+        assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] < 1.2
     for name in ("float_max", "longlong_and"):
         assert d["op_coverage"][name]["check"].startswith("bit-exact"), d["op_coverage"]
     assert d["small_call"]["us_per_call"] > 0
@@ -110,7 +112,7 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
     assert re.fullmatch(r"void mi355k::combine_vec<0, double, 2, \d, \d>\(mi355k::CombineParams\)", r["kernel"]), r
     shard = S // 2
     assert r["call"]["schedule"] == "p2p" and r["call"]["sources"] == 2 and r["call"]["outputs"] == 1, r
-    assert r["alg_bytes_per_launch"] == shard and r["hbm"]["bytes_per_launch"] == 3 * shard, r
+    assert r["xgmi_view"]["alg_bytes_per_launch"] == shard and r["alg_bytes_per_launch"] == 3 * shard, r
     # the opt-in persistent server at N > 1 (a child job of one PE per rank)
     sp = d["small_call_persistent"]
     assert "error" not in sp, sp
