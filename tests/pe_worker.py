@@ -314,6 +314,12 @@ def main():
             src, dst = priv_a, priv_a + 5 * es
         elif mode == "devother_overlap_down":
             src, dst = priv_a + 5 * es, priv_a
+        elif mode == "mixed_heapdst_hostsrc":   # target in the device heap, source a host array
+            src, dst = ha, db
+        elif mode == "mixed_hostdst_heapsrc":   # target a host array, source in the device heap
+            src, dst = da, hb
+        elif mode == "mixed_hostdst_devsrc":    # target a host array, source a hipMalloc buffer
+            src, dst = priv_a, hb
         elif mode == "devmap_inplace":   # one hipMalloc buffer, target == source
             src = dst = priv_a
         elif mode == "devmap_offset":    # each PE's buffers at other offsets into its allocations
@@ -345,8 +351,10 @@ def main():
             src, dst = da + es, db + es
         else:
             raise ValueError(mode)
+        host_src = mode.startswith("host") or mode == "mixed_heapdst_hostsrc"
+        host_dst = mode.startswith("host") or mode in ("mixed_hostdst_heapsrc", "mixed_hostdst_devsrc")
         if n:
-            if mode.startswith("host"):
+            if host_src:
                 ctypes.memmove(src, x.ctypes.data, x.nbytes)
             else:
                 shm.put(src, x)
@@ -375,7 +383,7 @@ def main():
             results[str(c["id"]) + "_seconds"] = np.array([time.perf_counter() - busy_t0])
             assert hip.hipStreamSynchronize(st) == 0
             hip.hipStreamDestroy(st)
-        if mode.startswith("host"):
+        if host_dst:
             out = np.empty(n, dtype=shmem_reduce.NP[dtype])
             if n:
                 ctypes.memmove(out.ctypes.data, dst, out.nbytes)

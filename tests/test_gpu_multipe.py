@@ -460,6 +460,22 @@ def test_external_device_buffers_fallbacks(tmp_path):
         assert tuple(int(v) for v in results[0]["external_map_stats"]) == (0, 0, 0)
 
 
+@pytest.mark.parametrize("npes", [1, 3])
+def test_mixed_memory_kinds(tmp_path, npes):
+    """Target and source of different kinds on every PE (heap target + host
+    source, host target + heap source, host target + hipMalloc source), in
+    one and several scratch chunks: staged, every PE's result exact."""
+    cases = []
+    cid = 0
+    for mode in ("mixed_heapdst_hostsrc", "mixed_hostdst_heapsrc", "mixed_hostdst_devsrc"):
+        for n in (1, 1000, 300000):
+            cases += make_cases([("sum", "double"), ("max", "float"), ("or", "long")], n, [[0, 0, npes]], mode,
+                                "p2p", cid)
+            cid += 100
+    results = run_pes(npes, cases, tmp_path, extra_env={"SHMEM_DEVICE_SCRATCH_SIZE": "3M"})
+    check(results, cases)
+
+
 @pytest.mark.parametrize("npes", [1, 2])
 def test_overlapping_buffers_outside_the_heap(tmp_path, npes):
     """Target 5 elements above / below source in host arrays and in hipMalloc
