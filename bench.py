@@ -551,6 +551,7 @@ def main():
     # headline value stays the default schedule's
     t_rccl_local = None
     distinct_gpus = shared_gpu = False
+    pes_on_gpu = 1   # PEs on this PE's GPU, itself included (test layouts share one)
     if npes > 1:
         # RCCL refuses two ranks on one device: compare only with one GPU per
         # PE. Same GPU = same PCI bus id (not the HIP ordinal, which is 0 on
@@ -560,6 +561,7 @@ def main():
         anyshared = np.zeros(1, dtype=np.int32)
         shm.to_all("max", "int", anyshared.ctypes.data, shared.ctypes.data, 1, 0, 0, npes)
         shared_gpu = int(anyshared[0]) != 0
+        pes_on_gpu = 1 + int(shared[0])
         distinct_gpus = not shared_gpu or args.force_rccl_compare
     rccl_ok = False
     # RCCL prints a version banner on stdout at communicator creation; keep
@@ -799,12 +801,20 @@ def main():
             xv = {k: roofline.pop(k) for k in ("bound", "achieved", "peak", "frac", "alg_bytes_per_launch",
                                                "peak_note")}
             h = roofline.pop("hbm")
-            roofline = {"bound": "hbm", "achieved": h["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": h["frac"], "traffic": None, "alg_bytes_per_launch": h["bytes_per_launch"],
+            # the PEs' folds run at once (they start after the same device
+            # barrier and take the same time), so the GPU's HBM carries
+            # pes_on_gpu launches' bytes in one kernel duration
+            dev = h["achieved"] * pes_on_gpu
+            roofline = {"bound": "hbm", "achieved": round(dev, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(dev / HBM_PEAK_GBS, 4), "traffic": None,
+                        "alg_bytes_per_launch": h["bytes_per_launch"], "pes_on_gpu": pes_on_gpu,
+                        "per_launch_achieved": h["achieved"], "per_launch_frac": h["frac"],
                         **roofline, "hbm_note": h["note"], "xgmi_view": xv,
                         "note": "the PEs share ONE GPU (test layout): every 'remote' read is this GPU's own HBM, "
-                                "so the fold is HBM-bound here; xgmi_view is what the line reports with one GPU "
-                                "per PE (not a link rate here)"}
+                                "so the fold is HBM-bound here; its %d PEs' folds run concurrently, so achieved = "
+                                "%d x one launch's bytes / its duration (per_launch_* = one PE's share); "
+                                "xgmi_view is what the line reports with one GPU per PE (not a link rate here)"
+                                % (pes_on_gpu, pes_on_gpu)}
     roofline["traffic_note"] = traffic_for(roofline, f"n{npes}_{args.mib}mib", args.host)
 
     # N > 1: bus bandwidth of the reduce-scatter + all-gather exchange against
@@ -852,7 +862,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (splitmix64 full-mantissa doubles, device-resident symmetric heap)",
-            "config": {"workload": f"shmem_double_sum_to_all, {npes} PE = {npes} GPU, {args.mib} MiB "
+            "config": {"workload": f"shmem_double_sum_to_all, {npes} PE = {npes} GPU"
+                                   f"{f' (test layout: {pes_on_gpu} PEs share each GPU)' if shared_gpu else ''}, {args.mib} MiB "
                                    f"{'host-memory (staged)' if args.host else 'device-resident'} array per PE", "nreduce": n, "bytes_per_pe": S,
                        "algorithm": "rccl (fallback: P2P self-test failed)" if rccl_fallback else args.algorithm,
                        "parallelism": f"pe{npes}"},

@@ -113,6 +113,9 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
     shard = S // 2
     assert r["call"]["schedule"] == "p2p" and r["call"]["sources"] == 2 and r["call"]["outputs"] == 1, r
     assert r["xgmi_view"]["alg_bytes_per_launch"] == shard and r["alg_bytes_per_launch"] == 3 * shard, r
+    # both PEs' folds share this GPU's HBM: the device rate is twice one launch's
+    assert r["pes_on_gpu"] == 2 and abs(r["achieved"] - 2 * r["per_launch_achieved"]) < 1.0, r
+    assert "2 PEs share each GPU" in d["config"]["workload"], d["config"]
     # the opt-in persistent server at N > 1 (a child job of one PE per rank)
     sp = d["small_call_persistent"]
     assert "error" not in sp, sp
