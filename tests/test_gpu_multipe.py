@@ -501,12 +501,12 @@ def test_random_sequence_stress_outside_heap(tmp_path, persistent):
     op/type, size and active set, including two disjoint sets at once: the
     per-call record exchange and the staging paths stay in step; with the
     opt-in persistent server too (heap calls served, the others stop it)."""
-    rng = np.random.default_rng(2027)
+    rng = np.random.default_rng(int(os.environ.get("SHMEM_TEST_STRESS_SEED", "2027")))
     sets_choices = [[[0, 0, 4]], [[0, 1, 2], [1, 1, 2]], [[1, 0, 3]], [[0, 0, 2], [2, 0, 2]]]
     modes = ["devother", "devmap_offset", "devmap_inplace", "devmap_symtarget", "devmap_unaligned_pe1", "host",
              "devother_mixed", "host_overlap_up", "devother_overlap_up", "devother_overlap_down", "dev"]
     cases = []
-    for cid in range(200):
+    for cid in range(int(os.environ.get("SHMEM_TEST_STRESS_CALLS", "200"))):
         op, dtype = oracle.PAIRS[rng.integers(len(oracle.PAIRS))]
         n = int(rng.choice([0, 1, 7, 1000, 8192, 40000, 150000, 300000]))
         cases.append({"id": cid, "op": op, "dtype": dtype, "n": n, "sets": sets_choices[rng.integers(4)],
@@ -535,10 +535,10 @@ def test_random_sequence_stress(tmp_path):
     across the fused/multi-launch threshold), buffer mode, schedule and active
     set -- including two disjoint sets running at once -- on 4 PEs. Catches
     races between consecutive calls (a PE racing ahead into the next call)."""
-    rng = np.random.default_rng(2026)
+    rng = np.random.default_rng(int(os.environ.get("SHMEM_TEST_STRESS_SEED", "2026")))
     sets_choices = [[[0, 0, 4]], [[0, 1, 2], [1, 1, 2]], [[1, 0, 3]], [[0, 0, 2], [2, 0, 2]], [[0, 0, 4]]]
     cases = []
-    for cid in range(300):
+    for cid in range(int(os.environ.get("SHMEM_TEST_STRESS_CALLS", "300"))):
         op, dtype = oracle.PAIRS[rng.integers(len(oracle.PAIRS))]
         n = int(rng.choice([0, 1, 7, 64, 1000, 8191, 40000, 150000, 300000]))
         mode = str(rng.choice(["dev", "dev", "inplace", "host", "host_mixed"]))
