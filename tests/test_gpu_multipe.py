@@ -554,6 +554,28 @@ def test_random_sequence_stress(tmp_path):
     check(results, cases)
 
 
+def test_random_sequence_stress_eight_pes(tmp_path):
+    """The random sequence on 8 PEs (the driver's largest job size): whole-job
+    sets (every-member fold of 8 sources in registers), halves, strided
+    quarters (logPE_stride 2: PEs {q, q+4}), a 7-member set starting at PE 1,
+    several disjoint sets at once; heap, in place, host and mapped hipMalloc
+    buffers; fused one-shot / two-shot, multi-launch (in rounds) and EXACT."""
+    rng = np.random.default_rng(int(os.environ.get("SHMEM_TEST_STRESS_SEED", "2028")))
+    sets_choices = [[[0, 0, 8]], [[0, 0, 4], [4, 0, 4]], [[0, 2, 2], [1, 2, 2], [2, 2, 2], [3, 2, 2]],
+                    [[1, 0, 7]], [[0, 1, 4], [1, 1, 4]], [[0, 0, 8]]]
+    cases = []
+    for cid in range(int(os.environ.get("SHMEM_TEST_STRESS_CALLS", "120"))):
+        op, dtype = oracle.PAIRS[rng.integers(len(oracle.PAIRS))]
+        n = int(rng.choice([0, 1, 7, 1000, 8192, 40000, 150000, 300000]))
+        cases.append({"id": cid, "op": op, "dtype": dtype, "n": n, "sets": sets_choices[rng.integers(len(sets_choices))],
+                      "mode": str(rng.choice(["dev", "dev", "inplace", "host", "devother", "devmap_offset"])),
+                      "algorithm": str(rng.choice(["p2p", "p2p", "p2p", "exact"])), "seed": 11000 + cid})
+    results = run_pes(8, cases, tmp_path, extra_env={"SHMEM_DEVICE_HEAP_SIZE": "64M",
+                                                     "SHMEM_DEVICE_SCRATCH_SIZE": "3M",
+                                                     "SHMEM_DEVICE_ORDER_SIZE": "1M"})
+    check(results, cases)
+
+
 # The RCCL schedule (SHMEM_REDUCE_ALGORITHM=rccl, csrc/rccl.c) with more than
 # one rank. RCCL refuses two ranks on one GPU of one host ("Duplicate GPU
 # detected"), and the test box has one GPU, so each PE announces a host of its
