@@ -368,6 +368,8 @@ def main():
                          "256 MiB, config 3 / 4's per-GPU reduce-scatter shapes)")
     ap.add_argument("--no-external", action="store_true",
                     help="N > 1: skip the leg on plain hipMalloc buffers (outside the symmetric heap)")
+    ap.add_argument("--no-link-probe", action="store_true",
+                    help="N > 1: skip PE 0's one-peer-at-a-time shmem_getmem / shmem_putmem rates")
     ap.add_argument("--kernel-reps", type=int, default=50)
     ap.add_argument("--no-fused", action="store_true",
                     help="N = 1: skip the fused-kernel leg (2 PE processes sharing this GPU, 64 KiB and 1 MiB calls)")
@@ -753,6 +755,53 @@ def main():
             if b.value:
                 hip.hipFree(b)
 
+    # N > 1: what one link carries alone -- PE 0 pulls 64 MiB from each peer's
+    # heap with shmem_getmem (the copy kernel reading the peer mapping, as the
+    # all-gather leg does) and pushes it back with shmem_putmem (the runtime's
+    # P2P copy), one peer at a time, the others waiting in a barrier. Beside
+    # xgmi.ag_kernel_remote_read_GB_s (all peers at once) it says whether the
+    # schedule is bound by the links or by how it drives them.
+    link_probe = None
+    if npes > 1 and not args.host and not args.no_link_probe:
+        import ctypes
+        # two 16 MiB buffers fit the heap's 64 MiB beside the headline's
+        nbp, reps = min(S, 16 << 20), 10
+        psym, ploc = shm.malloc_device(nbp), shm.malloc_device(nbp)
+        if not psym or not ploc:
+            raise SystemExit("link probe: shmemx_malloc_device of 2 x %d bytes failed" % nbp)
+        shm.put(psym, synth(me, np.arange(nbp // 8, dtype=np.uint64)))
+        shm.barrier_all()
+        get, put = shm.lib.shmem_getmem, shm.lib.shmem_putmem
+        for f in (get, put):
+            f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+            f.restype = None
+        peers = {}
+        if me == 0:
+            for q in range(1, npes):
+                rec = {}
+                for name, f, a, b in (("get_GB_s", get, ploc, psym), ("put_GB_s", put, psym, ploc)):
+                    f(a, b, nbp, q)
+                    tq0 = time.perf_counter()
+                    for _ in range(reps):
+                        f(a, b, nbp, q)
+                    shm.sync()
+                    rec[name] = round(nbp * reps / (time.perf_counter() - tq0) / 1e9, 1)
+                peers[str(q)] = rec
+            ok = True
+            if not args.no_check:   # the last get brought PE npes-1's bytes
+                got = shm.get(ploc, 1 << 16, "double").view(np.uint64)
+                ok = bool((got == synth(npes - 1, np.arange(1 << 16, dtype=np.uint64)).view(np.uint64)).all())
+        shm.barrier_all()
+        shm.free_device(ploc)
+        shm.free_device(psym)
+        if me == 0:
+            link_probe = {"bytes": nbp, "reps": reps, "from_pe0": peers,
+                          "check": "skipped" if args.no_check else "bit-exact" if ok else "MISMATCH",
+                          "note": "PE 0 alone, one peer at a time: shmem_getmem (copy kernel pulling over the "
+                                  "peer mapping) and shmem_putmem (HIP P2P copy) of 16 MiB, blocking calls"
+                                  + ("; the PEs share ONE GPU here: local HBM copies, not link rates"
+                                     if shared_gpu else "")}
+
     # dominant kernel and its algorithmic bytes per launch, from the schedule
     # the library reports for the timed calls (shmemx_last_call_info)
     launches = max(1, info["launches"])
@@ -887,6 +936,7 @@ def main():
             "check": check,
             "op_coverage": ops,
             "external_buffers": external,
+            "link_probe": link_probe,
             "kernels": kernels,
             "fused_same_gpu": fused,
             "fused_same_gpu_persistent": fused_p,
