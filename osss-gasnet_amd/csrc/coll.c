@@ -81,6 +81,8 @@ static void pull (void **dsts, const void **srcs, size_t *nbytes, int nseg);
 static void put_bytes (const char *fn, void *dest, const void *src, size_t nbytes, int pe)
 {
     shmemi_init_check (fn);
+    if (nbytes > 0 && (dest == NULL || src == NULL))
+        shmemi_fatal ("%s: NULL %s (%zu bytes, PE %d)", fn, dest == NULL ? "dest" : "source", nbytes, pe);
     if (shmemi.heap != NULL)
         shmemi_server_stop ();
     check_pe (fn, pe);
@@ -112,6 +114,8 @@ static void put_bytes (const char *fn, void *dest, const void *src, size_t nbyte
 static void get_bytes (const char *fn, void *dest, const void *src, size_t nbytes, int pe)
 {
     shmemi_init_check (fn);
+    if (nbytes > 0 && (dest == NULL || src == NULL))
+        shmemi_fatal ("%s: NULL %s (%zu bytes, PE %d)", fn, dest == NULL ? "dest" : "source", nbytes, pe);
     if (shmemi.heap != NULL)
         shmemi_server_stop ();
     check_pe (fn, pe);

@@ -133,3 +133,24 @@ def test_identity_from_torchrun_env(tmp_path):
     for p in procs:
         out, _ = p.communicate(timeout=60)
         assert p.returncode == 0, out
+
+
+def test_get_put_with_null_buffer_name_it(tmp_path):
+    """shmem_getmem / shmem_putmem with a NULL local buffer (e.g. an unchecked
+    failed shmemx_malloc_device) abort with the call and the argument named,
+    before any GPU work."""
+    body = """
+    f = shm.lib.shmem_getmem if me == 0 else shm.lib.shmem_putmem
+    f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    x = (ctypes.c_char * 64)()
+    if me == 0:
+        f(None, ctypes.addressof(x), 64, 1)
+    else:
+        f(ctypes.addressof(x), None, 64, 0)
+    print('UNREACHABLE')
+    """
+    res = spawn(2, body, tmp_path)
+    for rc, out in res:
+        assert rc != 0 and "UNREACHABLE" not in out, out
+    assert any("shmem_getmem: NULL dest" in out for _, out in res), res
+    assert any("shmem_putmem: NULL source" in out or "aborting" in out for _, out in res), res
