@@ -425,10 +425,15 @@ def main():
     coherence = None
     if npes > 1:
         ran, passed, stale = shm.coherence_selftest()
+        sysload, no_acq = shm.coherence_sysload()
         coherence = {"ran": ran, "passed": passed, "stale_without_acquire": stale,
+                     "sysload_fresh": sysload, "fused_acquires_skipped": no_acq,
                      "note": "every PE read each peer's marker through its L2, the peer rewrote it (write-through), "
                              "and the re-read after mi355_acquire_system must see the new value; "
-                             "stale_without_acquire: a re-read without the acquire returned the old value"}
+                             "stale_without_acquire: a re-read without the acquire returned the old value; "
+                             "sysload_fresh: system-coherent (sc0 sc1) loads, the fused kernel's reads of the "
+                             "members' buffers, saw every new value before any acquire, so the fused kernel "
+                             "skips its per-block acquires (fused_acquires_skipped)"}
     if args.host:
         import ctypes
         src, dst = shm.malloc(S), shm.malloc(S)

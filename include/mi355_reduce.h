@@ -178,6 +178,12 @@ typedef struct MI355FusedArgs {
      * the grid is capped at the kernel's resident blocks per CU (one fewer, as a margin) x CUs / share,
      * so every such grid can be resident at once and no spinning block keeps a peer's from starting. */
     int share;
+    /* Every read of the members' buffers is a system-coherent load (sc0 sc1: never served from a
+     * stale cache line), so the waits need no cache invalidation. 0: each block also runs a
+     * system-scope acquire (buffer_inv sc0 sc1) after each wait -- one per block, which queue up
+     * at every XCD's L2 on large grids. 1: it skips them; set only when the init coherence test
+     * showed system-coherent loads of peers' rewritten memory fresh without any acquire. */
+    int no_acquire;
 } MI355FusedArgs;
 
 /* Reduce-scatter + all-gather of n elements over the members in ONE launch:
@@ -285,6 +291,10 @@ int mi355_peek (const unsigned long long *const *src, int n, unsigned long long 
  * -- into out[b * n + i]. */
 int mi355_peek_cached (const unsigned long long *const *src, int n, unsigned long long *out, int nblocks,
                        void *stream);
+/* The same with system-coherent loads (sc0 sc1, as the fused kernel reads the members' buffers) and
+ * no fence: out[b * n + i]. */
+int mi355_peek_sysload (const unsigned long long *const *src, int n, unsigned long long *out, int nblocks,
+                        void *stream);
 
 /* Shard i of nshards for n elements of elem_size bytes: the P2P schedule's
  * partition (contiguous, shard starts 256-byte aligned, trailing shards may

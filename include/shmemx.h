@@ -174,6 +174,12 @@ int shmemx_last_call_info (shmemx_call_info *info);
  * P2P schedules queue before reading peers' buffers is needed). All three
  * are the job's (OR / AND over the PEs). */
 void shmemx_coherence_selftest (int *ran, int *passed, int *stale_without_acquire);
+/* The same test's check of system-coherent loads (sc0 sc1, the fused kernel's
+ * reads of the members' buffers), made before any acquire: sysload_fresh =
+ * every block of every PE saw every peer's new value; acquires_skipped = the
+ * fused kernel therefore runs without its per-block system-scope acquires
+ * (SHMEM_FUSED_ACQUIRE=1 keeps them). */
+void shmemx_coherence_sysload (int *sysload_fresh, int *acquires_skipped);
 
 /* Bring up the RCCL communicator of the whole job (what SHMEM_REDUCE_ALGORITHM=rccl uses) without
  * aborting when RCCL cannot come up within timeout_s seconds: 0 = ready on this PE, -1 = not. Every PE

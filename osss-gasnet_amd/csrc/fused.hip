@@ -55,6 +55,33 @@ using namespace mi355;
 constexpr int kBlock = 256;
 constexpr int kBatch = 8;  // members' vectors in flight per lane in the fold
 
+// Probe build only (csrc/Makefile `probe`, tools/fused_phases.py): the real-time
+// stamps of each call's phases, per call epoch in a ring of 64 -- [0] first
+// block start, [1] last block start, [2] last block past the ARRIVE wait, [3]
+// last block done folding, [4] last block past the RSDONE wait, [5] last block
+// done gathering, [6] the grid's last block past the AGDONE wait.
+#ifdef MI355_FUSED_PHASES
+__device__ unsigned long long g_phase[64][8];
+#define PHASE_MAX(c, k)                                                                             \
+    do {                                                                                            \
+        if (threadIdx.x == 0)                                                                       \
+            atomicMax(&g_phase[(c).epoch & 63][k], (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
+    } while (0)
+#define PHASE_MIN(c, k)                                                                             \
+    do {                                                                                            \
+        if (threadIdx.x == 0)                                                                       \
+            atomicMin(&g_phase[(c).epoch & 63][k], (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
+    } while (0)
+#define PHASE_RESET_NEXT(c)                                                                         \
+    do {                                                                                            \
+        if (threadIdx.x < 8) g_phase[((c).epoch + 1) & 63][threadIdx.x] = threadIdx.x == 0 ? ~0ull : 0ull; \
+    } while (0)
+#else
+#define PHASE_MAX(c, k) ((void)0)
+#define PHASE_MIN(c, k) ((void)0)
+#define PHASE_RESET_NEXT(c) ((void)0)
+#endif
+
 __device__ __forceinline__ void st_sys_u64(unsigned long long *p, unsigned long long v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -65,6 +92,46 @@ __device__ __forceinline__ unsigned long long ld_sys_u64(const unsigned long lon
 // over xGMI after the flag that follows it
 __device__ __forceinline__ void st16_sys(u32x4 *p, u32x4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+
+// Loads of the members' buffers (their sources, targets, version areas), at
+// system scope: `global_load_dwordx2 ... sc0 sc1` never returns a stale L2 or
+// L1 line -- a peer GPU's memory is cached without coherence (non-coherent
+// MTYPE), and on one GPU the 8 XCD L2s are not coherent with each other -- so
+// a block reads what the members wrote for THIS call without invalidating its
+// caches first (MI355FusedArgs.no_acquire). Every such byte is read once per
+// call, so bypassing the caches costs nothing.
+__device__ __forceinline__ u32x4 ld16_sys(const void *p) {
+    const unsigned long long *q = (const unsigned long long *)p;
+    const unsigned long long lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned long long hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    u32x4 r;
+    r.x = (unsigned)lo;
+    r.y = (unsigned)(lo >> 32);
+    r.z = (unsigned)hi;
+    r.w = (unsigned)(hi >> 32);
+    return r;
+}
+template <typename T>
+__device__ __forceinline__ T ld_elem_sys(const T *p) {
+    static_assert(sizeof(T) == 2 || sizeof(T) == 4 || sizeof(T) == 8 || sizeof(T) == 16, "element size");
+    T v;
+    if constexpr (sizeof(T) == 16) {
+        const u32x4 w = ld16_sys(p);
+        __builtin_memcpy(&v, &w, 16);
+    } else if constexpr (sizeof(T) == 8) {
+        const unsigned long long w =
+            __hip_atomic_load((const unsigned long long *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_memcpy(&v, &w, 8);
+    } else if constexpr (sizeof(T) == 4) {
+        const unsigned w = __hip_atomic_load((const unsigned *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_memcpy(&v, &w, 4);
+    } else {
+        const unsigned short w =
+            __hip_atomic_load((const unsigned short *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __builtin_memcpy(&v, &w, 2);
+    }
+    return v;
 }
 
 // This call's pair count with every member (lanes of wave 0, into LDS).
@@ -92,8 +159,10 @@ __device__ bool wait_members(const MI355FusedArgs &a, const unsigned long long *
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        if (i == 0) {
-            // acquire at system scope: drop this CU's stale copies of peer data
+        if (i == 0 && !a.no_acquire) {
+            // acquire at system scope: drop this CU's and XCD's stale copies of
+            // peer data (redundant beside the system-coherent loads of the
+            // members' buffers; kept unless the init test showed those fresh)
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -204,7 +273,7 @@ __device__ __forceinline__ Pack<T> fold_vec(const MI355FusedArgs &a, const Call 
 #pragma unroll
         for (int j = 0; j < kBatch; ++j)
             if (k0 + j < nm)
-                x[j].v = ((const u32x4 *)(src_of(a, c, order_member(k0 + j, first)) + lo * sizeof(T)))[v];
+                x[j].v = ld16_sys((const u32x4 *)(src_of(a, c, order_member(k0 + j, first)) + lo * sizeof(T)) + v);
 #pragma unroll
         for (int j = 0; j < kBatch; ++j) {
             if (k0 + j >= nm) break;
@@ -227,7 +296,7 @@ __device__ __forceinline__ T fold_elem(const MI355FusedArgs &a, const Call &c, u
         T x[kBatch];
 #pragma unroll
         for (int j = 0; j < kBatch; ++j)
-            if (k0 + j < nm) x[j] = ((const T *)src_of(a, c, order_member(k0 + j, first)))[i];
+            if (k0 + j < nm) x[j] = ld_elem_sys((const T *)src_of(a, c, order_member(k0 + j, first)) + i);
 #pragma unroll
         for (int j = 0; j < kBatch; ++j) {
             if (k0 + j >= nm) break;
@@ -258,7 +327,7 @@ __device__ __forceinline__ void versions_vec(const MI355FusedArgs &a, const Call
             Pack<T> x[kBatch];
 #pragma unroll
             for (int j = 0; j < kBatch; ++j)
-                if (j < nm) x[j].v = ((const u32x4 *)(src_of(a, c, j) + lo * sizeof(T)))[v];
+                if (j < nm) x[j].v = ld16_sys((const u32x4 *)(src_of(a, c, j) + lo * sizeof(T)) + v);
 #pragma unroll
             for (int q = 0; q < kBatch; ++q) {
                 if (q >= nm) break;
@@ -300,6 +369,8 @@ __device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &
     } else {
         load_counts(a, mine, cnt);
     }
+    PHASE_MIN(c, 0);
+    PHASE_MAX(c, 1);
 
     const bool staged = a.host_src != nullptr;
     if (staged) {
@@ -323,6 +394,7 @@ __device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &
     __syncthreads();
     if (!wait_members(a, mine, cnt, MI355_SIG_ARRIVE, staged)) ok_all = 0;
     __syncthreads();
+    PHASE_MAX(c, 2);
     if (!ok_all) goto fail;
 
     {
@@ -363,12 +435,14 @@ __device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &
                 if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // plain tail stores
             }
         }
+        PHASE_MAX(c, 3);
         if (!oneshot) {
             if (last_block(mine + MI355_SIG_RS_COUNT)) publish(a, cnt, MI355_SIG_RSDONE);
 
             // ---- every shard is reduced
             if (!wait_members(a, mine, cnt, MI355_SIG_RSDONE, true)) ok_all = 0;
             __syncthreads();
+            PHASE_MAX(c, 4);
             if (!ok_all) goto fail;
 
             // ---- gather the other shards: one grid-stride loop over all of
@@ -387,10 +461,10 @@ __device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &
                                                        (uint64_t)(a.me < j ? a.me : a.me - 1) * c.shard * sizeof(T)) - e0 + r0
                                          : (const T *)dst_of(a, c, j);
                 if (e0 + V <= c.n) {
-                    const u32x4 v = *(const u32x4 *)(from + e0);
+                    const u32x4 v = ld16_sys(from + e0);
                     st16_sys((u32x4 *)(dst_of(a, c, a.me) + e0 * sizeof(T)), v);
                 } else {
-                    for (uint64_t e = e0; e < c.n; ++e) ((T *)dst_of(a, c, a.me))[e] = from[e];
+                    for (uint64_t e = e0; e < c.n; ++e) ((T *)dst_of(a, c, a.me))[e] = ld_elem_sys(from + e);
                     tail_plain = true;
                 }
             }
@@ -401,12 +475,15 @@ __device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         if (__syncthreads_or(tail_plain) && threadIdx.x == 0)
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // the element tail went through L2
+        PHASE_MAX(c, 5);
         if (last_block(mine + MI355_SIG_AG_COUNT)) {
             publish(a, cnt, MI355_SIG_AGDONE);
             if (!staged) {
                 __syncthreads();
                 if (!wait_members(a, mine, cnt, MI355_SIG_AGDONE, true)) ok_all = 0;
                 __syncthreads();
+                PHASE_MAX(c, 6);
+                PHASE_RESET_NEXT(c);
                 finish(a, mine, cnt, ok_all != 0, c.epoch);
                 return;
             }
@@ -554,7 +631,11 @@ __global__ __launch_bounds__(kBlock) void fused_server(MI355FusedArgs a, MI355Se
         const Call c{u64(2), u64(4), u64(6), u64(8), f[10], (int)f[11]};
         if (a.nmembers == 1) {
             // the 1-PE identity: nobody to wait for -- copy, count the
-            // blocks out, the last one reports
+            // blocks out, the last one reports. The caller may have rewritten
+            // the source since the last call (other XCDs' kernels, DMA): drop
+            // this CU's and XCD's copies of it first
+            if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            __syncthreads();
             block_copy(dst_of(a, c, 0), src_of(a, c, 0), c.n * sizeof(T), blockIdx.x, gridDim.x);
             if (last_block(a.sig[0] + MI355_SIG_AG_COUNT) && threadIdx.x == 0)
                 __hip_atomic_store(a.host_flag, c.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -753,6 +834,12 @@ __global__ __launch_bounds__(kBlock) void peek_cached_kernel(PokeParams p) {
     for (int i = threadIdx.x; i < p.n; i += kBlock) p.out[(size_t)blockIdx.x * p.n + i] = *p.ptr[i];
 }
 
+// System-coherent loads, no fence: what the fused kernel's reads of the
+// members' buffers see without an acquire (the init coherence test).
+__global__ __launch_bounds__(kBlock) void peek_sysload_kernel(PokeParams p) {
+    for (int i = threadIdx.x; i < p.n; i += kBlock) p.out[(size_t)blockIdx.x * p.n + i] = ld_sys_u64(p.ptr[i]);
+}
+
 }  // namespace
 
 extern "C" int mi355_poke(unsigned long long *const *dst, int n, unsigned long long value, void *stream) {
@@ -789,6 +876,20 @@ extern "C" int mi355_peek_cached(const unsigned long long *const *src, int n, un
     p.out = out;
     p.n = n;
     hipLaunchKernelGGL(peek_cached_kernel, dim3(nblocks), dim3(kBlock), 0, (hipStream_t)stream, p);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+extern "C" int mi355_peek_sysload(const unsigned long long *const *src, int n, unsigned long long *out, int nblocks,
+                                  void *stream) {
+    if (n < 0 || n > kMaxPoke || nblocks < 1 || nblocks > 256 || (n > 0 && (src == nullptr || out == nullptr)))
+        return MI355_E_INVAL;
+    if (n == 0) return 0;
+    PokeParams p{};
+    for (int i = 0; i < n; ++i) p.ptr[i] = const_cast<unsigned long long *>(src[i]);
+    p.out = out;
+    p.n = n;
+    hipLaunchKernelGGL(peek_sysload_kernel, dim3(nblocks), dim3(kBlock), 0, (hipStream_t)stream, p);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
@@ -894,3 +995,16 @@ extern "C" int mi355_fused_server(const MI355FusedArgs *a, MI355ServerMailbox *m
     default: return MI355_E_INVAL;
     }
 }
+
+#ifdef MI355_FUSED_PHASES
+// probe build: copy the phase ring out (64 calls x 8 stamps)
+extern "C" int mi355_fused_phases(unsigned long long *out) {
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_phase), sizeof(g_phase)) == hipSuccess ? 0 : -1;
+}
+extern "C" int mi355_fused_phases_reset(void) {
+    unsigned long long h[64][8];
+    for (int i = 0; i < 64; ++i)
+        for (int k = 0; k < 8; ++k) h[i][k] = k == 0 ? ~0ull : 0ull;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_phase), h, sizeof(h)) == hipSuccess ? 0 : -1;
+}
+#endif

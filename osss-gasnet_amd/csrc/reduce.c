@@ -242,6 +242,7 @@ static void member_args (MI355FusedArgs *a, const struct aset *s, int chan)
     a->err_flag = shmemi.stream_err;
     a->timeout_ticks = (unsigned long long) (shmemi.barrier_timeout * 1e8);
     a->share = shmemi.local_pes;
+    a->no_acquire = shmemi.fused_no_acquire;
 }
 
 /* The device-flag kernels can carry this active set's synchronization. */
@@ -713,6 +714,7 @@ static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t sr
         a.host_src = host_src;
         a.host_dst = host_dst;
         a.share = shmemi.local_pes;
+        a.no_acquire = shmemi.fused_no_acquire;
         a.oneshot = n * es <= shmemi.oneshot_max && dst_off != src_off;
         fused_order (&a, s, SHMEMI_CHAN_HOST);
         shmemi_timed_begin (); /* the call's one (dominant) kernel */

@@ -768,7 +768,7 @@ static void heap_exchange (void)
  *      (evidence the acquire is needed; not an error);
  *   4. mi355_acquire_system, re-read: every block must see every new value.
  * SHMEM_TEST_IPC_FAIL=stale makes PE 1 report step 4 stale (tests). */
-static void coherence_test (size_t mark_off, int *passed, int *stale)
+static void coherence_test (size_t mark_off, int *passed, int *stale, int *sysload)
 {
     const int np = shmemi.npes, me = shmemi.mype, nb = 32;
     const unsigned long long newval = 0xC0DE5EE000000000ull;
@@ -794,6 +794,16 @@ static void coherence_test (size_t mark_off, int *passed, int *stale)
         shmemi_fatal ("coherence test: poke launch failed");
     SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
     shmemi_barrier_set (0, 1, np);
+    /* 3a. system-coherent loads, no acquire (the fused kernel's reads of the
+     * members' buffers): every block must see every new value */
+    if (mi355_peek_sysload ((const unsigned long long *const *) ptrs, np, dev, nb, shmemi.stream) != 0)
+        shmemi_fatal ("coherence test: system-load peek launch failed");
+    SHMEMI_HIP (hipMemcpy (host, dev, sizeof (unsigned long long) * (size_t) np * nb, hipMemcpyDeviceToHost));
+    *sysload = 1;
+    for (int b = 0; b < nb; ++b)
+        for (int q = 0; q < np; ++q)
+            if (host[(size_t) b * np + q] != newval + (unsigned long long) q)
+                *sysload = 0;
     PEEK ("re-read without acquire");
     *stale = 0;
     for (int b = 0; b < nb; ++b)
@@ -811,7 +821,9 @@ static void coherence_test (size_t mark_off, int *passed, int *stale)
                 *passed = 0;
     const char *fail = me == 1 ? getenv ("SHMEM_TEST_IPC_FAIL") : NULL;
     if (fail != NULL && strcmp (fail, "stale") == 0)
-        *passed = 0, *stale = 1;
+        *passed = 0, *stale = 1, *sysload = 0;
+    if (fail != NULL && strcmp (fail, "sysload") == 0)
+        *sysload = 0; /* only the system-coherent loads stale: the fused kernel keeps its acquires */
     (void) hipFree (dev);
     free (host);
     free (ptrs);
@@ -888,9 +900,9 @@ static void interconnect_selftest (void)
         all_mapped &= (__atomic_load_n (&seg_info (q)->selftest, __ATOMIC_ACQUIRE) >> 1) & 1;
     int coh = 0;
     if (all_mapped) {
-        int passed = 1, stale = 0;
-        coherence_test (mark_off, &passed, &stale);
-        coh = 4 | (passed << 3) | (stale << 4);
+        int passed = 1, stale = 0, sysload = 0;
+        coherence_test (mark_off, &passed, &stale, &sysload);
+        coh = 4 | (passed << 3) | (stale << 4) | (sysload << 5);
         if (!passed)
             heap_ok = 0;
     }
@@ -901,12 +913,21 @@ static void interconnect_selftest (void)
     shmemi.coh_ran = all_mapped;
     shmemi.coh_passed = all_mapped;
     shmemi.coh_stale = 0;
+    shmemi.coh_sysload = all_mapped;
     for (int q = 0; q < np; ++q) {
         const int r = __atomic_load_n (&seg_info (q)->selftest, __ATOMIC_ACQUIRE);
         all_sig &= r & 1;
         all_heap &= (r >> 1) & 1;
         shmemi.coh_passed &= (r >> 3) & 1;
         shmemi.coh_stale |= (r >> 4) & 1;
+        shmemi.coh_sysload &= (r >> 5) & 1;
+    }
+    /* the fused kernel's per-block acquires are redundant when its
+     * system-coherent loads read fresh data on every PE (the same decision on
+     * every PE: from the same records); SHMEM_FUSED_ACQUIRE=1 keeps them */
+    {
+        static const char *acq_env[] = {"SHMEM_FUSED_ACQUIRE", NULL};
+        shmemi.fused_no_acquire = shmemi.coh_sysload && shmemi.coh_passed && env_long (acq_env, 0) == 0;
     }
     if (all_mapped && !shmemi.coh_passed && me == 0)
         fprintf (stderr, "[shmem] warning: a peer heap re-read after a system-scope acquire returned stale data "
@@ -1441,6 +1462,14 @@ void shmemx_coherence_selftest (int *ran, int *passed, int *stale_without_acquir
         *passed = shmemi.coh_passed;
     if (stale_without_acquire != NULL)
         *stale_without_acquire = shmemi.coh_stale;
+}
+
+void shmemx_coherence_sysload (int *sysload_fresh, int *acquires_skipped)
+{
+    if (sysload_fresh != NULL)
+        *sysload_fresh = shmemi.coh_sysload;
+    if (acquires_skipped != NULL)
+        *acquires_skipped = shmemi.fused_no_acquire;
 }
 
 int shmemx_get_reduce_order (void) { return shmemi.order; }

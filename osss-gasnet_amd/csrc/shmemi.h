@@ -171,6 +171,11 @@ struct shmemi_state {
 
     /* the init-time coherence test of peer-heap reads (job-wide results) */
     int coh_ran, coh_passed, coh_stale;
+    /* ... and whether system-coherent loads (the fused kernel's reads of the
+     * members' buffers) saw the rewritten data with no acquire at all, on
+     * every PE: then the fused kernel skips its per-block acquires
+     * (fused_no_acquire; SHMEM_FUSED_ACQUIRE=1 keeps them) */
+    int coh_sysload, fused_no_acquire;
 
     /* what the last *_to_all call ran (shmemx_last_call_info); the kernel
      * stub is resolved to its name only on request */

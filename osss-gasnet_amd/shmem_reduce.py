@@ -12,7 +12,10 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "libshmem_reduce.so")
+# SHMEM_REDUCE_LIBDIR: a variant build of the same library (e.g. lib/probe,
+# csrc/Makefile `probe`) for measurement tools; default: the in-tree lib/
+LIB_DIR = os.environ.get("SHMEM_REDUCE_LIBDIR") or os.path.join(HERE, "lib")
+LIB_PATH = os.path.join(LIB_DIR, "libshmem_reduce.so")
 
 OPS = ["sum", "prod", "and", "or", "xor", "min", "max"]           # enum mi355_op
 DTYPES = ["short", "int", "long", "longlong", "float", "double",   # enum mi355_dtype
@@ -71,6 +74,7 @@ def load(path=LIB_PATH):
         "shmemx_rccl_init": ([ctypes.c_double], _i),
         "shmemx_last_call_info": ([ctypes.POINTER(CallInfo)], _i),
         "shmemx_coherence_selftest": ([ctypes.POINTER(_i)] * 3, None),
+        "shmemx_coherence_sysload": ([ctypes.POINTER(_i)] * 2, None),
         "shmemx_kernel_timing_stats": ([ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double),
                                         ctypes.POINTER(ctypes.c_double)], None),
         "shmemx_kernel_timing_phase_stats": ([_i, ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_double),
@@ -299,6 +303,13 @@ class Shmem:
         self.lib.shmemx_coherence_selftest(ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
         return bool(a.value), bool(b.value), bool(c.value)
 
+    def coherence_sysload(self):
+        """(sysload_fresh, acquires_skipped): the coherence test's check of the
+        fused kernel's system-coherent loads, and whether its acquires are off"""
+        a, b = _i(), _i()
+        self.lib.shmemx_coherence_sysload(ctypes.byref(a), ctypes.byref(b))
+        return bool(a.value), bool(b.value)
+
     def kernel_timing(self, enable):
         self.lib.shmemx_kernel_timing(1 if enable else 0)
 
@@ -314,7 +325,7 @@ class Shmem:
         return n.value, tot.value, avg.value
 
 
-BENCH_LIB_PATH = os.path.join(HERE, "lib", "libshmem_bench.so")
+BENCH_LIB_PATH = os.path.join(LIB_DIR, "libshmem_bench.so")
 
 
 def bench_loop(path=BENCH_LIB_PATH, name="double_sum"):

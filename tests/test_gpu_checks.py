@@ -97,6 +97,39 @@ def test_stale_reread_falls_back_to_rccl():
     assert "init coherence test" in outs[0]
 
 
+SYSLOAD = ("import oracle\n"
+           "fresh, skipped = shm.coherence_sysload()\n"
+           "print('SYS', int(fresh), int(skipped), flush=True)\n"
+           "d = shm.malloc_device(40000 * 8); t = shm.malloc_device(40000 * 8)\n"
+           "bad = 0\n"
+           "for k in range(24):\n"
+           "    n = 40000 if k % 2 else 3000\n"          # fused two-shot (ordered) / one-shot
+           "    xs = [np.random.default_rng(1000 * k + p).random(n) - 0.5 for p in range(npes)]\n"
+           "    shm.put(d, xs[me])\n"                     # the same buffers rewritten every call
+           "    shm.to_all('sum', 'double', t, d, n, 0, 0, npes)\n"
+           "    got = shm.get(t, n, 'double')\n"
+           "    bad += int((got.view(np.uint64) != oracle.reduce_pe('sum', 'double', xs, me).view(np.uint64)).sum())\n"
+           "print('BAD', bad, 'SCHED', shm.last_call_info()['schedule'], flush=True)\n"
+           "shm.finalize()\n")
+
+
+@pytest.mark.parametrize("env,want", [({}, ["1", "1"]), ({"SHMEM_TEST_IPC_FAIL": "sysload"}, ["0", "0"]),
+                                      ({"SHMEM_FUSED_ACQUIRE": "1"}, ["1", "0"])],
+                         ids=["acquires-skipped", "sysload-stale-keeps-acquires", "forced-acquires"])
+def test_fused_acquires_follow_the_sysload_check(env, want):
+    """The fused kernel reads the members' buffers with system-coherent loads
+    and skips its per-block acquires only when the init coherence test saw
+    those loads fresh on every PE: here (one GPU) they are; a simulated stale
+    result on PE 1, or SHMEM_FUSED_ACQUIRE=1, keeps the acquires. Every way,
+    24 calls on rewritten buffers (ordered two-shot and one-shot, 3 PEs) are
+    bit-exact on every PE."""
+    rcs, outs, _ = spawn(3, SYSLOAD, extra=env)
+    for rc, out in zip(rcs, outs):
+        assert rc == 0, out[-2000:]
+        assert parse(out, "SYS")[0] == want, out
+        assert parse(out, "BAD")[0] == ["0", "SCHED", "fused-twoshot"], out
+
+
 # ---------------------------------------------------------------------------
 # SHMEM_DEBUG=1 collective argument check
 # ---------------------------------------------------------------------------
