@@ -142,8 +142,11 @@ __device__ void load_counts(const MI355FusedArgs &a, const unsigned long long *m
 
 // Wait until slot `base + pe[i]` of this PE's signal region holds cnt[i]
 // for every member i; lanes i < nmembers of wave 0 poll one member each.
+// acquire = false only where every later read of the members' buffers is a
+// system-coherent load (fused_body under no_acquire); fused_pull's copies
+// read with plain loads and always acquire.
 __device__ bool wait_members(const MI355FusedArgs &a, const unsigned long long *mine, const unsigned long long *cnt,
-                             int base, bool include_self) {
+                             int base, bool include_self, bool acquire = true) {
     bool ok = true;
     if (threadIdx.x < 64) {
         const int i = threadIdx.x;
@@ -159,7 +162,7 @@ __device__ bool wait_members(const MI355FusedArgs &a, const unsigned long long *
             }
             __builtin_amdgcn_s_sleep(1);
         }
-        if (i == 0 && !a.no_acquire) {
+        if (i == 0 && acquire) {
             // acquire at system scope: drop this CU's and XCD's stale copies of
             // peer data (redundant beside the system-coherent loads of the
             // members' buffers; kept unless the init test showed those fresh)
@@ -392,7 +395,7 @@ __device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &
             st_sys_u64(a.sig[threadIdx.x] + MI355_SIG_ARRIVE + a.pe[a.me], cnt[threadIdx.x]);
     }
     __syncthreads();
-    if (!wait_members(a, mine, cnt, MI355_SIG_ARRIVE, staged)) ok_all = 0;
+    if (!wait_members(a, mine, cnt, MI355_SIG_ARRIVE, staged, !a.no_acquire)) ok_all = 0;
     __syncthreads();
     PHASE_MAX(c, 2);
     if (!ok_all) goto fail;
@@ -440,7 +443,7 @@ __device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &
             if (last_block(mine + MI355_SIG_RS_COUNT)) publish(a, cnt, MI355_SIG_RSDONE);
 
             // ---- every shard is reduced
-            if (!wait_members(a, mine, cnt, MI355_SIG_RSDONE, true)) ok_all = 0;
+            if (!wait_members(a, mine, cnt, MI355_SIG_RSDONE, true, !a.no_acquire)) ok_all = 0;
             __syncthreads();
             PHASE_MAX(c, 4);
             if (!ok_all) goto fail;
@@ -480,7 +483,7 @@ __device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &
             publish(a, cnt, MI355_SIG_AGDONE);
             if (!staged) {
                 __syncthreads();
-                if (!wait_members(a, mine, cnt, MI355_SIG_AGDONE, true)) ok_all = 0;
+                if (!wait_members(a, mine, cnt, MI355_SIG_AGDONE, true, !a.no_acquire)) ok_all = 0;
                 __syncthreads();
                 PHASE_MAX(c, 6);
                 PHASE_RESET_NEXT(c);
@@ -510,7 +513,7 @@ __device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &
         if (last_block(mine + MI355_SIG_STAGE_COUNT)) {
             if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             __syncthreads();
-            if (!wait_members(a, mine, cnt, MI355_SIG_AGDONE, true)) ok_all = 0;
+            if (!wait_members(a, mine, cnt, MI355_SIG_AGDONE, true, !a.no_acquire)) ok_all = 0;
             __syncthreads();
             finish(a, mine, cnt, ok_all != 0, c.epoch);
         }
