@@ -7,6 +7,8 @@ set -euo pipefail
 R=${1:-r03}
 mkdir -p gpurun_out/bench_$R
 timeout -k 10 600 bash tools/profile_round.sh "$R" > gpurun_out/profile_round_$R.log 2>&1
+# the bench lines below report the traffic just profiled (same code objects)
+cp gpurun_out/profiles/pmc_traffic.json profiles/pmc_traffic.json
 timeout -k 10 300 bash tools/profile_fused.sh "$R" > gpurun_out/profile_fused_$R.log 2>&1
 timeout -k 10 300 python3 bench.py > gpurun_out/bench_$R/bench_n1.json 2> gpurun_out/bench_$R/bench_n1.err
 timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
