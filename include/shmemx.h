@@ -39,6 +39,9 @@ int shmemx_is_device_symmetric (const void *ptr);
  * PE; stats = allocations mapped now, opened and closed since init. */
 void shmemx_external_map_flush (void);
 void shmemx_external_map_stats (long *mapped, long *opened, long *closed);
+/* Calls on mapped buffers that staged instead because a member could not open
+ * a peer's buffer (its export is re-made for the next call). */
+long shmemx_external_map_fallbacks (void);
 
 /* Cross-PE schedule for *_to_all (env SHMEM_REDUCE_ALGORITHM sets the
  * default at init):

@@ -28,6 +28,14 @@
  * (each member's result needs every member's source, which a member offers
  * only after reading them), so one barrier suffices: the next call may
  * rewrite the record.
+ *   5. opening a peer's handle can fail although the peer exported it: a
+ *      handle whose every importer has closed it (this cache's LRU
+ *      evictions, on every PE) cannot be opened again on this HIP (dmabuf
+ *      IPC: "invalid device pointer", seen intermittently in the random
+ *      stress with a 3-entry cache). So after opening, the members publish
+ *      whether they opened everything and pass a second barrier; if one did
+ *      not, every member stages this call and drops its cached exports of
+ *      the call's buffers, so the next call exports fresh handles.
  *
  * Imported mappings hold the peer's memory alive; the cache keeps at most
  * SHMEM_EXTERNAL_MAP_CACHE of them (default 64, least recently used closed
@@ -67,8 +75,9 @@ struct import {
 };
 static struct import *imports;
 static int n_imports, cap_imports;
+static long n_fallbacks; /* calls staged because a member could not open a peer's handle */
 static unsigned long long tick;
-static long n_opened, n_closed;
+static long n_opened, n_closed, n_open_failed;
 static int cache_limit; /* SHMEM_EXTERNAL_MAP_CACHE */
 
 static int export_of (const void *p, size_t nbytes, hipIpcMemHandle_t *h, uint64_t *off)
@@ -151,11 +160,18 @@ static char *import_of (int pe, const hipIpcMemHandle_t *h, unsigned long long f
         cap_imports = nc;
     }
     void *p = NULL;
-    const hipError_t e = hipIpcOpenMemHandle (&p, *h, hipIpcMemLazyEnablePeerAccess);
-    if (e != hipSuccess)
-        shmemi_fatal ("%s: mapping PE %d's device buffer (outside the symmetric heap) failed: %s; "
-                      "SHMEM_EXTERNAL_MAP=0 stages such buffers through the heap instead",
+    /* SHMEM_TEST_IPC_FAIL=extopen: PE 1 cannot open peers' buffers (tests) */
+    const char *fail = shmemi.mype == 1 ? getenv ("SHMEM_TEST_IPC_FAIL") : NULL;
+    const hipError_t e = fail != NULL && strcmp (fail, "extopen") == 0
+                             ? hipErrorInvalidDevicePointer
+                             : hipIpcOpenMemHandle (&p, *h, hipIpcMemLazyEnablePeerAccess);
+    if (e != hipSuccess) {
+        (void) hipGetLastError ();
+        ++n_open_failed;
+        SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "%s: mapping PE %d's device buffer failed (%s): the call stages",
                       call_fn, pe, hipGetErrorString (e));
+        return NULL;
+    }
     imports[n_imports++] = (struct import) {pe, *h, (char *) p, ++tick};
     ++n_opened;
     return (char *) p;
@@ -219,6 +235,7 @@ int shmemi_ext_begin (const char *fn, void *target, const void *source, size_t n
         if (tab[w] == NULL && (tab[w] = (char **) calloc ((size_t) shmemi.npes, sizeof (char *))) == NULL)
             shmemi_fatal ("out of host memory");
     const unsigned long long first = tick + 1;
+    int opened = 1;
     for (int i = 0; i < PE_size; ++i) {
         const int pe = PE_start + i * stride;
         if (pe == shmemi.mype) {
@@ -226,11 +243,34 @@ int shmemi_ext_begin (const char *fn, void *target, const void *source, size_t n
             tab[1][pe] = (char *) source;
             continue;
         }
-        tab[0][pe] = kt == SHMEMI_PK_DEV_OTHER ? import_of (pe, &rec[i].th, first) + rec[i].toff : NULL;
-        tab[1][pe] = same ? tab[0][pe]
-                          : ks == SHMEMI_PK_DEV_OTHER ? import_of (pe, &rec[i].sh, first) + rec[i].soff : NULL;
+        char *tb = kt == SHMEMI_PK_DEV_OTHER ? import_of (pe, &rec[i].th, first) : NULL;
+        char *sb = ks == SHMEMI_PK_DEV_OTHER && !same ? import_of (pe, &rec[i].sh, first) : NULL;
+        if ((kt == SHMEMI_PK_DEV_OTHER && tb == NULL) || (ks == SHMEMI_PK_DEV_OTHER && !same && sb == NULL))
+            opened = 0;
+        tab[0][pe] = tb != NULL ? tb + rec[i].toff : NULL;
+        tab[1][pe] = same ? tab[0][pe] : sb != NULL ? sb + rec[i].soff : NULL;
     }
     free (rec);
+    /* second round: did every member open everything? (the same answer on
+     * every member, read after the barrier from the same records) */
+    shmemi_seg_info (shmemi.mype)->ext.open_ok = opened;
+    atomic_thread_fence (memory_order_release);
+    shmemi_barrier_set (PE_start, stride, PE_size);
+    atomic_thread_fence (memory_order_acquire);
+    int all_opened = 1;
+    for (int i = 0; i < PE_size; ++i)
+        all_opened &= shmemi_seg_info (PE_start + i * stride)->ext.open_ok;
+    if (!all_opened) {
+        /* stage this call; export this call's buffers afresh next time */
+        for (int i = 0; i < n_exports; ++i)
+            if ((kt == SHMEMI_PK_DEV_OTHER && memcmp (&exports[i].h, &r.th, sizeof r.th) == 0) ||
+                (ks == SHMEMI_PK_DEV_OTHER && memcmp (&exports[i].h, &r.sh, sizeof r.sh) == 0)) {
+                exports[i] = exports[--n_exports];
+                --i;
+            }
+        ++n_fallbacks;
+        return 0;
+    }
     *toff = kt == SHMEMI_PK_DEV_SYM ? r.toff : SHMEMI_EXT_TARGET;
     *soff = ks == SHMEMI_PK_DEV_SYM ? r.soff : same ? SHMEMI_EXT_TARGET : SHMEMI_EXT_SOURCE;
     active = 1;
@@ -270,6 +310,8 @@ void shmemx_external_map_flush (void)
         import_close (n_imports - 1);
     n_exports = 0;
 }
+
+long shmemx_external_map_fallbacks (void) { return n_fallbacks; }
 
 void shmemx_external_map_stats (long *mapped, long *opened, long *closed)
 {

@@ -52,6 +52,8 @@ struct shmemi_ext_rec {
     int32_t tkind, skind;       /* 1 device heap, 2 other device memory */
     hipIpcMemHandle_t th, sh;
     uint64_t toff, soff;
+    int32_t open_ok;            /* second round: this member opened every peer's buffer */
+    int32_t pad;
 };
 
 struct shmemi_pe_info {

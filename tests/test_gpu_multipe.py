@@ -460,6 +460,22 @@ def test_external_device_buffers_fallbacks(tmp_path):
         assert tuple(int(v) for v in results[0]["external_map_stats"]) == (0, 0, 0)
 
 
+def test_external_buffer_open_failure_stages_the_call(tmp_path):
+    """A member that cannot open a peer's exported buffer (this HIP's dmabuf
+    IPC refuses a handle once every importer has closed it; simulated here on
+    PE 1, SHMEM_TEST_IPC_FAIL=extopen) does not abort the job: after the
+    second round of the record exchange every member stages the call, and the
+    results stay exact on every PE, fused and multi-launch sizes alike."""
+    cases = make_cases(MAPPED_PAIRS, 5000, [[0, 0, 3]], "devother", "p2p", 0)
+    cases += make_cases(MAPPED_PAIRS, 200000, [[0, 0, 3]], "devmap_offset", "p2p", 100)
+    results = run_pes(3, cases, tmp_path, extra_env={"SHMEM_DEVICE_SCRATCH_SIZE": "3M",
+                                                     "SHMEM_TEST_IPC_FAIL": "extopen"})
+    check(results, cases)
+    for c in cases:
+        for pe in range(3):
+            assert not str(results[pe][str(c["id"]) + "_schedule"][0]).startswith("mapped-"), (c["id"], pe)
+
+
 @pytest.mark.parametrize("npes", [1, 3])
 def test_mixed_memory_kinds(tmp_path, npes):
     """Target and source of different kinds on every PE (heap target + host
