@@ -42,10 +42,22 @@ __device__ __forceinline__ void store(u32x4 *p, u32x4 v) {
         *p = v;
 }
 
+// NT: 0 plain, 1 non-temporal, 2 system-coherent (two dwordx2 sc0 sc1, the
+// fused kernel's loads of the members' buffers)
 template <int NT>
 __device__ __forceinline__ u32x4 load(const u32x4 *p) {
-    if constexpr (NT) return __builtin_nontemporal_load(p);
-    else return *p;
+    if constexpr (NT == 2) {
+        const unsigned long long *q = (const unsigned long long *)p;
+        const unsigned long long lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned long long hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        u32x4 r;
+        r.x = (unsigned)lo; r.y = (unsigned)(lo >> 32); r.z = (unsigned)hi; r.w = (unsigned)(hi >> 32);
+        return r;
+    } else if constexpr (NT) {
+        return __builtin_nontemporal_load(p);
+    } else {
+        return *p;
+    }
 }
 
 // grid-stride, U vectors per lane, all K*U loads before the adds (the library's combine_vec)
@@ -531,7 +543,7 @@ int main(int argc, char **argv) {
     char name[128];
 #define RUN(KERNEL, K, U, ST, NT, BPC, SRCS, LABEL) do {                                            \
         Srcs s_ = (SRCS);                                                                           \
-        snprintf(name, sizeof name, "%s<U%d,%s,%s> %d/CU %s", #KERNEL, U, #ST, NT ? "nt-ld" : "ld",  \
+        snprintf(name, sizeof name, "%s<U%d,%s,%s> %d/CU %s", #KERNEL, U, #ST, NT == 2 ? "sys-ld" : NT ? "nt-ld" : "ld", \
                  BPC, LABEL);                                                                       \
         rep(name, K, time_us([&] { hipLaunchKernelGGL((KERNEL<K, U, ST, NT>), dim3(cus * BPC), dim3(256), 0, 0, \
                                                         s_, d, nvec); }));                          \
@@ -587,6 +599,19 @@ int main(int argc, char **argv) {
             RUN(fold_pp, 8, 2, ST_SC1, 1, 8, srcs_sep(), "compiler-scheduled ping-pong");
             RUN(fold_pp, 8, 2, ST_SC1, 1, 4, srcs_sep(), "compiler-scheduled ping-pong");
             RUN(fold_gs, 8, 4, ST_NONE, 1, 8, srcs_sep(), "no store: read ceiling");
+        }
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 's') {  // system-coherent loads (sc0 sc1) vs the library's load policies
+        for (int r = 0; r < 3; ++r) {
+            RUN(fold_gs, 8, 4, ST_SC1, 1, 8, srcs_sep(), "library shape k=8");
+            RUN(fold_gs, 8, 4, ST_SC1, 2, 8, srcs_sep(), "k=8, system-coherent loads");
+            RUN(fold_gs, 2, 1, ST_SC1, 1, 2, srcs_sep(), "library shape k=2");
+            RUN(fold_gs, 2, 1, ST_SC1, 2, 2, srcs_sep(), "k=2, system-coherent loads");
+            RUN(fold_gs, 2, 2, ST_SC1, 2, 2, srcs_sep(), "k=2, system-coherent loads");
+            RUN(fold_gs, 1, 4, ST_NT_SC1, 0, 1, srcs_sep(), "copy, library-like");
+            RUN(fold_gs, 1, 4, ST_NT_SC1, 2, 1, srcs_sep(), "copy, system-coherent loads");
+            RUN(fold_gs, 1, 4, ST_NT_SC1, 2, 4, srcs_sep(), "copy, system-coherent loads");
         }
         return 0;
     }
