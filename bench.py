@@ -20,6 +20,7 @@ by rank 0 before any rank's PE joins the job (the other ranks wait in the
 bootstrap), at every N.
 """
 import argparse
+import contextlib
 import json
 import os
 import sys
@@ -27,6 +28,7 @@ import time
 
 import numpy as np
 
+T_START = time.perf_counter()
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "osss-gasnet_amd"))
 sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -237,6 +239,88 @@ def persistent_child(rank, world, calls):
     return leg
 
 
+def host_staged_leg(shm, loop, S, me, npes, k, check):
+    """north_star's second rate: the symmetric-heap buffers in HOST memory, as
+    the reference's heap is (symmem.c:212-236, comms-inline.h:797-807):
+    shmem_malloc's page-locked arrays, K blocking calls that each stage the
+    source in over PCIe, reduce and stage the result out (the library's
+    chunked copy-in / reduce / copy-out pipeline on two streams, or the fused
+    kernel's in-kernel staging for small messages). Beside it, the same run's
+    PCIe ceiling: hipMemcpyAsync of S bytes H2D alone, D2H alone, and both at
+    once on two streams; a staged call moves S each way, so its ceiling is the
+    two-way rate and pcie_frac = (S / t) / both_GB_s_each_direction. The result
+    is checked bit-exact against the oracle on a sample."""
+    import ctypes
+    L, vp = shm.lib, ctypes.c_void_p
+    n = S // 8
+    hsrc, hdst = shm.malloc(S), shm.malloc(S)
+    if not hsrc or not hdst:
+        raise RuntimeError("shmem_malloc of 2 x %d bytes failed" % S)
+    x = synth(me, np.arange(n, dtype=np.uint64))
+    ctypes.memmove(hsrc, x.ctypes.data, S)
+    del x
+    loop(hdst, hsrc, n, 0, 0, npes, None, shm._psync_ptr, 2)
+    shm.barrier_all()
+    shm.sync()
+    t0 = time.perf_counter()
+    loop(hdst, hsrc, n, 0, 0, npes, None, shm._psync_ptr, k)
+    shm.sync()
+    t = (time.perf_counter() - t0) / k
+    info = shm.last_call_info()
+    ck = "skipped"
+    if check:
+        import oracle
+        idx = np.unique(np.random.default_rng(300 + me).integers(0, n, 1 << 16)).astype(np.uint64)
+        got = np.ctypeslib.as_array(ctypes.cast(hdst, ctypes.POINTER(ctypes.c_double)), shape=(n,))[idx.astype(np.int64)]
+        want = oracle.reduce_pe("sum", "double", [synth(p, idx) for p in range(npes)], me)
+        bad = int((got.view(np.uint64) != want.view(np.uint64)).sum())
+        ck = "bit-exact vs the reference's per-PE order, %d samples" % len(idx) if bad == 0 else \
+            "MISMATCH %d of %d samples" % (bad, len(idx))
+    # the PCIe ceiling, same run, same page-locked arrays
+    L.hipMemcpyAsync.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
+    L.hipStreamSynchronize.argtypes = [vp]
+    L.hipStreamCreate.argtypes = [ctypes.POINTER(vp)]
+    L.hipStreamDestroy.argtypes = [vp]
+    dev = [vp(), vp()]
+    st = [vp(), vp()]
+    for d in dev:
+        if L.hipMalloc(ctypes.byref(d), ctypes.c_size_t(S)) != 0:
+            raise RuntimeError("hipMalloc failed")
+    for s in st:
+        L.hipStreamCreate(ctypes.byref(s))
+    h2d = lambda: L.hipMemcpyAsync(dev[0], vp(hsrc), S, 1, st[0])  # noqa: E731
+    d2h = lambda: L.hipMemcpyAsync(vp(hdst), dev[1], S, 2, st[1])  # noqa: E731
+
+    def rate(fns, reps=5):
+        for f in fns:
+            f()
+        for s in st:
+            L.hipStreamSynchronize(s)
+        tq = time.perf_counter()
+        for _ in range(reps):
+            for f in fns:
+                f()
+        for s in st:
+            L.hipStreamSynchronize(s)
+        return S * reps / (time.perf_counter() - tq) / 1e9
+
+    pcie = {"h2d_GB_s": round(rate([h2d]), 1), "d2h_GB_s": round(rate([d2h]), 1),
+            "both_GB_s_each_direction": round(rate([h2d, d2h]), 1)}
+    for s in st:
+        L.hipStreamDestroy(s)
+    for d in dev:
+        L.hipFree(d)
+    shm.free(hdst)
+    shm.free(hsrc)
+    gbs = S / t / 1e9
+    return {"bytes_per_pe": S, "calls": k, "ms_per_call": round(t * 1e3, 3), "value": round(npes * S / t / GIB, 2),
+            "unit": "GiB/s", "GB_s_per_pe": round(gbs, 1), "schedule": info["schedule"], "pcie": pcie,
+            "pcie_frac": round(gbs / pcie["both_GB_s_each_direction"], 4), "check": ck,
+            "note": "source and target in shmem_malloc's page-locked host arrays (the reference's heap is host "
+                    "memory): each call stages S in over PCIe, reduces and stages S out; the headline value is "
+                    "device-resident. pcie_frac = per-PE S / t against the same run's two-way hipMemcpyAsync rate"}
+
+
 # ---------------------------------------------------------------------------
 # kernel legs (N = 1): the fold kernels themselves, timed on one GPU
 # ---------------------------------------------------------------------------
@@ -376,7 +460,28 @@ def main():
     ap.add_argument("--host", action="store_true",
                     help="source/target in host memory (shmem_malloc, page-locked): the rate includes the "
                          "H2D/D2H staging copies (DESIGN.md); not the headline metric")
+    ap.add_argument("--no-host-staged", action="store_true",
+                    help="N = 1: skip the host_staged leg (the same call on page-locked host arrays, with the "
+                         "same run's PCIe ceiling)")
     args = ap.parse_args()
+
+    # wall time of every leg (legs_s in the line), and optional legs that fail
+    # become an {"error": ...} entry instead of ending the headline line
+    legs_s, leg_errors = {}, {}
+
+    @contextlib.contextmanager
+    def timed_leg(name, optional=True):
+        t0 = time.perf_counter()
+        try:
+            yield
+        except Exception as e:  # noqa: BLE001 -- reported in the line
+            if not optional:
+                raise
+            import traceback
+            traceback.print_exc(file=sys.stderr)
+            leg_errors[name] = f"{type(e).__name__}: {e}"
+        finally:
+            legs_s[name] = round(legs_s.get(name, 0.0) + time.perf_counter() - t0, 2)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -389,18 +494,23 @@ def main():
     # (every rank at once, before any of them touches the GPU)
     small_p_child = None
     if world > 1 and not args.no_small and not args.host:
-        small_p_child = persistent_child(rank, world, 4096)
+        with timed_leg("small_call_persistent"):
+            small_p_child = persistent_child(rank, world, 4096)
     # CPU baseline, before this process initialises the GPU; at N > 1 the
     # other ranks wait for rank 0 in the bootstrap (SHMEM_BARRIER_TIMEOUT)
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(S, args.gpus, args.cpu_seconds)
+        with timed_leg("cpu_baseline"):
+            cpu = cpu_baseline(S, args.gpus, args.cpu_seconds)
     # the fused kernel on 2 PE processes sharing this GPU (children; this
     # process has not touched the GPU yet)
     fused = fused_p = None
     if world == 1 and not args.no_fused and not args.host:
-        fused = fused_same_gpu(2, 4096 if args.no_small is False else 512)
-        fused_p = fused_same_gpu(2, 4096 if args.no_small is False else 512, persistent=True)
+        with timed_leg("fused_same_gpu"):
+            fused = fused_same_gpu(2, 4096 if args.no_small is False else 512)
+        with timed_leg("fused_same_gpu_persistent"):
+            fused_p = fused_same_gpu(2, 4096 if args.no_small is False else 512, persistent=True)
+    t_init0 = time.perf_counter()
 
     os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(2 * S + (64 << 20)))
     os.environ.setdefault("SHMEM_DEVICE_SCRATCH_SIZE", str(96 << 20))
@@ -413,6 +523,8 @@ def main():
     os.environ.setdefault("SHMEM_BOOTSTRAP_TIMEOUT", "600")
     shm = shmem_reduce.Shmem()
     shm.init()
+    legs_s["init"] = round(time.perf_counter() - t_init0, 2)
+    t_head0 = time.perf_counter()
     # the init self-test found peer heap reads broken: the library runs the
     # RCCL pairs through RCCL whatever is selected
     rccl_fallback = shm.n_pes() > 1 and shm.lib.shmemx_get_reduce_algorithm() == shmem_reduce.ALGORITHMS["rccl"] \
@@ -426,8 +538,16 @@ def main():
     if npes > 1:
         ran, passed, stale = shm.coherence_selftest()
         sysload, no_acq = shm.coherence_sysload()
+        prod_ran, prod = shm.coherence_producer()
         coherence = {"ran": ran, "passed": passed, "stale_without_acquire": stale,
                      "sysload_fresh": sysload, "fused_acquires_skipped": no_acq,
+                     "producer_path": dict(prod, ran=prod_ran,
+                                           note="32 words written with plain stores by a kernel on the null stream "
+                                                "(a caller's producer), re-read by every peer after caching the old "
+                                                "values: fused_* after the fused kernel's same-stream flag + device "
+                                                "wait, host_* after the signal kernel + host wait + host barrier; "
+                                                "plain loads without an acquire, 16-byte system-coherent loads, "
+                                                "plain loads after a system-scope acquire"),
                      "note": "every PE read each peer's marker through its L2, the peer rewrote it (write-through), "
                              "and the re-read after mi355_acquire_system must see the new value; "
                              "stale_without_acquire: a re-read without the acquire returned the old value; "
@@ -478,84 +598,89 @@ def main():
     shm.kernel_timing(False)
     # what the library ran for these calls: schedule, dominant kernel, bytes
     info = shm.last_call_info()
+    legs_s["headline"] = round(time.perf_counter() - t_head0, 2)
 
     # the many-small-bucket regime (BASELINE config 5 shape: 64 KiB per call)
     small_n, small_calls = 8192, 0 if args.no_small else 4096   # BASELINE config 5: 4096 x 64 KiB
     t_small = None
-    if small_calls:
-        steps(20, small_n)
-        shm.barrier_all()
-        shm.sync()
-        ts0 = time.perf_counter()
-        steps(small_calls, small_n)
-        shm.sync()
-        t_small = (time.perf_counter() - ts0) / small_calls
-        small_info = shm.last_call_info()
-        shm.barrier_all()
+    with timed_leg("small_call"):
+        if small_calls:
+            steps(20, small_n)
+            shm.barrier_all()
+            shm.sync()
+            ts0 = time.perf_counter()
+            steps(small_calls, small_n)
+            shm.sync()
+            t_small = (time.perf_counter() - ts0) / small_calls
+            small_info = shm.last_call_info()
+            shm.barrier_all()
 
     # N = 1: the same calls with the opt-in persistent server (shmemx.h
     # shmemx_set_persistent): the identity copy served by a resident one-member
     # fused kernel, no launch per call. Not at N > 1 (kept out of the driver's
     # multi-GPU line; the same-GPU multi-PE figures are in fused_same_gpu_persistent).
-    t_small_p = None
-    if small_calls and npes == 1 and not args.host:
-        shm.set_persistent(True)
-        served0, launched0 = shm.persistent_stats()
-        steps(20, small_n)
-        shm.barrier_all()
-        ts0 = time.perf_counter()
-        steps(small_calls, small_n)
-        t_small_p = (time.perf_counter() - ts0) / small_calls
-        served1, launched1 = shm.persistent_stats()
-        shm.set_persistent(False)  # stops the server
-        shm.sync()
-        shm.barrier_all()
+    with timed_leg("small_call_persistent"):
+        t_small_p = None
+        if small_calls and npes == 1 and not args.host:
+            shm.set_persistent(True)
+            served0, launched0 = shm.persistent_stats()
+            steps(20, small_n)
+            shm.barrier_all()
+            ts0 = time.perf_counter()
+            steps(small_calls, small_n)
+            t_small_p = (time.perf_counter() - ts0) / small_calls
+            served1, launched1 = shm.persistent_stats()
+            shm.set_persistent(False)  # stops the server
+            shm.sync()
+            shm.barrier_all()
 
     # The same 64 KiB calls through the stream-ordered API (shmemx.h), 64 of
     # them captured once into a HIP graph and the graph replayed: how a caller
     # that batches small buckets into a graph (e.g. torch.cuda.graph) sees
     # them; the graph launch and its wait amortised over its 64 calls.
-    small_graph = None
-    if small_calls and not args.host and not rccl_fallback:
-        per_graph, replays = 64, max(1, small_calls // 64)
-        st = shm.stream_create()
-        gsrc, gdst = shm.malloc_device(small_n * 8), shm.malloc_device(small_n * 8)
-        shm.put(gsrc, synth(me, np.arange(small_n, dtype=np.uint64)))
-        shm.to_all_on_stream("sum", "double", gdst, gsrc, small_n, 0, 0, npes, st)
-        shm.stream_sync(st)
-        shm.capture_begin(st)
-        for _ in range(per_graph):
+    with timed_leg("small_call_graph"):
+        small_graph = None
+        if small_calls and not args.host and not rccl_fallback:
+            per_graph, replays = 64, max(1, small_calls // 64)
+            st = shm.stream_create()
+            gsrc, gdst = shm.malloc_device(small_n * 8), shm.malloc_device(small_n * 8)
+            shm.put(gsrc, synth(me, np.arange(small_n, dtype=np.uint64)))
             shm.to_all_on_stream("sum", "double", gdst, gsrc, small_n, 0, 0, npes, st)
-        graph, exe = shm.capture_end(st)
-        shm.graph_launch(exe, st)
-        shm.stream_sync(st)
-        shm.barrier_all()
-        tg0 = time.perf_counter()
-        for _ in range(replays):
+            shm.stream_sync(st)
+            shm.capture_begin(st)
+            for _ in range(per_graph):
+                shm.to_all_on_stream("sum", "double", gdst, gsrc, small_n, 0, 0, npes, st)
+            graph, exe = shm.capture_end(st)
             shm.graph_launch(exe, st)
             shm.stream_sync(st)
-        t_graph_local = (time.perf_counter() - tg0) / (replays * per_graph)
-        gsched = shm.last_call_info()["schedule"]
-        ck = "skipped"
-        if not args.no_check:
-            import oracle
-            idx = np.arange(small_n, dtype=np.uint64)
-            got = shm.get(gdst, small_n, "double")
-            want = oracle.reduce_pe("sum", "double", [synth(p, idx) for p in range(npes)], me)
-            ck = (got.view(np.uint64) != want.view(np.uint64)).sum()
-        shm.graph_destroy(graph, exe)
-        shm.stream_destroy(st)
-        shm.barrier_all()
-        shm.free_device(gdst)
-        shm.free_device(gsrc)
-        small_graph = {"bytes_per_pe": small_n * 8, "calls": replays * per_graph, "calls_per_graph": per_graph,
-                       "t_local": t_graph_local, "schedule": gsched, "bad": ck,
-                       "note": "the 64 KiB calls as shmemx_double_sum_to_all_on_stream, 64 per HIP graph, the graph "
-                               "replayed and waited for: per-call time including the graph launch and wait"}
+            shm.barrier_all()
+            tg0 = time.perf_counter()
+            for _ in range(replays):
+                shm.graph_launch(exe, st)
+                shm.stream_sync(st)
+            t_graph_local = (time.perf_counter() - tg0) / (replays * per_graph)
+            gsched = shm.last_call_info()["schedule"]
+            ck = "skipped"
+            if not args.no_check:
+                import oracle
+                idx = np.arange(small_n, dtype=np.uint64)
+                got = shm.get(gdst, small_n, "double")
+                want = oracle.reduce_pe("sum", "double", [synth(p, idx) for p in range(npes)], me)
+                ck = (got.view(np.uint64) != want.view(np.uint64)).sum()
+            shm.graph_destroy(graph, exe)
+            shm.stream_destroy(st)
+            shm.barrier_all()
+            shm.free_device(gdst)
+            shm.free_device(gsrc)
+            small_graph = {"bytes_per_pe": small_n * 8, "calls": replays * per_graph, "calls_per_graph": per_graph,
+                           "t_local": t_graph_local, "schedule": gsched, "bad": ck,
+                           "note": "the 64 KiB calls as shmemx_double_sum_to_all_on_stream, 64 per HIP graph, the graph "
+                                   "replayed and waited for: per-call time including the graph launch and wait"}
 
     # N > 1: the same K calls through RCCL (ncclAllReduce on the whole job,
     # SHMEM_REDUCE_ALGORITHM=rccl) for comparison with the P2P schedule; the
     # headline value stays the default schedule's
+    t_rccl0 = time.perf_counter()
     t_rccl_local = None
     distinct_gpus = shared_gpu = False
     pes_on_gpu = 1   # PEs on this PE's GPU, itself included (test layouts share one)
@@ -610,6 +735,14 @@ def main():
     sys.stdout.flush()
     os.dup2(saved_stdout, 1)
     os.close(saved_stdout)
+    legs_s["rccl_compare"] = round(time.perf_counter() - t_rccl0, 2)
+    # an optional leg that failed reports {"error": ...} (below), not a partial record
+    if "small_call" in leg_errors:
+        t_small = None
+    if "small_call_persistent" in leg_errors:
+        t_small_p = None
+    if "small_call_graph" in leg_errors:
+        small_graph = None
 
     # max over PEs, through the library's own host-staged double max reduction
     def max_over_pes(x):
@@ -618,6 +751,7 @@ def main():
         shm.to_all("max", "double", tout.ctypes.data, tbuf.ctypes.data, 1, 0, 0, npes)
         return float(tout[0])
 
+    t_check0 = time.perf_counter()
     t_step = max_over_pes(t_local) / args.steps
     if small_graph is not None:
         t_sg = max_over_pes(small_graph.pop("t_local"))
@@ -668,97 +802,109 @@ def main():
             check = "bit-exact vs the reference's per-PE order on every PE, %d samples each" % len(idx) if bad == 0 \
                 else "MISMATCH %d of %d samples (worst PE)" % (bad, len(idx))
         del got_full
+    legs_s["check"] = round(time.perf_counter() - t_check0, 2)
 
-    kernels = None
-    if npes == 1 and not args.no_kernels and not args.host:
-        kernels = kernel_legs(shm, args.kernel_reps, not args.no_check)
-        for name, leg in kernels.items():
-            if isinstance(leg, dict):
-                leg["traffic_note"] = traffic_for(leg, f"kernel_{name}", False)
-                if leg.get("traffic"):
-                    leg["traffic_over_alg"] = round(leg["traffic"] / leg["alg_bytes_per_launch"], 4)
+    # N = 1: north_star's host-memory rate -- the same call on shmem_malloc's
+    # page-locked host arrays, staged over PCIe inside each call, with the
+    # same run's PCIe ceiling (host_staged_leg)
+    host_staged = None
+    if npes == 1 and not args.host and not args.no_host_staged:
+        with timed_leg("host_staged"):
+            host_staged = host_staged_leg(shm, loop, S, me, npes, max(10, args.steps), not args.no_check)
+
+    with timed_leg("kernels"):
+        kernels = None
+        if npes == 1 and not args.no_kernels and not args.host:
+            kernels = kernel_legs(shm, args.kernel_reps, not args.no_check)
+            for name, leg in kernels.items():
+                if isinstance(leg, dict):
+                    leg["traffic_note"] = traffic_for(leg, f"kernel_{name}", False)
+                    if leg.get("traffic"):
+                        leg["traffic_over_alg"] = round(leg["traffic"] / leg["alg_bytes_per_launch"], 4)
 
     # BASELINE config 4 (op coverage): shmem_float_max_to_all and
     # shmem_longlong_and_to_all on 64 MiB per PE, timed like the headline
     # (C loop, max over PEs) and checked bit-exact on a sample
-    ops = None
-    if not args.no_ops and not args.host:
-        import oracle
-        ops = {}
-        ob = min(64 << 20, S)
-        for name, op, dtype, es, gen in (
-                ("float_max", "max", "float", 4, lambda pe, i: synth(pe, i).astype(np.float32)),
-                ("longlong_and", "and", "longlong", 8, synth_bits)):
-            if rccl_fallback and op == "and":
-                ops[name] = {"skipped": "RCCL fallback (peer heap reads failed the init self-test): no bitwise and"}
-                continue
-            no = ob // es
-            shm.put(src, gen(me, np.arange(no, dtype=np.uint64)))
-            oloop = shmem_reduce.bench_loop(name=name)
-            k = max(10, args.steps // 4)
-            oloop(dst, src, no, 0, 0, npes, None, shm._psync_ptr, 3)
-            shm.barrier_all()
-            shm.sync()
-            to0 = time.perf_counter()
-            oloop(dst, src, no, 0, 0, npes, None, shm._psync_ptr, k)
-            shm.sync()
-            t_op = max_over_pes(time.perf_counter() - to0) / k
-            shm.barrier_all()
-            ck = "skipped"
-            if not args.no_check:
-                idx = np.unique(np.random.default_rng(100 + me).integers(0, no, 1 << 14)).astype(np.uint64)
-                got = shm.get(dst, no, dtype)[idx.astype(np.int64)]
-                want = oracle.reduce_pe(op, dtype, [gen(p, idx) for p in range(npes)], me)
-                bad = int(max_over_pes(int((got.view(np.uint8) != want.view(np.uint8)).sum())))
-                ck = "bit-exact, %d samples" % len(idx) if bad == 0 else "MISMATCH in %d bytes" % bad
-            ops[name] = {"bytes_per_pe": ob, "steps": k, "us_per_call": round(t_op * 1e6, 2),
-                         "value": round(npes * ob / t_op / GIB, 2), "per_pe_gib_s": round(ob / t_op / GIB, 2),
-                         "check": ck}
-        ops["note"] = ("BASELINE config 4 (op coverage): shmem_float_max_to_all and shmem_longlong_and_to_all, "
-                       "64 MiB per PE, GiB/s reduced whole job; longlong words with bits 1 at p = 7/8")
+    with timed_leg("op_coverage"):
+        ops = None
+        if not args.no_ops and not args.host:
+            import oracle
+            ops = {}
+            ob = min(64 << 20, S)
+            for name, op, dtype, es, gen in (
+                    ("float_max", "max", "float", 4, lambda pe, i: synth(pe, i).astype(np.float32)),
+                    ("longlong_and", "and", "longlong", 8, synth_bits)):
+                if rccl_fallback and op == "and":
+                    ops[name] = {"skipped": "RCCL fallback (peer heap reads failed the init self-test): no bitwise and"}
+                    continue
+                no = ob // es
+                shm.put(src, gen(me, np.arange(no, dtype=np.uint64)))
+                oloop = shmem_reduce.bench_loop(name=name)
+                k = max(10, args.steps // 4)
+                oloop(dst, src, no, 0, 0, npes, None, shm._psync_ptr, 3)
+                shm.barrier_all()
+                shm.sync()
+                to0 = time.perf_counter()
+                oloop(dst, src, no, 0, 0, npes, None, shm._psync_ptr, k)
+                shm.sync()
+                t_op = max_over_pes(time.perf_counter() - to0) / k
+                shm.barrier_all()
+                ck = "skipped"
+                if not args.no_check:
+                    idx = np.unique(np.random.default_rng(100 + me).integers(0, no, 1 << 14)).astype(np.uint64)
+                    got = shm.get(dst, no, dtype)[idx.astype(np.int64)]
+                    want = oracle.reduce_pe(op, dtype, [gen(p, idx) for p in range(npes)], me)
+                    bad = int(max_over_pes(int((got.view(np.uint8) != want.view(np.uint8)).sum())))
+                    ck = "bit-exact, %d samples" % len(idx) if bad == 0 else "MISMATCH in %d bytes" % bad
+                ops[name] = {"bytes_per_pe": ob, "steps": k, "us_per_call": round(t_op * 1e6, 2),
+                             "value": round(npes * ob / t_op / GIB, 2), "per_pe_gib_s": round(ob / t_op / GIB, 2),
+                             "check": ck}
+            ops["note"] = ("BASELINE config 4 (op coverage): shmem_float_max_to_all and shmem_longlong_and_to_all, "
+                           "64 MiB per PE, GiB/s reduced whole job; longlong words with bits 1 at p = 7/8")
 
     # N > 1: the same call on plain hipMalloc buffers (a framework's tensors,
     # outside the symmetric heap): the members map each other's allocations
     # for the call (csrc/extmap.c) instead of staging them through scratch
-    external = None
-    if npes > 1 and not args.host and not args.no_external and not rccl_fallback:
-        import ctypes
-        hip = ctypes.CDLL("libamdhip64.so")
-        bufs = [ctypes.c_void_p(), ctypes.c_void_p()]
-        if all(hip.hipMalloc(ctypes.byref(b), ctypes.c_size_t(S)) == 0 for b in bufs):
-            esrc, edst = bufs[0].value, bufs[1].value
-            shm.put(esrc, synth(me, np.arange(n, dtype=np.uint64)))  # the op-coverage leg rewrote src
-            k = max(5, args.steps // 4)
-            loop(edst, esrc, n, 0, 0, npes, None, shm._psync_ptr, 3)
-            shm.barrier_all()
-            shm.sync()
-            te0 = time.perf_counter()
-            loop(edst, esrc, n, 0, 0, npes, None, shm._psync_ptr, k)
-            shm.sync()
-            t_ext_local = time.perf_counter() - te0
-            einfo = shm.last_call_info()   # before max_over_pes: its own call replaces it
-            t_ext = max_over_pes(t_ext_local) / k
-            ck = "skipped"
-            if not args.no_check:
-                import oracle
-                idx = np.unique(np.random.default_rng(50 + me).integers(0, n, 1 << 14)).astype(np.uint64)
-                got = shm.get(edst, n, "double")[idx.astype(np.int64)]
-                want = oracle.reduce_pe("sum", "double", [synth(p, idx) for p in range(npes)], me)
-                bad = int(max_over_pes(int((got.view(np.uint64) != want.view(np.uint64)).sum())))
-                ck = "bit-exact, %d samples" % len(idx) if bad == 0 else "MISMATCH %d samples" % bad
-            shm.barrier_all()
-            mapped, opened, closed = shm.external_map_stats()
-            external = {"bytes_per_pe": S, "steps": k, "us_per_call": round(t_ext * 1e6, 2),
-                        "value": round(npes * S / t_ext / GIB, 2), "over_heap_buffers": round(t_ext / t_step, 3),
-                        "schedule": einfo["schedule"], "mappings_opened": opened, "check": ck,
-                        "note": "the headline call on plain hipMalloc buffers (outside the symmetric heap): "
-                                "the members map each other's allocations for the call (IPC, cached) instead "
-                                "of staging them through scratch (SHMEM_EXTERNAL_MAP)"}
-        else:
-            external = {"error": "hipMalloc of the two buffers failed"}
-        for b in bufs:
-            if b.value:
-                hip.hipFree(b)
+    with timed_leg("external_buffers"):
+        external = None
+        if npes > 1 and not args.host and not args.no_external and not rccl_fallback:
+            import ctypes
+            hip = ctypes.CDLL("libamdhip64.so")
+            bufs = [ctypes.c_void_p(), ctypes.c_void_p()]
+            if all(hip.hipMalloc(ctypes.byref(b), ctypes.c_size_t(S)) == 0 for b in bufs):
+                esrc, edst = bufs[0].value, bufs[1].value
+                shm.put(esrc, synth(me, np.arange(n, dtype=np.uint64)))  # the op-coverage leg rewrote src
+                k = max(5, args.steps // 4)
+                loop(edst, esrc, n, 0, 0, npes, None, shm._psync_ptr, 3)
+                shm.barrier_all()
+                shm.sync()
+                te0 = time.perf_counter()
+                loop(edst, esrc, n, 0, 0, npes, None, shm._psync_ptr, k)
+                shm.sync()
+                t_ext_local = time.perf_counter() - te0
+                einfo = shm.last_call_info()   # before max_over_pes: its own call replaces it
+                t_ext = max_over_pes(t_ext_local) / k
+                ck = "skipped"
+                if not args.no_check:
+                    import oracle
+                    idx = np.unique(np.random.default_rng(50 + me).integers(0, n, 1 << 14)).astype(np.uint64)
+                    got = shm.get(edst, n, "double")[idx.astype(np.int64)]
+                    want = oracle.reduce_pe("sum", "double", [synth(p, idx) for p in range(npes)], me)
+                    bad = int(max_over_pes(int((got.view(np.uint64) != want.view(np.uint64)).sum())))
+                    ck = "bit-exact, %d samples" % len(idx) if bad == 0 else "MISMATCH %d samples" % bad
+                shm.barrier_all()
+                mapped, opened, closed = shm.external_map_stats()
+                external = {"bytes_per_pe": S, "steps": k, "us_per_call": round(t_ext * 1e6, 2),
+                            "value": round(npes * S / t_ext / GIB, 2), "over_heap_buffers": round(t_ext / t_step, 3),
+                            "schedule": einfo["schedule"], "mappings_opened": opened, "check": ck,
+                            "note": "the headline call on plain hipMalloc buffers (outside the symmetric heap): "
+                                    "the members map each other's allocations for the call (IPC, cached) instead "
+                                    "of staging them through scratch (SHMEM_EXTERNAL_MAP)"}
+            else:
+                external = {"error": "hipMalloc of the two buffers failed"}
+            for b in bufs:
+                if b.value:
+                    hip.hipFree(b)
 
     # N > 1: what one link carries alone -- PE 0 pulls 64 MiB from each peer's
     # heap with shmem_getmem (the copy kernel reading the peer mapping, as the
@@ -766,46 +912,47 @@ def main():
     # P2P copy), one peer at a time, the others waiting in a barrier. Beside
     # xgmi.ag_kernel_remote_read_GB_s (all peers at once) it says whether the
     # schedule is bound by the links or by how it drives them.
-    link_probe = None
-    if npes > 1 and not args.host and not args.no_link_probe:
-        import ctypes
-        # two 16 MiB buffers fit the heap's 64 MiB beside the headline's
-        nbp, reps = min(S, 16 << 20), 10
-        psym, ploc = shm.malloc_device(nbp), shm.malloc_device(nbp)
-        if not psym or not ploc:
-            raise SystemExit("link probe: shmemx_malloc_device of 2 x %d bytes failed" % nbp)
-        shm.put(psym, synth(me, np.arange(nbp // 8, dtype=np.uint64)))
-        shm.barrier_all()
-        get, put = shm.lib.shmem_getmem, shm.lib.shmem_putmem
-        for f in (get, put):
-            f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-            f.restype = None
-        peers = {}
-        if me == 0:
-            for q in range(1, npes):
-                rec = {}
-                for name, f, a, b in (("get_GB_s", get, ploc, psym), ("put_GB_s", put, psym, ploc)):
-                    f(a, b, nbp, q)
-                    tq0 = time.perf_counter()
-                    for _ in range(reps):
+    with timed_leg("link_probe"):
+        link_probe = None
+        if npes > 1 and not args.host and not args.no_link_probe:
+            import ctypes
+            # two 16 MiB buffers fit the heap's 64 MiB beside the headline's
+            nbp, reps = min(S, 16 << 20), 10
+            psym, ploc = shm.malloc_device(nbp), shm.malloc_device(nbp)
+            if not psym or not ploc:
+                raise SystemExit("link probe: shmemx_malloc_device of 2 x %d bytes failed" % nbp)
+            shm.put(psym, synth(me, np.arange(nbp // 8, dtype=np.uint64)))
+            shm.barrier_all()
+            get, put = shm.lib.shmem_getmem, shm.lib.shmem_putmem
+            for f in (get, put):
+                f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+                f.restype = None
+            peers = {}
+            if me == 0:
+                for q in range(1, npes):
+                    rec = {}
+                    for name, f, a, b in (("get_GB_s", get, ploc, psym), ("put_GB_s", put, psym, ploc)):
                         f(a, b, nbp, q)
-                    shm.sync()
-                    rec[name] = round(nbp * reps / (time.perf_counter() - tq0) / 1e9, 1)
-                peers[str(q)] = rec
-            ok = True
-            if not args.no_check:   # the last get brought PE npes-1's bytes
-                got = shm.get(ploc, 1 << 16, "double").view(np.uint64)
-                ok = bool((got == synth(npes - 1, np.arange(1 << 16, dtype=np.uint64)).view(np.uint64)).all())
-        shm.barrier_all()
-        shm.free_device(ploc)
-        shm.free_device(psym)
-        if me == 0:
-            link_probe = {"bytes": nbp, "reps": reps, "from_pe0": peers,
-                          "check": "skipped" if args.no_check else "bit-exact" if ok else "MISMATCH",
-                          "note": "PE 0 alone, one peer at a time: shmem_getmem (copy kernel pulling over the "
-                                  "peer mapping) and shmem_putmem (HIP P2P copy) of 16 MiB, blocking calls"
-                                  + ("; the PEs share ONE GPU here: local HBM copies, not link rates"
-                                     if shared_gpu else "")}
+                        tq0 = time.perf_counter()
+                        for _ in range(reps):
+                            f(a, b, nbp, q)
+                        shm.sync()
+                        rec[name] = round(nbp * reps / (time.perf_counter() - tq0) / 1e9, 1)
+                    peers[str(q)] = rec
+                ok = True
+                if not args.no_check:   # the last get brought PE npes-1's bytes
+                    got = shm.get(ploc, 1 << 16, "double").view(np.uint64)
+                    ok = bool((got == synth(npes - 1, np.arange(1 << 16, dtype=np.uint64)).view(np.uint64)).all())
+            shm.barrier_all()
+            shm.free_device(ploc)
+            shm.free_device(psym)
+            if me == 0:
+                link_probe = {"bytes": nbp, "reps": reps, "from_pe0": peers,
+                              "check": "skipped" if args.no_check else "bit-exact" if ok else "MISMATCH",
+                              "note": "PE 0 alone, one peer at a time: shmem_getmem (copy kernel pulling over the "
+                                      "peer mapping) and shmem_putmem (HIP P2P copy) of 16 MiB, blocking calls"
+                                      + ("; the PEs share ONE GPU here: local HBM copies, not link rates"
+                                         if shared_gpu else "")}
 
     # dominant kernel and its algorithmic bytes per launch, from the schedule
     # the library reports for the timed calls (shmemx_last_call_info)
@@ -945,7 +1092,12 @@ def main():
             "kernels": kernels,
             "fused_same_gpu": fused,
             "fused_same_gpu_persistent": fused_p,
+            "host_staged": host_staged,
         }
+        for name, err in leg_errors.items():   # optional legs that raised
+            out[name] = {"error": err}
+        legs_s["total_before_print"] = round(time.perf_counter() - T_START, 2)
+        out["legs_s"] = legs_s
         print(json.dumps(out), flush=True)
     if args.host:
         shm.free(dst)

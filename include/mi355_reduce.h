@@ -143,7 +143,8 @@ int mi355_convert_short (int widen, const void *src, void *dst, size_t n, void *
 #define MI355_SIG_CHANNEL_WORDS 4176
 #define MI355_SIG_CHANNELS 2
 #define MI355_SIG_SELFTEST (MI355_SIG_CHANNELS * MI355_SIG_CHANNEL_WORDS) /* [PE]: init-time check */
-#define MI355_SIG_WORDS (MI355_SIG_SELFTEST + 1024)
+#define MI355_SIG_SELFTEST2 (MI355_SIG_SELFTEST + 1024) /* [PE]: init-time producer-path check */
+#define MI355_SIG_WORDS (MI355_SIG_SELFTEST2 + 1024)
 
 typedef struct MI355FusedArgs {
     int op, dtype;
@@ -295,6 +296,22 @@ int mi355_peek_cached (const unsigned long long *const *src, int n, unsigned lon
  * no fence: out[b * n + i]. */
 int mi355_peek_sysload (const unsigned long long *const *src, int n, unsigned long long *out, int nblocks,
                         void *stream);
+
+/* The init-time check of the CALLER's producer path (runtime.c producer_test):
+ * mi355_mark_plain is a caller's kernel writing its source -- `words` blocks
+ * (dealt over the XCDs), block b storing value + b into dst[b] with a plain
+ * write-back store; words <= 1024. mi355_producer_read, nblocks blocks
+ * (<= 256): when flag != NULL wave 0 first waits until flag[q] == token for
+ * every q < np (bounded by timeout_ticks of s_memrealtime; a timeout sets
+ * out[3 * nblocks * np * words] = 1), then every block reads the np x words
+ * words of src[q] three ways into out: plain loads (third 0), 16-byte
+ * system-coherent loads as the fused kernel's folds (third 1), plain loads
+ * after a system-scope acquire (third 2); each third is [nblocks][np * words].
+ * np <= 64, words even (16-byte aligned pairs). */
+int mi355_mark_plain (unsigned long long *dst, int words, unsigned long long value, void *stream);
+int mi355_producer_read (const unsigned long long *const *src, int np, int words, const unsigned long long *flag,
+                         unsigned long long token, unsigned long long timeout_ticks, unsigned long long *out,
+                         int nblocks, void *stream);
 
 /* Shard i of nshards for n elements of elem_size bytes: the P2P schedule's
  * partition (contiguous, shard starts 256-byte aligned, trailing shards may

@@ -183,6 +183,18 @@ void shmemx_coherence_selftest (int *ran, int *passed, int *stale_without_acquir
  * fused kernel therefore runs without its per-block system-scope acquires
  * (SHMEM_FUSED_ACQUIRE=1 keeps them). */
 void shmemx_coherence_sysload (int *sysload_fresh, int *acquires_skipped);
+/* The init test of the CALLER's producer path (round 4): every PE wrote 32
+ * words with plain stores from a kernel on the null stream, as a caller
+ * writes its source, and every peer re-read them (after caching the old
+ * values) in the fused kernel's ordering (same-stream flag, device wait) and
+ * in the multi-launch schedules' (signal kernel, host wait, host barrier).
+ * fresh[6] (1 = every block of every PE saw every new word), in order:
+ * fused ordering plain loads / 16-byte system-coherent loads / plain loads
+ * after a system-scope acquire, then the same three after the host-wait
+ * ordering. The fused kernel skips its acquires only when fresh[1] (and
+ * sysload_fresh) hold; it is not used when neither fresh[1] nor fresh[2];
+ * the job runs RCCL when fresh[5] fails. ran = 0 above 64 PEs. */
+void shmemx_coherence_producer (int *ran, int *fresh);
 
 /* Bring up the RCCL communicator of the whole job (what SHMEM_REDUCE_ALGORITHM=rccl uses) without
  * aborting when RCCL cannot come up within timeout_s seconds: 0 = ready on this PE, -1 = not. Every PE

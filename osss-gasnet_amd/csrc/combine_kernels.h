@@ -279,7 +279,13 @@ __device__ __forceinline__ void x80_orders_vector(const OrdersParams &p, uint64_
     bool have_first = false;
 #pragma unroll 1
     for (int q = 0; q < NSRC; ++q) {
-        if (!ALL && p.dst[q] == nullptr) continue;
+        // member q's output, picked with compile-time indices: p.dst[q] with
+        // the rolled loop's q made the compiler copy the kernel arguments'
+        // pointer array into scratch memory (24 bytes per lane at NSRC = 2)
+        u32x4 *dq = (u32x4 *)p.dst[0];
+#pragma unroll
+        for (int k = 1; k < NSRC; ++k) dq = q == k ? (u32x4 *)p.dst[k] : dq;
+        if (!ALL && dq == nullptr) continue;
         x80 acc = v[0];
 #pragma unroll
         for (int k = 1; k < NSRC; ++k) acc = x80d::pick(q == k, v[k], acc);
@@ -301,7 +307,7 @@ __device__ __forceinline__ void x80_orders_vector(const OrdersParams &p, uint64_
         for (int w = 0; w < 3; ++w) acc.pad[w] = own.pad[w];  // the padding of the member's own slot
         Pack<x80> o;
         o.e[0] = acc;
-        st16_fold((u32x4 *)p.dst[q] + i, o.v);
+        st16_fold(dq + i, o.v);
     }
 }
 

@@ -112,6 +112,19 @@ __device__ __forceinline__ u32x4 ld16_sys(const void *p) {
     r.w = (unsigned)(hi >> 32);
     return r;
 }
+// The folds' form of the same load: one 16-byte `buffer_load_dwordx4 ...
+// sc0 sc1` from a wave-uniform base (a member's buffer) at a per-lane byte
+// offset, through the builtin so the compiler places the waits. Round 4
+// (tools/fold_probe S, profiles/r04/fold_probe_sysload16.txt): 16-byte
+// system-coherent loads fold 2 sources in 134 us per 256 MiB against 143 us
+// for ld16_sys's two 8-byte loads (8 sources: 441 vs 459 us); non-temporal
+// loads take 116 / 381 us, so the multi-launch folds keep theirs.
+// The offset must stay below 4 GiB (the fused path is capped at 1 GiB).
+__device__ __forceinline__ u32x4 ld16_sys_at(const char *base, uint32_t off) {
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0, (int)0xFFFFFFF0u, 0x00020000);
+    return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 17);  // aux 17: sc0 | sc1
+}
 template <typename T>
 __device__ __forceinline__ T ld_elem_sys(const T *p) {
     static_assert(sizeof(T) == 2 || sizeof(T) == 4 || sizeof(T) == 8 || sizeof(T) == 16, "element size");
@@ -135,7 +148,7 @@ __device__ __forceinline__ T ld_elem_sys(const T *p) {
 }
 
 // This call's pair count with every member (lanes of wave 0, into LDS).
-__device__ void load_counts(const MI355FusedArgs &a, const unsigned long long *mine, unsigned long long *cnt) {
+__device__ __forceinline__ void load_counts(const MI355FusedArgs &a, const unsigned long long *mine, unsigned long long *cnt) {
     if (threadIdx.x < a.nmembers) cnt[threadIdx.x] = ld_sys_u64(mine + MI355_SIG_CALLS + a.pe[threadIdx.x]) + 1;
     __syncthreads();
 }
@@ -145,7 +158,7 @@ __device__ void load_counts(const MI355FusedArgs &a, const unsigned long long *m
 // acquire = false only where every later read of the members' buffers is a
 // system-coherent load (fused_body under no_acquire); fused_pull's copies
 // read with plain loads and always acquire.
-__device__ bool wait_members(const MI355FusedArgs &a, const unsigned long long *mine, const unsigned long long *cnt,
+__device__ __forceinline__ bool wait_members(const MI355FusedArgs &a, const unsigned long long *mine, const unsigned long long *cnt,
                              int base, bool include_self, bool acquire = true) {
     bool ok = true;
     if (threadIdx.x < 64) {
@@ -174,7 +187,7 @@ __device__ bool wait_members(const MI355FusedArgs &a, const unsigned long long *
 }
 
 // Count this block in on a local counter; true for the grid's last block.
-__device__ bool last_block(unsigned long long *counter) {
+__device__ __forceinline__ bool last_block(unsigned long long *counter) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     __shared__ int is_last;
@@ -187,13 +200,13 @@ __device__ bool last_block(unsigned long long *counter) {
     return is_last != 0;
 }
 
-__device__ void publish(const MI355FusedArgs &a, const unsigned long long *cnt, int base) {
+__device__ __forceinline__ void publish(const MI355FusedArgs &a, const unsigned long long *cnt, int base) {
     // lanes of wave 0: one member each (this PE included)
     if (threadIdx.x < a.nmembers) st_sys_u64(a.sig[threadIdx.x] + base + a.pe[a.me], cnt[threadIdx.x]);
 }
 
 // Advance the pair counts (the call is over on every member), then report.
-__device__ void finish(const MI355FusedArgs &a, unsigned long long *mine, const unsigned long long *cnt, bool ok,
+__device__ __forceinline__ void finish(const MI355FusedArgs &a, unsigned long long *mine, const unsigned long long *cnt, bool ok,
                        unsigned epoch) {
     if (ok && threadIdx.x < a.nmembers) st_sys_u64(mine + MI355_SIG_CALLS + a.pe[threadIdx.x], cnt[threadIdx.x]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -235,7 +248,7 @@ __device__ void block_drain(bool plain) {
     if (__syncthreads_or(plain) && threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
-__device__ void block_copy(void *dst, const void *src, uint64_t nbytes, unsigned bi, unsigned nblocks) {
+__device__ __forceinline__ void block_copy(void *dst, const void *src, uint64_t nbytes, unsigned bi, unsigned nblocks) {
     block_drain(block_copy_issue(dst, src, nbytes, bi, nblocks));
 }
 
@@ -276,7 +289,7 @@ __device__ __forceinline__ Pack<T> fold_vec(const MI355FusedArgs &a, const Call 
 #pragma unroll
         for (int j = 0; j < kBatch; ++j)
             if (k0 + j < nm)
-                x[j].v = ld16_sys((const u32x4 *)(src_of(a, c, order_member(k0 + j, first)) + lo * sizeof(T)) + v);
+                x[j].v = ld16_sys_at(src_of(a, c, order_member(k0 + j, first)) + lo * sizeof(T), (uint32_t)(v * 16));
 #pragma unroll
         for (int j = 0; j < kBatch; ++j) {
             if (k0 + j >= nm) break;
@@ -330,7 +343,7 @@ __device__ __forceinline__ void versions_vec(const MI355FusedArgs &a, const Call
             Pack<T> x[kBatch];
 #pragma unroll
             for (int j = 0; j < kBatch; ++j)
-                if (j < nm) x[j].v = ld16_sys((const u32x4 *)(src_of(a, c, j) + lo * sizeof(T)) + v);
+                if (j < nm) x[j].v = ld16_sys_at(src_of(a, c, j) + lo * sizeof(T), (uint32_t)(v * 16));
 #pragma unroll
             for (int q = 0; q < kBatch; ++q) {
                 if (q >= nm) break;
@@ -560,7 +573,7 @@ __device__ __forceinline__ bool line_has(const unsigned *line, unsigned seq, uns
     return head == seq && tail == seq && check == (__shfl(x, 0) ^ (seq * 0x9E3779B1u));
 }
 
-__device__ void server_next(const MI355FusedArgs &a, MI355ServerMailbox *mb, unsigned seq,
+__device__ __forceinline__ void server_next(const MI355FusedArgs &a, MI355ServerMailbox *mb, unsigned seq,
                             unsigned long long idle_ticks, unsigned *f) {
     unsigned *slot = (unsigned *)(a.sig[a.me] + MI355_SIG_SERVER);
     if (threadIdx.x < 64) {
@@ -843,7 +856,96 @@ __global__ __launch_bounds__(kBlock) void peek_sysload_kernel(PokeParams p) {
     for (int i = threadIdx.x; i < p.n; i += kBlock) p.out[(size_t)blockIdx.x * p.n + i] = ld_sys_u64(p.ptr[i]);
 }
 
+// ---- the caller's producer path (runtime.c producer_test, round 4) ----
+// A caller writes its source with plain stores in its own kernel, then calls;
+// the peers then read it. mark_plain_kernel is that caller kernel: block b
+// stores value + b into dst[b] with a plain (write-back, L2-cached) store,
+// the blocks dealt over the XCDs.
+__global__ __launch_bounds__(64) void mark_plain_kernel(unsigned long long *dst, int words, unsigned long long value) {
+    if (threadIdx.x == 0 && (int)blockIdx.x < words) dst[blockIdx.x] = value + blockIdx.x;
+}
+
+constexpr int kProducerMaxPes = 64;
+struct ProducerReadParams {
+    const unsigned long long *src[kProducerMaxPes];
+    const unsigned long long *flag;  // this PE's flag words [np], or null: no wait
+    unsigned long long token, timeout_ticks;
+    unsigned long long *out;         // [3][nblocks][np * words] + 1 timeout word
+    int np, words;
+};
+
+// The peers' side: (optionally) wait on this PE's signal words for every
+// member's token -- the fused kernel's ARRIVE wait -- then read every
+// member's marker words three ways: plain loads without an acquire (as a
+// multi-launch fold would without mi355_acquire_system), 16-byte system-
+// coherent loads (the fused kernel's folds, ld16_sys_at), and plain loads
+// after a system-scope acquire (the multi-launch schedules' protocol).
+__global__ __launch_bounds__(kBlock) void producer_read_kernel(ProducerReadParams p) {
+    __shared__ int timed_out;
+    if (threadIdx.x == 0) timed_out = 0;
+    __syncthreads();
+    if (p.flag != nullptr && threadIdx.x < 64) {
+        const int q = threadIdx.x;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        unsigned spins = 0;
+        while (true) {
+            const bool done = q >= p.np || ld_sys_u64(p.flag + q) == p.token;
+            if (__all(done)) break;
+            if ((++spins & 63u) == 0 && __builtin_amdgcn_s_memrealtime() - t0 > p.timeout_ticks) {
+                if (q == 0) timed_out = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    __syncthreads();
+    const int per = p.np * p.words;
+    unsigned long long *plain = p.out + (size_t)blockIdx.x * per;
+    unsigned long long *sys = p.out + ((size_t)gridDim.x + blockIdx.x) * per;
+    unsigned long long *acq = p.out + ((size_t)2 * gridDim.x + blockIdx.x) * per;
+    for (int i = threadIdx.x; i < per; i += kBlock) plain[i] = p.src[i / p.words][i % p.words];
+    for (int i = 2 * threadIdx.x; i < per; i += 2 * kBlock) {  // words even: pairs never straddle members
+        const int q = i / p.words, w = i % p.words;
+        const u32x4 v = ld16_sys_at((const char *)p.src[q], (uint32_t)(w * 8));
+        sys[i] = (unsigned long long)v.x | ((unsigned long long)v.y << 32);
+        sys[i + 1] = (unsigned long long)v.z | ((unsigned long long)v.w << 32);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: this CU's L1, its XCD's L2
+    __syncthreads();
+    for (int i = threadIdx.x; i < per; i += kBlock) acq[i] = p.src[i / p.words][i % p.words];
+    if (threadIdx.x == 0 && timed_out) p.out[(size_t)3 * gridDim.x * per] = 1;
+}
+
 }  // namespace
+
+extern "C" int mi355_mark_plain(unsigned long long *dst, int words, unsigned long long value, void *stream) {
+    if (dst == nullptr || words < 1 || words > 1024) return MI355_E_INVAL;
+    hipLaunchKernelGGL(mark_plain_kernel, dim3(words), dim3(64), 0, (hipStream_t)stream, dst, words, value);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+extern "C" int mi355_producer_read(const unsigned long long *const *src, int np, int words,
+                                   const unsigned long long *flag, unsigned long long token,
+                                   unsigned long long timeout_ticks, unsigned long long *out, int nblocks,
+                                   void *stream) {
+    if (src == nullptr || out == nullptr || np < 1 || np > kProducerMaxPes || words < 2 || (words & 1) != 0 ||
+        nblocks < 1 || nblocks > 256)
+        return MI355_E_INVAL;
+    ProducerReadParams p{};
+    for (int q = 0; q < np; ++q) p.src[q] = src[q];
+    p.flag = flag;
+    p.token = token;
+    p.timeout_ticks = timeout_ticks;
+    p.out = out;
+    p.np = np;
+    p.words = words;
+    hipLaunchKernelGGL(producer_read_kernel, dim3(nblocks), dim3(kBlock), 0, (hipStream_t)stream, p);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
 
 extern "C" int mi355_poke(unsigned long long *const *dst, int n, unsigned long long value, void *stream) {
     if (n < 0 || n > kMaxPoke || (n > 0 && dst == nullptr)) return MI355_E_INVAL;

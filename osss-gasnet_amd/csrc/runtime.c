@@ -829,6 +829,101 @@ static void coherence_test (size_t mark_off, int *passed, int *stale, int *syslo
     free (ptrs);
 }
 
+/* The CALLER's producer path (round 4). coherence_test above rewrites its
+ * marker with the library's own write-through store; a caller writes its
+ * source with plain stores in a kernel of its own and then calls. Here every
+ * PE writes 32 marker words with plain stores from 32 blocks of a kernel on
+ * the NULL stream (mi355_mark_plain: dirty lines in several XCDs' L2s), and
+ * the peers read them, after peer reads of the old values cached them, in the
+ * two orderings the library relies on:
+ *   F  the fused kernel's: the same-stream flag publish (mi355_poke on the
+ *      blocking library stream, so after the caller's kernel) and a device
+ *      wait for every member's flag (mi355_producer_read), no host involved;
+ *   H  the multi-launch schedules': shmemi_order_after_caller (signal kernel,
+ *      host wait), host barrier, then the read kernel.
+ * Each read three ways: plain loads with no acquire, 16-byte system-coherent
+ * loads (the fused kernel's folds), plain loads after a system-scope acquire.
+ * res[] = 1 where every block of this PE saw every member's new words, in
+ * shmemi.prod[] order (F plain, F sysload, F acquire, H plain, H sysload,
+ * H acquire). SHMEM_TEST_IPC_FAIL=sysload (PE 1) reports F sysload stale;
+ * =producer reports H acquire stale. */
+static void producer_test (size_t off, int *res)
+{
+    const int np = shmemi.npes, me = shmemi.mype, nb = 32, W = 32;
+    const size_t per = (size_t) np * W, nout = 3 * (size_t) nb * per + 1;
+    const unsigned long long *ptrs[64];
+    unsigned long long *flags[64];
+    unsigned long long *host = (unsigned long long *) calloc (nout, sizeof (unsigned long long));
+    unsigned long long *dev = NULL;
+    if (host == NULL)
+        shmemi_fatal ("out of host memory");
+    SHMEMI_HIP (hipMalloc ((void **) &dev, nout * sizeof (unsigned long long)));
+    for (int q = 0; q < np; ++q) {
+        ptrs[q] = (const unsigned long long *) (shmemi.peer_heap[q] + off);
+        flags[q] = shmemi.peer_sig[q] + MI355_SIG_SELFTEST2 + me;
+    }
+    unsigned long long *own = (unsigned long long *) (shmemi.heap + off);
+    const unsigned long long timeout = 1000000000ull; /* 10 s of the 100 MHz s_memrealtime */
+    const unsigned long long v_old = 0x01D0000000000000ull, v_f = 0xF05ED00000000000ull,
+                             v_h = 0xB05ED00000000000ull, token = 0x70CE000000000001ull;
+    for (int i = 0; i < 6; ++i)
+        res[i] = 1;
+#define RUN(call)                                                                                               \
+    do {                                                                                                        \
+        if ((call) != 0)                                                                                        \
+            shmemi_fatal ("producer-path test: launch failed: %s", #call);                                     \
+    } while (0)
+#define READ_BACK(first)                                                                                        \
+    do {                                                                                                        \
+        SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));                                                      \
+        SHMEMI_HIP (hipMemcpy (host, dev, nout * sizeof (unsigned long long), hipMemcpyDeviceToHost));          \
+        for (int t = 0; t < 3; ++t)                                                                             \
+            for (int b = 0; b < nb; ++b)                                                                        \
+                for (size_t i = 0; i < per; ++i)                                                                \
+                    if (host[((size_t) t * nb + b) * per + i] !=                                                \
+                        val + ((unsigned long long) (i / W) << 16) + (i % W))                                   \
+                        res[(first) + t] = 0;                                                                   \
+        if (host[nout - 1] != 0)                                                                                \
+            res[(first)] = res[(first) + 1] = res[(first) + 2] = 0;                                             \
+    } while (0)
+    /* the old values, cached by every PE's reads */
+    RUN (mi355_mark_plain (own, W, v_old + ((unsigned long long) me << 16), NULL));
+    SHMEMI_HIP (hipDeviceSynchronize ());
+    shmemi_barrier_set (0, 1, np);
+    SHMEMI_HIP (hipMemset (dev, 0, nout * sizeof (unsigned long long)));
+    RUN (mi355_producer_read (ptrs, np, W, NULL, 0, 0, dev, nb, shmemi.stream));
+    SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    shmemi_barrier_set (0, 1, np);
+    /* F: caller kernel on the null stream, then the fused kernel's ordering */
+    unsigned long long val = v_f;
+    RUN (mi355_mark_plain (own, W, v_f + ((unsigned long long) me << 16), NULL));
+    SHMEMI_HIP (hipMemsetAsync (dev, 0, nout * sizeof (unsigned long long), shmemi.stream));
+    RUN (mi355_poke (flags, np, token, shmemi.stream));
+    RUN (mi355_producer_read (ptrs, np, W, shmemi.sigmem + MI355_SIG_SELFTEST2, token, timeout, dev, nb,
+                              shmemi.stream));
+    /* kernel order = PE order of the results (i / W = member q) */
+    READ_BACK (0);
+    shmemi_barrier_set (0, 1, np); /* nobody reads the F words any more */
+    /* H: caller kernel on the null stream, then the multi-launch ordering */
+    val = v_h;
+    RUN (mi355_mark_plain (own, W, v_h + ((unsigned long long) me << 16), NULL));
+    shmemi_order_after_caller (1);
+    shmemi_barrier_set (0, 1, np);
+    SHMEMI_HIP (hipMemsetAsync (dev, 0, nout * sizeof (unsigned long long), shmemi.stream));
+    RUN (mi355_producer_read (ptrs, np, W, NULL, 0, 0, dev, nb, shmemi.stream));
+    READ_BACK (3);
+    shmemi_barrier_set (0, 1, np);
+#undef READ_BACK
+#undef RUN
+    const char *fail = me == 1 ? getenv ("SHMEM_TEST_IPC_FAIL") : NULL;
+    if (fail != NULL && strcmp (fail, "sysload") == 0)
+        res[MI355_PROD_F_SYS] = 0;
+    if (fail != NULL && strcmp (fail, "producer") == 0)
+        res[MI355_PROD_H_ACQ] = 0;
+    (void) hipFree (dev);
+    free (host);
+}
+
 /* Interconnect check at init (PE_size > 1): every PE stores a value into
  * every peer's signal region over the peer mapping (what the fused kernel's
  * flags do) and reads a marker from every peer's heap (what the reduce-scatter
@@ -903,6 +998,16 @@ static void interconnect_selftest (void)
         int passed = 1, stale = 0, sysload = 0;
         coherence_test (mark_off, &passed, &stale, &sysload);
         coh = 4 | (passed << 3) | (stale << 4) | (sysload << 5);
+        if (np <= 64) { /* mi355_producer_read's member limit */
+            int prod[6];
+            producer_test (mark_off + 8 - 1024, prod); /* 32 words below the marker, 16-byte aligned */
+            coh |= 1 << 6;
+            for (int i = 0; i < 6; ++i)
+                coh |= prod[i] << (7 + i);
+            /* the multi-launch schedules read peers' buffers the H way */
+            passed &= prod[MI355_PROD_H_ACQ];
+            coh = (coh & ~(1 << 3)) | (passed << 3);
+        }
         if (!passed)
             heap_ok = 0;
     }
@@ -914,6 +1019,9 @@ static void interconnect_selftest (void)
     shmemi.coh_passed = all_mapped;
     shmemi.coh_stale = 0;
     shmemi.coh_sysload = all_mapped;
+    shmemi.prod_ran = all_mapped;
+    for (int i = 0; i < 6; ++i)
+        shmemi.prod[i] = all_mapped;
     for (int q = 0; q < np; ++q) {
         const int r = __atomic_load_n (&seg_info (q)->selftest, __ATOMIC_ACQUIRE);
         all_sig &= r & 1;
@@ -921,13 +1029,31 @@ static void interconnect_selftest (void)
         shmemi.coh_passed &= (r >> 3) & 1;
         shmemi.coh_stale |= (r >> 4) & 1;
         shmemi.coh_sysload &= (r >> 5) & 1;
+        shmemi.prod_ran &= (r >> 6) & 1;
+        for (int i = 0; i < 6; ++i)
+            shmemi.prod[i] &= (r >> (7 + i)) & 1;
     }
+    if (!shmemi.prod_ran)
+        for (int i = 0; i < 6; ++i)
+            shmemi.prod[i] = 0;
     /* the fused kernel's per-block acquires are redundant when its
-     * system-coherent loads read fresh data on every PE (the same decision on
-     * every PE: from the same records); SHMEM_FUSED_ACQUIRE=1 keeps them */
+     * system-coherent loads read fresh data on every PE, both after the
+     * library's own write-through stores and after a caller's kernel wrote
+     * with plain stores and the fused kernel's flag ordering passed (the same
+     * decision on every PE: from the same records); SHMEM_FUSED_ACQUIRE=1
+     * keeps them */
     {
         static const char *acq_env[] = {"SHMEM_FUSED_ACQUIRE", NULL};
-        shmemi.fused_no_acquire = shmemi.coh_sysload && shmemi.coh_passed && env_long (acq_env, 0) == 0;
+        shmemi.fused_no_acquire = shmemi.coh_sysload && shmemi.prod_ran && shmemi.prod[MI355_PROD_F_SYS] &&
+                                  shmemi.coh_passed && env_long (acq_env, 0) == 0;
+    }
+    /* a caller's data not seen through the fused kernel's ordering even
+     * after an acquire: the fused kernel is not used */
+    if (shmemi.prod_ran && !shmemi.prod[MI355_PROD_F_ACQ] && !shmemi.prod[MI355_PROD_F_SYS]) {
+        if (me == 0)
+            fprintf (stderr, "[shmem] warning: a caller's plain stores were not visible to peers through the fused "
+                             "kernel's flag ordering (init producer-path test); the fused kernel is disabled\n");
+        shmemi.fused_max = 0;
     }
     if (all_mapped && !shmemi.coh_passed && me == 0)
         fprintf (stderr, "[shmem] warning: a peer heap re-read after a system-scope acquire returned stale data "
@@ -1216,6 +1342,10 @@ void pshmem_init (void)
     sigmem_init ();
     server_init ();
     shmemi.fused_max = env_size ("SHMEM_FUSED_MAX_BYTES", (size_t) 1 << 20);
+    /* the fused kernel's folds address a member's buffer with 32-bit byte
+     * offsets (fused.hip ld16_sys_at) */
+    if (shmemi.fused_max > ((size_t) 1 << 30))
+        shmemi.fused_max = (size_t) 1 << 30;
     shmemi.oneshot_max = env_size ("SHMEM_ONESHOT_MAX_BYTES", (size_t) 64 << 10);
 
     if (shmemi.npes > 1) {
@@ -1470,6 +1600,16 @@ void shmemx_coherence_sysload (int *sysload_fresh, int *acquires_skipped)
         *sysload_fresh = shmemi.coh_sysload;
     if (acquires_skipped != NULL)
         *acquires_skipped = shmemi.fused_no_acquire;
+}
+
+/* MI355X extension (shmemx.h): the init producer-path test's job-wide outcomes */
+void shmemx_coherence_producer (int *ran, int *fresh)
+{
+    if (ran != NULL)
+        *ran = shmemi.prod_ran;
+    if (fresh != NULL)
+        for (int i = 0; i < 6; ++i)
+            fresh[i] = shmemi.prod[i];
 }
 
 int shmemx_get_reduce_order (void) { return shmemi.order; }

@@ -65,7 +65,11 @@ struct shmemi_pe_info {
     uint64_t heap_size;
     int32_t published;
     int32_t selftest;           /* bit 0: signal region stores seen, bit 1: heap reads ok,
-                                   bit 2: coherence test ran, bit 3: it passed, bit 4: stale without acquire */
+                                   bit 2: coherence test ran, bit 3: it passed, bit 4: stale without acquire,
+                                   bit 5: system-coherent loads fresh without an acquire (write-through marker),
+                                   bit 6: producer-path test ran, bits 7-12: its six outcomes (1 = fresh) in
+                                   shmemi.prod[] order: fused ordering plain / sysload / acquire, then the
+                                   host-wait ordering plain / sysload / acquire */
     uint64_t collect_bytes;     /* this PE's contribution to the current shmem_collect */
     struct shmemi_settings settings;
     struct shmemi_dbg_rec dbg;
@@ -178,6 +182,20 @@ struct shmemi_state {
      * every PE: then the fused kernel skips its per-block acquires
      * (fused_no_acquire; SHMEM_FUSED_ACQUIRE=1 keeps them) */
     int coh_sysload, fused_no_acquire;
+    /* the caller's producer path (producer_test, job-wide ANDs): sources
+     * written by plain stores in a kernel on the null stream, then read by
+     * the peers after the fused kernel's ordering (same-stream flag, device
+     * wait: prod[0..2]) and after the multi-launch schedules' ordering (signal
+     * kernel, host wait, host barrier: prod[3..5]), each read three ways:
+     * plain loads without an acquire, 16-byte system-coherent loads, plain
+     * loads after a system-scope acquire (MI355_PROD_* indices) */
+    int prod_ran, prod[6];
+#define MI355_PROD_F_PLAIN 0
+#define MI355_PROD_F_SYS 1
+#define MI355_PROD_F_ACQ 2
+#define MI355_PROD_H_PLAIN 3
+#define MI355_PROD_H_SYS 4
+#define MI355_PROD_H_ACQ 5
 
     /* what the last *_to_all call ran (shmemx_last_call_info); the kernel
      * stub is resolved to its name only on request */

@@ -310,6 +310,17 @@ class Shmem:
         self.lib.shmemx_coherence_sysload(ctypes.byref(a), ctypes.byref(b))
         return bool(a.value), bool(b.value)
 
+    PRODUCER_FIELDS = ("fused_plain_no_acquire", "fused_sysload", "fused_after_acquire",
+                       "host_plain_no_acquire", "host_sysload", "host_after_acquire")
+
+    def coherence_producer(self):
+        """(ran, {field: fresh}) of the init test of a caller's producer path
+        (plain stores in a null-stream kernel, then the fused kernel's or the
+        multi-launch schedules' ordering; shmemx.h shmemx_coherence_producer)"""
+        ran, fresh = _i(), (ctypes.c_int * 6)()
+        self.lib.shmemx_coherence_producer(ctypes.byref(ran), fresh)
+        return bool(ran.value), {k: bool(fresh[i]) for i, k in enumerate(self.PRODUCER_FIELDS)}
+
     def kernel_timing(self, enable):
         self.lib.shmemx_kernel_timing(1 if enable else 0)
 

@@ -48,3 +48,27 @@ def test_register_heavy_variant_trips_the_check(tmp_path):
     assert bad.returncode == 1
     fails = [ln for ln in bad.stderr.splitlines() if "FAIL" in ln]
     assert len(fails) == 1 and "fused_allreduce_heavy" in fails[0] and "admits 6" in fails[0], bad.stderr
+
+
+def test_library_kernels_use_no_scratch():
+    """Round 4: no kernel of the library has a private
+    segment -- the complex-product fused kernels had 1,264 B per lane (call
+    frames of non-inlined helpers), the x87 every-member fold 24 B."""
+    lib = os.path.join(ROOT, "osss-gasnet_amd", "lib")
+    objs = ["combine.o", "fused.o"] + sorted(f for f in os.listdir(lib) if f.startswith("combine_t_"))
+    for o in objs:
+        r = subprocess.run([sys.executable, TOOL, "--no-scratch", os.path.join(lib, o)], capture_output=True,
+                           text=True)
+        assert r.returncode == 0, o + ": " + r.stdout + r.stderr
+        assert ", 0 with scratch" in r.stdout, r.stdout
+
+
+def test_scratch_kernel_trips_the_no_scratch_check(tmp_path):
+    obj = str(tmp_path / "scratch_probe.o")
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O2", "-c",
+                    os.path.join(ROOT, "tests", "native", "scratch_probe.hip"), "-o", obj], check=True,
+                   cwd=str(tmp_path))
+    r = subprocess.run([sys.executable, TOOL, "--no-scratch", obj], capture_output=True, text=True)
+    assert r.returncode == 1
+    fails = [ln for ln in r.stderr.splitlines() if "FAIL" in ln]
+    assert len(fails) == 1 and "with_scratch" in fails[0], r.stderr

@@ -15,7 +15,18 @@ min(constant, the occupancy API's view: VGPRs, LDS, 8) -- exceed what the
 hardware admits (the same, and the SGPR limit).
 
 usage: check_residency.py OBJECT [--header residency.h] [--kernels REGEX] [--quiet]
+       check_residency.py --no-scratch OBJECT
 OBJECT: a hipcc -c output (its .hip_fatbin section is unbundled) or a code object.
+
+--no-scratch (round 4): every kernel of OBJECT must have a private segment of
+0 bytes and no dynamic stack -- no scratch memory per lane. Scratch in a
+kernel with several blocks per CU was the suspect of round 2's x87 errors
+(the probe of profiles/r04 ruled it out there), and in the
+spin-waiting grids it is a cost on every launch: the 1,264 bytes per lane of
+the complex-product fused kernels were the call frames of non-inlined
+helpers, the 24 bytes of the x87 every-member fold a copy of the kernel
+arguments' pointer array indexed by a rolled loop. A kernel that must keep
+scratch is listed in SCRATCH_ALLOWED with its reason.
 """
 import argparse
 import os
@@ -91,6 +102,27 @@ def admitted(k):
     return min(MAX_PER_CU, by_sgpr, by_vgpr, by_lds), by_sgpr, by_vgpr, by_lds
 
 
+SCRATCH_ALLOWED = {}   # demangled-name regex -> why the scratch is needed (none today)
+
+
+def no_scratch(path):
+    with tempfile.TemporaryDirectory() as tmp:
+        ks = kernels(code_object(path, tmp))
+    names = demangle([k["name"] for k in ks])
+    bad = []
+    for k, dn in zip(ks, names):
+        ps = int(k.get("private_segment_fixed_size", 0))
+        dyn = k.get("uses_dynamic_stack", "false") == "true"
+        if (ps or dyn) and not any(re.search(rx, dn) for rx in SCRATCH_ALLOWED):
+            bad.append((dn, ps, dyn))
+    for dn, ps, dyn in bad:
+        print(f"check_residency: FAIL {dn}: {ps} bytes of scratch per lane{' + a dynamic stack' if dyn else ''} "
+              f"(private_segment_fixed_size); inline the callees / index register arrays with constants, or "
+              f"justify it in SCRATCH_ALLOWED", file=sys.stderr)
+    print(f"check_residency --no-scratch: {len(ks)} kernels in {os.path.basename(path)}, {len(bad)} with scratch")
+    return 1 if bad else 0
+
+
 def header_constant(path):
     m = re.search(r"#define\s+MI355_FUSED_RESIDENT_PER_CU\s+(\d+)", open(path).read())
     if not m:
@@ -99,6 +131,8 @@ def header_constant(path):
 
 
 def main():
+    if len(sys.argv) == 3 and sys.argv[1] == "--no-scratch":
+        sys.exit(no_scratch(sys.argv[2]))
     here = os.path.dirname(os.path.abspath(__file__))
     ap = argparse.ArgumentParser()
     ap.add_argument("object")

@@ -90,6 +90,92 @@ __global__ __launch_bounds__(256) void fold_gs(Srcs in, u32x4 *d, size_t nvec) {
     }
 }
 
+// Round 4: fold_gs with 16-byte loads issued as inline asm (global_load_dwordx4
+// with the cache bits POL names), every load of a pass issued before the first
+// wait. The compiler does not track an asm load's destination, so each loaded
+// vector is tied to an explicit s_waitcnt through a "+v" operand: COUNTED = 0
+// waits for vmcnt(0) once (the later waits are already satisfied); COUNTED = 1
+// waits for each vector with vmcnt(loads issued after it), so the first
+// sources' adds overlap the last loads (vmcnt retires in issue order on gfx9,
+// and the previous pass's stores were issued before these loads). A partial
+// last pass falls back to vmcnt(0).
+enum { LD_SYS = 0, LD_NT = 1, LD_PLAIN = 2 };
+template <int POL>
+__device__ __forceinline__ u32x4 ld16_asm(const u32x4 *p) {
+    u32x4 r;
+    if constexpr (POL == LD_SYS)
+        asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(r) : "v"(p) : "memory");
+    else if constexpr (POL == LD_NT)
+        asm volatile("global_load_dwordx4 %0, %1, off nt" : "=v"(r) : "v"(p) : "memory");
+    else
+        asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+    return r;
+}
+template <int N>
+__device__ __forceinline__ void wait_vm(u32x4 &v) {
+    asm volatile("s_waitcnt vmcnt(%1)" : "+v"(v) : "i"(N));
+}
+// group u's K vectors: load j = u*K + k has K*U-1-j loads and u stores (groups
+// 0..u-1, stored since) issued after it
+template <int K, int U, int UU, int KK>
+__device__ __forceinline__ void wait_group(P2 (&x)[U][K]) {
+    if constexpr (KK < K) {
+        wait_vm<K * U - 1 - (UU * K + KK) + UU>(x[UU][KK].v);
+        wait_group<K, U, UU, KK + 1>(x);
+    }
+}
+template <int K, int U, int ST, int UU>
+__device__ __forceinline__ void fold_counted(P2 (&x)[U][K], u32x4 *d, size_t base) {
+    if constexpr (UU < U) {
+        wait_group<K, U, UU, 0>(x);
+        P2 a = x[UU][0];
+#pragma unroll
+        for (int k = 1; k < K; ++k) {
+            a.e[0] = a.e[0] + x[UU][k].e[0];
+            a.e[1] = a.e[1] + x[UU][k].e[1];
+        }
+        store<ST>(d + base + (size_t)UU * 256, a.v);
+        fold_counted<K, U, ST, UU + 1>(x, d, base);
+    }
+}
+template <int K, int U, int ST, int POL, int COUNTED>
+__global__ __launch_bounds__(256) void fold_asm(Srcs in, u32x4 *d, size_t nvec) {
+    const size_t step = (size_t)gridDim.x * 256 * U;
+    for (size_t base = (size_t)blockIdx.x * 256 * U + threadIdx.x; base < nvec; base += step) {
+        P2 x[U][K];
+        const bool full = base + (size_t)(U - 1) * 256 < nvec;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            size_t i = base + (size_t)u * 256;
+            if (i < nvec) {
+#pragma unroll
+                for (int k = 0; k < K; ++k) x[u][k].v = ld16_asm<POL>(in.s[k] + i);
+            }
+        }
+        if (COUNTED && full) {
+            fold_counted<K, U, ST, 0>(x, d, base);
+            continue;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < K; ++k) wait_vm<0>(x[u][k].v);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            size_t i = base + (size_t)u * 256;
+            if (i < nvec) {
+                P2 a = x[u][0];
+#pragma unroll
+                for (int k = 1; k < K; ++k) {
+                    a.e[0] = a.e[0] + x[u][k].e[0];
+                    a.e[1] = a.e[1] + x[u][k].e[1];
+                }
+                store<ST>(d + i, a.v);
+            }
+        }
+    }
+}
+
 // as fold_gs, but full passes (all U vectors in range) run without per-vector
 // range tests; only the last, partial pass is guarded
 template <int K, int U, int ST, int NT>
@@ -612,6 +698,74 @@ int main(int argc, char **argv) {
             RUN(fold_gs, 1, 4, ST_NT_SC1, 0, 1, srcs_sep(), "copy, library-like");
             RUN(fold_gs, 1, 4, ST_NT_SC1, 2, 1, srcs_sep(), "copy, system-coherent loads");
             RUN(fold_gs, 1, 4, ST_NT_SC1, 2, 4, srcs_sep(), "copy, system-coherent loads");
+        }
+        return 0;
+    }
+    if (argc > 1 && argv[1][0] == 'S') {  // round 4: 16-byte system-coherent loads (fold_asm) vs the library's
+#define RUNA(K, U, ST, POL, C, BPC, LABEL) do {                                                     \
+        Srcs s_ = srcs_sep();                                                                       \
+        snprintf(name, sizeof name, "fold_asm<U%d,%s,%s,%s> %d/CU %s", U, #ST, #POL,                \
+                 C ? "counted" : "vmcnt0", BPC, LABEL);                                             \
+        rep(name, K, time_us([&] { hipLaunchKernelGGL((fold_asm<K, U, ST, POL, C>), dim3(cus * BPC), \
+                                                        dim3(256), 0, 0, s_, d, nvec); }));         \
+    } while (0)
+        // correctness first: every asm variant against fold_gs (nt loads) on distinct per-source data,
+        // over a length that leaves a partial last pass
+        {
+            Srcs s_ = srcs_sep();
+            std::vector<double> h(nvec * 2);
+            for (int k = 0; k < 8; ++k) {
+                uint64_t z = 0x9E3779B97F4A7C15ull * (k + 3);
+                for (auto &v : h) { z ^= z << 13; z ^= z >> 7; z ^= z << 17; v = (double)(int64_t)z * 0x1p-63; }
+                CHECK(hipMemcpy(sep[k], h.data(), bytes, hipMemcpyHostToDevice));
+            }
+            u32x4 *d2;
+            CHECK(hipMalloc(&d2, bytes));
+            const size_t nv = nvec - 77;
+            std::vector<double> a(nv * 2), b(nv * 2);
+            auto check = [&](const char *what, auto launch_ref, auto launch) {
+                CHECK(hipMemset(d, 0xff, bytes));
+                CHECK(hipMemset(d2, 0xee, bytes));
+                launch_ref();
+                launch();
+                CHECK(hipDeviceSynchronize());
+                CHECK(hipMemcpy(a.data(), d, nv * 16, hipMemcpyDeviceToHost));
+                CHECK(hipMemcpy(b.data(), d2, nv * 16, hipMemcpyDeviceToHost));
+                size_t bad = 0;
+                for (size_t i = 0; i < nv * 2; ++i) bad += memcmp(&a[i], &b[i], 8) != 0;
+                printf("check %-40s vs fold_gs: %zu mismatches of %zu\n", what, bad, nv * 2);
+                fflush(stdout);
+            };
+#define CHK(K, U, BPC, POL, C)                                                                                  \
+            check(#K " " #U " " #POL " " #C,                                                                   \
+                  [&] { hipLaunchKernelGGL((fold_gs<K, U, ST_SC1, 1>), dim3(cus * BPC), dim3(256), 0, 0, s_, d, nv); }, \
+                  [&] { hipLaunchKernelGGL((fold_asm<K, U, ST_SC1, POL, C>), dim3(cus * BPC), dim3(256), 0, 0, s_, d2, nv); })
+            CHK(8, 4, 8, LD_SYS, 0);
+            CHK(8, 4, 8, LD_SYS, 1);
+            CHK(2, 1, 2, LD_SYS, 0);
+            CHK(2, 1, 2, LD_SYS, 1);
+            CHK(2, 2, 2, LD_SYS, 1);
+            CHK(1, 4, 1, LD_SYS, 1);
+            CHK(8, 4, 8, LD_NT, 1);
+            CHECK(hipFree(d2));
+        }
+        for (int r = 0; r < 3; ++r) {
+            RUN(fold_gs, 8, 4, ST_SC1, 1, 8, srcs_sep(), "library shape k=8");
+            RUNA(8, 4, ST_SC1, LD_NT, 0, 8, "k=8 asm nt loads");
+            RUNA(8, 4, ST_SC1, LD_NT, 1, 8, "k=8 asm nt loads");
+            RUNA(8, 4, ST_SC1, LD_SYS, 0, 8, "k=8 16-B system-coherent");
+            RUNA(8, 4, ST_SC1, LD_SYS, 1, 8, "k=8 16-B system-coherent");
+            RUNA(8, 2, ST_SC1, LD_SYS, 1, 8, "k=8 16-B system-coherent");
+            RUN(fold_gs, 8, 4, ST_SC1, 2, 8, srcs_sep(), "k=8, 2x8-B system-coherent (r03)");
+            RUN(fold_gs, 2, 1, ST_SC1, 1, 2, srcs_sep(), "library shape k=2");
+            RUNA(2, 1, ST_SC1, LD_NT, 1, 2, "k=2 asm nt loads");
+            RUNA(2, 1, ST_SC1, LD_SYS, 0, 2, "k=2 16-B system-coherent");
+            RUNA(2, 1, ST_SC1, LD_SYS, 1, 2, "k=2 16-B system-coherent");
+            RUNA(2, 2, ST_SC1, LD_SYS, 1, 2, "k=2 16-B system-coherent");
+            RUN(fold_gs, 2, 1, ST_SC1, 2, 2, srcs_sep(), "k=2, 2x8-B system-coherent (r03)");
+            RUN(fold_gs, 1, 4, ST_NT_SC1, 0, 1, srcs_sep(), "copy, library-like");
+            RUNA(1, 4, ST_NT_SC1, LD_SYS, 1, 1, "copy 16-B system-coherent");
+            RUNA(1, 4, ST_NT_SC1, LD_PLAIN, 1, 1, "copy asm plain loads");
         }
         return 0;
     }
