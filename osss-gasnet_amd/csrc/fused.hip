@@ -82,6 +82,26 @@ __device__ unsigned long long g_phase[64][8];
 #define PHASE_RESET_NEXT(c) ((void)0)
 #endif
 
+// The protocol helpers below (counts, waits, block counting, publish, finish,
+// staging copy, the server's mailbox) are inlined into every kernel: in the
+// large complex-product instantiations the compiler had left them as calls,
+// whose frames took 1,264 bytes of scratch per lane (round 4;
+// tools/check_residency.py --no-scratch). -DMI355_FUSED_INLINE_HELPERS=0
+// restores the compiler's choice (measurement builds only).
+#ifndef MI355_FUSED_INLINE_HELPERS
+#define MI355_FUSED_INLINE_HELPERS 1
+#endif
+#if MI355_FUSED_INLINE_HELPERS
+#define FUSED_HELPER __device__ __forceinline__
+#else
+#define FUSED_HELPER __device__
+#endif
+// -DMI355_FUSED_BUFFER_LOADS=0: the folds read with ld16_sys (two 8-byte
+// atomic loads) instead of ld16_sys_at (measurement builds only)
+#ifndef MI355_FUSED_BUFFER_LOADS
+#define MI355_FUSED_BUFFER_LOADS 1
+#endif
+
 __device__ __forceinline__ void st_sys_u64(unsigned long long *p, unsigned long long v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -121,9 +141,13 @@ __device__ __forceinline__ u32x4 ld16_sys(const void *p) {
 // loads take 116 / 381 us, so the multi-launch folds keep theirs.
 // The offset must stay below 4 GiB (the fused path is capped at 1 GiB).
 __device__ __forceinline__ u32x4 ld16_sys_at(const char *base, uint32_t off) {
+#if MI355_FUSED_BUFFER_LOADS
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0, (int)0xFFFFFFF0u, 0x00020000);
     return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 17);  // aux 17: sc0 | sc1
+#else
+    return ld16_sys(base + off);
+#endif
 }
 template <typename T>
 __device__ __forceinline__ T ld_elem_sys(const T *p) {
@@ -148,7 +172,7 @@ __device__ __forceinline__ T ld_elem_sys(const T *p) {
 }
 
 // This call's pair count with every member (lanes of wave 0, into LDS).
-__device__ __forceinline__ void load_counts(const MI355FusedArgs &a, const unsigned long long *mine, unsigned long long *cnt) {
+FUSED_HELPER void load_counts(const MI355FusedArgs &a, const unsigned long long *mine, unsigned long long *cnt) {
     if (threadIdx.x < a.nmembers) cnt[threadIdx.x] = ld_sys_u64(mine + MI355_SIG_CALLS + a.pe[threadIdx.x]) + 1;
     __syncthreads();
 }
@@ -158,7 +182,7 @@ __device__ __forceinline__ void load_counts(const MI355FusedArgs &a, const unsig
 // acquire = false only where every later read of the members' buffers is a
 // system-coherent load (fused_body under no_acquire); fused_pull's copies
 // read with plain loads and always acquire.
-__device__ __forceinline__ bool wait_members(const MI355FusedArgs &a, const unsigned long long *mine, const unsigned long long *cnt,
+FUSED_HELPER bool wait_members(const MI355FusedArgs &a, const unsigned long long *mine, const unsigned long long *cnt,
                              int base, bool include_self, bool acquire = true) {
     bool ok = true;
     if (threadIdx.x < 64) {
@@ -187,7 +211,7 @@ __device__ __forceinline__ bool wait_members(const MI355FusedArgs &a, const unsi
 }
 
 // Count this block in on a local counter; true for the grid's last block.
-__device__ __forceinline__ bool last_block(unsigned long long *counter) {
+FUSED_HELPER bool last_block(unsigned long long *counter) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     __shared__ int is_last;
@@ -200,13 +224,13 @@ __device__ __forceinline__ bool last_block(unsigned long long *counter) {
     return is_last != 0;
 }
 
-__device__ __forceinline__ void publish(const MI355FusedArgs &a, const unsigned long long *cnt, int base) {
+FUSED_HELPER void publish(const MI355FusedArgs &a, const unsigned long long *cnt, int base) {
     // lanes of wave 0: one member each (this PE included)
     if (threadIdx.x < a.nmembers) st_sys_u64(a.sig[threadIdx.x] + base + a.pe[a.me], cnt[threadIdx.x]);
 }
 
 // Advance the pair counts (the call is over on every member), then report.
-__device__ __forceinline__ void finish(const MI355FusedArgs &a, unsigned long long *mine, const unsigned long long *cnt, bool ok,
+FUSED_HELPER void finish(const MI355FusedArgs &a, unsigned long long *mine, const unsigned long long *cnt, bool ok,
                        unsigned epoch) {
     if (ok && threadIdx.x < a.nmembers) st_sys_u64(mine + MI355_SIG_CALLS + a.pe[threadIdx.x], cnt[threadIdx.x]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -248,7 +272,7 @@ __device__ void block_drain(bool plain) {
     if (__syncthreads_or(plain) && threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
-__device__ __forceinline__ void block_copy(void *dst, const void *src, uint64_t nbytes, unsigned bi, unsigned nblocks) {
+FUSED_HELPER void block_copy(void *dst, const void *src, uint64_t nbytes, unsigned bi, unsigned nblocks) {
     block_drain(block_copy_issue(dst, src, nbytes, bi, nblocks));
 }
 
@@ -573,7 +597,7 @@ __device__ __forceinline__ bool line_has(const unsigned *line, unsigned seq, uns
     return head == seq && tail == seq && check == (__shfl(x, 0) ^ (seq * 0x9E3779B1u));
 }
 
-__device__ __forceinline__ void server_next(const MI355FusedArgs &a, MI355ServerMailbox *mb, unsigned seq,
+FUSED_HELPER void server_next(const MI355FusedArgs &a, MI355ServerMailbox *mb, unsigned seq,
                             unsigned long long idle_ticks, unsigned *f) {
     unsigned *slot = (unsigned *)(a.sig[a.me] + MI355_SIG_SERVER);
     if (threadIdx.x < 64) {

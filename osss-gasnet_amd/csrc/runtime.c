@@ -990,15 +990,20 @@ static void interconnect_selftest (void)
     /* every PE runs the coherence test when every PE has its peers mapped */
     __atomic_store_n (&seg_info (me)->selftest, sig_ok | (heap_ok << 1), __ATOMIC_RELEASE);
     shmemi_barrier_set (0, 1, np);
-    int all_mapped = 1;
-    for (int q = 0; q < np; ++q)
-        all_mapped &= (__atomic_load_n (&seg_info (q)->selftest, __ATOMIC_ACQUIRE) >> 1) & 1;
+    int all_mapped = 1, all_sig_mapped = 1;
+    for (int q = 0; q < np; ++q) {
+        const int r = __atomic_load_n (&seg_info (q)->selftest, __ATOMIC_ACQUIRE);
+        all_mapped &= (r >> 1) & 1;
+        all_sig_mapped &= r & 1;
+    }
     int coh = 0;
     if (all_mapped) {
         int passed = 1, stale = 0, sysload = 0;
         coherence_test (mark_off, &passed, &stale, &sysload);
         coh = 4 | (passed << 3) | (stale << 4) | (sysload << 5);
-        if (np <= 64) { /* mi355_producer_read's member limit */
+        /* mi355_producer_read's member limit; its F round stores flags into
+         * every peer's signal region, so every PE must have mapped them all */
+        if (np <= 64 && all_sig_mapped) {
             int prod[6];
             producer_test (mark_off + 8 - 1024, prod); /* 32 words below the marker, 16-byte aligned */
             coh |= 1 << 6;

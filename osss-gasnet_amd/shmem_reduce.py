@@ -155,6 +155,11 @@ class Shmem:
         self.lib.shmemx_persistent_stats(ctypes.byref(a), ctypes.byref(b))
         return a.value, b.value
 
+    def external_map_fallbacks(self):
+        """calls staged because a member could not open a peer's buffer (shmemx.h)"""
+        self.lib.shmemx_external_map_fallbacks.restype = ctypes.c_long
+        return int(self.lib.shmemx_external_map_fallbacks())
+
     def external_map_stats(self):
         """(peers' allocations mapped now, opened, closed since init): device
         buffers outside the heap that calls mapped (shmemx.h)"""

@@ -393,6 +393,7 @@ def main():
         if n and c.get("api") != "fortran":
             results[str(c["id"]) + "_schedule"] = np.array([shm.last_call_info()["schedule"]])
     results["external_map_stats"] = np.array(shm.external_map_stats())
+    results["external_map_fallbacks"] = np.array([shm.external_map_fallbacks()])
     results["fd_count"] = np.array([fds_start, len(os.listdir("/proc/self/fd"))])
     hip.hipFree(pa)
     hip.hipFree(pb)

@@ -461,9 +461,9 @@ def test_external_device_buffers_fallbacks(tmp_path):
 
 
 def test_external_buffer_open_failure_stages_the_call(tmp_path):
-    """A member that cannot open a peer's exported buffer (this HIP's dmabuf
-    IPC refuses a handle once every importer has closed it; simulated here on
-    PE 1, SHMEM_TEST_IPC_FAIL=extopen) does not abort the job: after the
+    """A member that cannot open a peer's exported buffer (simulated on PE 1,
+    SHMEM_TEST_IPC_FAIL=extopen; HIP refuses the handle of an allocation its
+    owner has freed, tools/ipc_reopen_probe.py) does not abort the job: after the
     second round of the record exchange every member stages the call, and the
     results stay exact on every PE, fused and multi-launch sizes alike."""
     cases = make_cases(MAPPED_PAIRS, 5000, [[0, 0, 3]], "devother", "p2p", 0)
@@ -474,6 +474,26 @@ def test_external_buffer_open_failure_stages_the_call(tmp_path):
     for c in cases:
         for pe in range(3):
             assert not str(results[pe][str(c["id"]) + "_schedule"][0]).startswith("mapped-"), (c["id"], pe)
+
+
+def test_external_buffer_open_failure_recovers(tmp_path):
+    """after ONE failed open (SHMEM_TEST_IPC_FAIL=extopen1, PE 1's
+    first hipIpcOpenMemHandle) the call stages, every member drops its cached
+    exports of the call's buffers, and the next calls on the same buffers map
+    again: exactly one staged fallback on every PE, every later call
+    "mapped-*", the results exact."""
+    cases = make_cases(MAPPED_PAIRS[:4], 5000, [[0, 0, 3]], "devother", "p2p", 0)
+    cases += make_cases(MAPPED_PAIRS[:4], 200000, [[0, 0, 3]], "devmap_offset", "p2p", 100)
+    results = run_pes(3, cases, tmp_path, extra_env={"SHMEM_DEVICE_SCRATCH_SIZE": "3M",
+                                                     "SHMEM_TEST_IPC_FAIL": "extopen1"})
+    check(results, cases)
+    for pe in range(3):
+        assert int(results[pe]["external_map_fallbacks"][0]) == 1, pe
+        scheds = [str(results[pe][str(c["id"]) + "_schedule"][0]) for c in cases]
+        assert not scheds[0].startswith("mapped-"), scheds[0]
+        assert all(s.startswith("mapped-") for s in scheds[1:]), (pe, scheds)
+        mapped, opened, closed = (int(v) for v in results[pe]["external_map_stats"])
+        assert opened >= 2, (pe, opened)
 
 
 @pytest.mark.parametrize("npes", [1, 3])

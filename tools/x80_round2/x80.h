@@ -1,4 +1,8 @@
-// Round 2 x80.h (branchy general path), kept only for tools/x80_lane_probe.hip's before/after runs.
+// Round 2 x80.h (branchy general path): the FIXTURE of the x87 co-residency
+// investigation. Built into tools/x80_lane_probe_r2 (tools/Makefile),
+// it is the control of tests/test_gpu_x87_coresidency.py: its general kernels
+// return wrong x87 results in waves that share a SIMD with another wave
+// (profiles/r04/x80/). Not product code; never linked into the library.
 // x80.h -- x87 80-bit extended ("long double" on x86-64 Linux) arithmetic on
 // the GPU, for shmem_longdouble_{sum,prod,min,max}_to_all.
 //
