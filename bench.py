@@ -614,6 +614,17 @@ def main():
             t_small = (time.perf_counter() - ts0) / small_calls
             small_info = shm.last_call_info()
             shm.barrier_all()
+            # the last small call's result on every element: at N > 1 these calls run the fused
+            # kernel, with its per-block acquires skipped when the init test allowed it
+            # (coherence_selftest.fused_acquires_skipped), so the driver's multi-GPU line pins
+            # that decision's correctness across GPUs
+            small_bad = 0
+            if not args.no_check:
+                import oracle
+                sidx = np.arange(small_n, dtype=np.uint64)
+                got_s = shm.get(dst, small_n, "double")
+                want_s = oracle.reduce_pe("sum", "double", [synth(p, sidx) for p in range(npes)], me)
+                small_bad = int((got_s.view(np.uint64) != want_s.view(np.uint64)).sum())
 
     # N = 1: the same calls with the opt-in persistent server (shmemx.h
     # shmemx_set_persistent): the identity copy served by a resident one-member
@@ -762,6 +773,9 @@ def main():
 
     if t_small is not None:
         t_small = max_over_pes(t_small)
+        small_check = "skipped" if args.no_check else \
+            "bit-exact vs the reference's per-PE order, every element, every PE" \
+            if int(max_over_pes(small_bad)) == 0 else "MISMATCH"
     rccl = None
     if npes > 1 and distinct_gpus and not args.no_rccl_compare and not args.host and not rccl_ok and not rccl_fallback:
         rccl = {"error": "RCCL did not come up (communicator within 60 s, or a probe allreduce) on every PE; "
@@ -1075,7 +1089,7 @@ def main():
             "cpu_baseline": cpu,
             "small_call": None if t_small is None else
             {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small * 1e6, 2), "calls": small_calls,
-             "schedule": small_info["schedule"], "kernel": small_info["kernel"],
+             "schedule": small_info["schedule"], "kernel": small_info["kernel"], "check": small_check,
              "note": "BASELINE config 5 shape: 4096 back-to-back 64 KiB shmem_double_sum_to_all calls, max over PEs"},
             "small_call_persistent": small_p_child if world > 1 else None if t_small_p is None else
             {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small_p * 1e6, 2), "calls": small_calls,

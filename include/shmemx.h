@@ -104,7 +104,10 @@ int shmemx_get_reduce_order (void);
  * and aborts every PE with a message naming the first field that differs
  * (the reference's debug build checks init and symmetry,
  * src/reduce/reduce-op.c:395-398, src/utils/utils.h:74-129). Costs two host
- * barriers per call. */
+ * barriers per call. The exchange runs on the host when the call is issued,
+ * so a stream-ordered call captured into a HIP graph is checked once, at
+ * capture time: its replays repeat the captured arguments and are not
+ * checked again. */
 
 /* Persistent fused server (opt-in; env SHMEM_PERSISTENT=1 sets it at init,
  * SHMEM_PERSISTENT_IDLE_US = how long it stays without a call, default 1000):

@@ -7,6 +7,9 @@
 #include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#include <atomic>
+#include <mutex>
 #include <type_traits>
 
 #include "mi355_reduce.h"
@@ -467,19 +470,28 @@ constexpr int kBlocksPerCU = 8;
 // The HBM-bound folds do not: capped at their residency (the 8-source fold
 // holds 152 VGPRs, 3 blocks per CU) they ran 1-4 % slower -- the queued
 // blocks refill CUs as others finish.
+// Several host threads may launch folds (the launch state is per thread):
+// readers see an entry only once its key and value are written (release /
+// acquire on `used`), writers append under a mutex.
 inline int resident_blocks(const void *fn) {
     static const void *keys[512];
     static int vals[512];
-    static int used = 0;
-    for (int i = 0; i < used; ++i)
+    static std::atomic<int> used{0};
+    static std::mutex mu;
+    const int seen = used.load(std::memory_order_acquire);
+    for (int i = 0; i < seen; ++i)
         if (keys[i] == fn) return vals[i];
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kBlock, 0) != hipSuccess || n < 1) n = 1;
     (void)hipGetLastError();
-    if (used < 512) {
-        keys[used] = fn;
-        vals[used] = n;
-        ++used;
+    std::lock_guard<std::mutex> lock(mu);
+    const int u = used.load(std::memory_order_relaxed);
+    for (int i = seen; i < u; ++i)
+        if (keys[i] == fn) return vals[i];  // another thread added it meanwhile
+    if (u < 512) {
+        keys[u] = fn;
+        vals[u] = n;
+        used.store(u + 1, std::memory_order_release);
     }
     return n;
 }

@@ -37,6 +37,7 @@ def run(cmd, timeout=240, env=None):
 
 
 def common(d, n):
+    assert "legs_s" in d and d["legs_s"]["total_before_print"] > 0, d.get("legs_s")
     assert d["metric"] == METRIC and d["unit"] == "GiB/s" and d["n_gpus"] == n
     assert d["value"] > 0 and d["ms_per_step"] > 0 and d["higher_is_better"] is True
     assert d["check"].startswith("bit-exact"), d["check"]
@@ -70,6 +71,10 @@ def test_bench_one_gpu_line():
     assert r["kernel"] == "void mi355k::copy_segments<4, 1>(mi355k::SegParams<1>)", r
     assert r["call"]["schedule"] == "identity" and r["alg_bytes_per_launch"] == 2 * (256 << 20), r
     assert d["coherence_selftest"] is None
+    # north_star's host-memory rate: page-locked host arrays, staged over PCIe in each call
+    hs = d["host_staged"]
+    assert hs["check"].startswith("bit-exact") and hs["value"] > 0 and 0.2 < hs["pcie_frac"] < 1.2, hs
+    assert hs["pcie"]["both_GB_s_each_direction"] > 0, hs
     k = d["kernels"]
     for name in ("fold_k2_double_sum", "fold_k8_double_sum", "rs_shard_n8_double_sum", "fold_k8_float_max",
                  "fold_k8_longlong_and", "rs_shard_n8_float_max"):
@@ -124,6 +129,16 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
     # the init coherence test ran on the real layout (here: one GPU) and passed
     c = d["coherence_selftest"]
     assert c["ran"] and c["passed"], c
+    # round 4: the caller's producer path (plain stores in a null-stream kernel), both orderings,
+    # all three ways of reading; the fused kernel skips its acquires only with fused_sysload
+    pp = c["producer_path"]
+    assert pp["ran"] and all(pp[k] for k in ("fused_sysload", "fused_after_acquire", "host_after_acquire")), pp
+    assert c["fused_acquires_skipped"] == (c["sysload_fresh"] and pp["fused_sysload"]), c
+    # the fused small calls' results, every element on every PE
+    assert d["small_call"]["check"].startswith("bit-exact"), d["small_call"]
+    # every leg's wall time, and no optional leg failed
+    assert d["legs_s"]["headline"] > 0 and d["legs_s"]["cpu_baseline"] > 0, d["legs_s"]
+    assert not any(isinstance(v, dict) and "error" in v and k != "rccl_compare" for k, v in d.items()), d
     # the same call on plain hipMalloc buffers: mapped by the peers, not staged
     e = d["external_buffers"]
     assert e["schedule"] == "mapped-p2p" and e["check"].startswith("bit-exact") and e["mappings_opened"] >= 1, e
