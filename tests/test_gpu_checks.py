@@ -80,19 +80,24 @@ def test_coherence_selftest_runs_and_passes():
         assert parse(out, "EXACT")[0] == ["True"] and parse(out, "SCHED")[0] == ["fused-twoshot"], out
 
 
-def test_stale_reread_falls_back_to_rccl():
-    """PE 1 reports its re-read after the acquire stale: every PE learns it at
-    init and runs the RCCL schedule (RCCL joins the two ranks on the one GPU
-    through its socket transport, NCCL_HOSTID per PE, as in
+@pytest.mark.parametrize("mode", ["stale", "producer"])
+def test_stale_reread_falls_back_to_rccl(mode):
+    """PE 1 reports its re-read after the acquire stale -- of the library's own
+    write-through marker (stale), or of a caller's plain-store words after the
+    multi-launch ordering (producer, round 4's producer-path test): every PE
+    learns it at init and runs the RCCL schedule (RCCL joins the two ranks on
+    the one GPU through its socket transport, NCCL_HOSTID per PE, as in
     test_gpu_multipe.test_rccl_schedule_multi_rank); a 2-PE double sum is
     a + b either way, so the result stays exact."""
     per_pe = {pe: {"NCCL_HOSTID": f"shmem-stale-test-pe{pe}"} for pe in range(2)}
-    rcs, outs, _ = spawn(2, COH, extra={"SHMEM_TEST_IPC_FAIL": "stale", "NCCL_SOCKET_IFNAME": "lo",
+    rcs, outs, _ = spawn(2, COH, extra={"SHMEM_TEST_IPC_FAIL": mode, "NCCL_SOCKET_IFNAME": "lo",
                                         "NCCL_IB_DISABLE": "1"}, per_pe=per_pe)
     for rc, out in zip(rcs, outs):
         assert rc == 0, out[-2000:]
         coh = parse(out, "COH")[0]
-        assert coh[:3] == ["1", "0", "1"] and coh[4] == "3", out  # ran, failed, stale; algorithm RCCL
+        # ran, failed, (stale marker), algorithm RCCL
+        assert coh[:2] == ["1", "0"] and coh[4] == "3", out
+        assert coh[2] == ("1" if mode == "stale" else "0"), out
         assert parse(out, "EXACT")[0] == ["True"] and parse(out, "SCHED")[0] == ["rccl"], out
     assert "init coherence test" in outs[0]
 
