@@ -460,6 +460,8 @@ def main():
     ap.add_argument("--host", action="store_true",
                     help="source/target in host memory (shmem_malloc, page-locked): the rate includes the "
                          "H2D/D2H staging copies (DESIGN.md); not the headline metric")
+    ap.add_argument("--no-threshold-sweep", action="store_true",
+                    help="N > 1: skip the fused / multi-launch and one-shot / two-shot per-size comparison")
     ap.add_argument("--no-host-staged", action="store_true",
                     help="N = 1: skip the host_staged leg (the same call on page-locked host arrays, with the "
                          "same run's PCIe ceiling)")
@@ -920,6 +922,65 @@ def main():
                 if b.value:
                     hip.hipFree(b)
 
+    # N > 1: where the fused one-launch kernel stops paying, on this layout --
+    # the same calls per message size with the fused path forced on (fused_max
+    # 1 GiB) and off (0, the multi-launch schedule), and one-shot vs two-shot
+    # inside the fused kernel: the data to set SHMEM_FUSED_MAX_BYTES /
+    # SHMEM_ONESHOT_MAX_BYTES from one GPU per PE (defaults 1 MiB / 64 KiB were
+    # set with the PEs sharing one GPU)
+    threshold_sweep = None
+    if npes > 1 and not args.host and not args.no_threshold_sweep and not rccl_fallback:
+        with timed_leg("threshold_sweep"):
+            import oracle
+            f0, o0 = shm.set_fused_max(1 << 30), shm.set_oneshot_max(64 << 10)
+            shm.set_fused_max(f0)
+            shm.set_oneshot_max(o0)
+
+            def per_call(nel, fused_max, oneshot_max, calls=200):
+                shm.set_fused_max(fused_max)
+                shm.set_oneshot_max(oneshot_max)
+                loop(dst, src, nel, 0, 0, npes, None, shm._psync_ptr, 10)
+                shm.barrier_all()
+                tq = time.perf_counter()
+                loop(dst, src, nel, 0, 0, npes, None, shm._psync_ptr, calls)
+                shm.sync()
+                t = max_over_pes((time.perf_counter() - tq) / calls)
+                sched = shm.last_call_info()["schedule"]
+                m = min(nel, 4096)
+                sidx = np.arange(m, dtype=np.uint64)
+                got = shm.get(dst, m, "double")
+                want = oracle.reduce_pe("sum", "double", [synth(p, sidx) for p in range(npes)], me)
+                bad = int(max_over_pes(int((got.view(np.uint64) != want.view(np.uint64)).sum())))
+                return round(t * 1e6, 2), sched, bad
+
+            shm.put(src, synth(me, np.arange(n, dtype=np.uint64)))  # the op-coverage leg rewrote src
+            rows, bad_total = [], 0
+            for nb in (64 << 10, 256 << 10, 1 << 20, 2 << 20, 4 << 20, 8 << 20):
+                fu, fs, b1 = per_call(nb // 8, 1 << 30, o0)
+                mu, ms, b2 = per_call(nb // 8, 0, o0)
+                bad_total += b1 + b2
+                rows.append({"bytes": nb, "fused_us": fu, "fused_schedule": fs, "multi_launch_us": mu,
+                             "multi_launch_schedule": ms})
+            oneshot = []
+            for nb in (16 << 10, 64 << 10, 256 << 10):
+                ou, osch, b1 = per_call(nb // 8, 1 << 30, 1 << 30)
+                tu, tsch, b2 = per_call(nb // 8, 1 << 30, 0)
+                bad_total += b1 + b2
+                oneshot.append({"bytes": nb, "oneshot_us": ou, "oneshot_schedule": osch, "twoshot_us": tu,
+                                "twoshot_schedule": tsch})
+            shm.set_fused_max(f0)
+            shm.set_oneshot_max(o0)
+            wins = [r["bytes"] for r in rows if r["fused_us"] < r["multi_launch_us"]]
+            threshold_sweep = {
+                "fused_vs_multi_launch": rows, "oneshot_vs_twoshot": oneshot,
+                "largest_size_fused_wins": max(wins) if wins else 0,
+                "defaults": {"fused_max": f0, "oneshot_max": o0},
+                "check": "bit-exact (first 4096 elements, every PE, every size and mode)" if bad_total == 0
+                else "MISMATCH in %d elements" % bad_total,
+                "note": "us per shmem_double_sum_to_all call (200 calls, max over PEs) with the fused path forced "
+                        "on (shmemx_set_fused_max_bytes(1 GiB)) and off (0: multi-launch), and inside the fused "
+                        "kernel one-shot vs two-shot (shmemx_set_oneshot_max_bytes)"}
+
     # N > 1: what one link carries alone -- PE 0 pulls 64 MiB from each peer's
     # heap with shmem_getmem (the copy kernel reading the peer mapping, as the
     # all-gather leg does) and pushes it back with shmem_putmem (the runtime's
@@ -1107,6 +1168,7 @@ def main():
             "fused_same_gpu": fused,
             "fused_same_gpu_persistent": fused_p,
             "host_staged": host_staged,
+            "threshold_sweep": threshold_sweep,
         }
         for name, err in leg_errors.items():   # optional legs that raised
             out[name] = {"error": err}

@@ -64,6 +64,15 @@ enum shmemx_reduce_algorithm {
 };
 int shmemx_set_reduce_algorithm (int algorithm); /* returns the previous one */
 int shmemx_get_reduce_algorithm (void);
+/* The schedule thresholds at run time (defaults: SHMEM_FUSED_MAX_BYTES = 1 MiB,
+ * SHMEM_ONESHOT_MAX_BYTES = 64 KiB): messages up to fused_max bytes per PE
+ * take the one-launch fused kernel (capped at 1 GiB; 0 = never), those up to
+ * oneshot_max of them its one-shot fold. Collective settings like the
+ * algorithm: every PE sets the same value between calls (SHMEM_DEBUG=1
+ * checks both per call). Return the previous value. A fused path that the
+ * init self-test turned off stays off. */
+size_t shmemx_set_fused_max_bytes (size_t bytes);
+size_t shmemx_set_oneshot_max_bytes (size_t bytes);
 
 /* Whose result the P2P schedules (and the stream-ordered calls) deliver
  * (env SHMEM_REDUCE_ORDER=reference|pe_start sets the default at init):

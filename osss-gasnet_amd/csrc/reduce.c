@@ -1027,6 +1027,8 @@ static void debug_check (const char *fn, int op, int dtype, const void *target, 
     }
     r.algorithm = shmemi.algorithm;
     r.order = shmemi.order;
+    r.fused_max = shmemi.fused_max;
+    r.oneshot_max = shmemi.oneshot_max;
     snprintf (r.fn, sizeof r.fn, "%s", fn);
     shmemi_debug_exchange (&r, PE_start, 1 << logPE_stride, PE_size);
 }

@@ -410,6 +410,8 @@ static const char *dbg_diff (const struct shmemi_dbg_rec *a, const struct shmemi
     F (algorithm, "reduce algorithm (shmemx_set_reduce_algorithm)")
     F (order, "result order (shmemx_set_reduce_order)")
     F (overlap, "target/source relation (0 disjoint, 1 the same buffer, 2 target overlapping above source, 3 below)")
+    F (fused_max, "fused-kernel threshold in bytes (SHMEM_FUSED_MAX_BYTES / shmemx_set_fused_max_bytes)")
+    F (oneshot_max, "one-shot threshold in bytes (SHMEM_ONESHOT_MAX_BYTES / shmemx_set_oneshot_max_bytes)")
 #undef F
     if (strcmp (a->fn, b->fn) != 0) {
         *va = *vb = 0;
@@ -1058,7 +1060,7 @@ static void interconnect_selftest (void)
         if (me == 0)
             fprintf (stderr, "[shmem] warning: a caller's plain stores were not visible to peers through the fused "
                              "kernel's flag ordering (init producer-path test); the fused kernel is disabled\n");
-        shmemi.fused_max = 0;
+        shmemi.fused_max = 0, shmemi.fused_off = 1;
     }
     if (all_mapped && !shmemi.coh_passed && me == 0)
         fprintf (stderr, "[shmem] warning: a peer heap re-read after a system-scope acquire returned stale data "
@@ -1067,7 +1069,7 @@ static void interconnect_selftest (void)
         if (me == 0)
             fprintf (stderr, "[shmem] warning: peer signal-region stores are not visible; "
                              "the fused small-message kernel is disabled\n");
-        shmemi.fused_max = 0;
+        shmemi.fused_max = 0, shmemi.fused_off = 1;
         shmemi.sig_broken = 1;
     }
     if (!all_heap) {
@@ -1076,7 +1078,7 @@ static void interconnect_selftest (void)
                              "using the RCCL schedule\n");
         shmemi.algorithm = SHMEMX_REDUCE_RCCL;
         shmemi.p2p_broken = 1;
-        shmemi.fused_max = 0; /* its kernels read the peers' heaps too: every PE takes the same path */
+        shmemi.fused_max = 0, shmemi.fused_off = 1; /* its kernels read the peers' heaps too: every PE takes the same path */
         shmemi.ext_map = 0;   /* peers' other allocations would be mapped the same way (extmap.c) */
     }
     shmemi_barrier_set (0, 1, np);
@@ -1577,6 +1579,31 @@ int shmemx_set_reduce_algorithm (int algorithm)
 }
 
 int shmemx_get_reduce_algorithm (void) { return shmemi.algorithm; }
+
+/* MI355X extensions (shmemx.h): the schedule thresholds at run time. Like
+ * the algorithm, every PE must set the same value (SHMEM_DEBUG checks it per
+ * call). A fused path a failed init self-test turned off stays off. */
+size_t shmemx_set_fused_max_bytes (size_t bytes)
+{
+    const size_t old = shmemi.fused_max;
+    if (bytes > ((size_t) 1 << 30)) /* 32-bit byte offsets in the fused folds (fused.hip ld16_sys_at) */
+        bytes = (size_t) 1 << 30;
+    if (shmemi.fused_off)
+        bytes = 0;
+    if (old != bytes && shmemi.initialized && shmemi.heap != NULL)
+        shmemi_server_stop (); /* a resident server serves fused calls only */
+    shmemi.fused_max = bytes;
+    return old;
+}
+
+size_t shmemx_set_oneshot_max_bytes (size_t bytes)
+{
+    const size_t old = shmemi.oneshot_max;
+    if (old != bytes && shmemi.initialized && shmemi.heap != NULL)
+        shmemi_server_stop (); /* a resident server keeps the one-shot choice it was started with */
+    shmemi.oneshot_max = bytes;
+    return old;
+}
 
 int shmemx_set_reduce_order (int order)
 {

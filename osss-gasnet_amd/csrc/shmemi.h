@@ -34,6 +34,7 @@ struct shmemi_dbg_rec {
     int32_t algorithm, order, persistent;
     int32_t overlap;            /* target vs source: 0 disjoint, 1 same, 2 overlapping above, 3 below */
     uint64_t toff, soff;        /* heap offsets (device heap kinds), else 0 */
+    uint64_t fused_max, oneshot_max; /* the schedule thresholds (shmemx_set_fused_max_bytes / _oneshot_) */
     char fn[48];
 };
 
@@ -149,6 +150,7 @@ struct shmemi_state {
     unsigned long long **peer_sig;  /* [npes] */
     size_t fused_max;           /* SHMEM_FUSED_MAX_BYTES: largest message on the fused path */
     size_t oneshot_max;         /* SHMEM_ONESHOT_MAX_BYTES: largest fused message folded one-shot */
+    int fused_off;              /* a failed self-test disabled the fused path: the setters keep it off */
     int sig_broken;             /* peers' signal-region stores failed the init self-test */
 
     /* completion signal: host-coherent word the last block of a kernel writes */

@@ -145,6 +145,18 @@ class Shmem:
         """"reference": every PE gets the reference's result for itself; "pe_start": PE_start's everywhere"""
         return self.lib.shmemx_set_reduce_order(ORDERS[name])
 
+    def set_fused_max(self, nbytes):
+        """fused-kernel threshold in bytes per PE (collective setting, shmemx.h); returns the previous"""
+        f = self.lib.shmemx_set_fused_max_bytes
+        f.argtypes, f.restype = [ctypes.c_size_t], ctypes.c_size_t
+        return int(f(nbytes))
+
+    def set_oneshot_max(self, nbytes):
+        """one-shot threshold in bytes per PE (collective setting, shmemx.h); returns the previous"""
+        f = self.lib.shmemx_set_oneshot_max_bytes
+        f.argtypes, f.restype = [ctypes.c_size_t], ctypes.c_size_t
+        return int(f(nbytes))
+
     def set_persistent(self, enable):
         """opt-in persistent fused server (shmemx.h); returns the previous setting"""
         return bool(self.lib.shmemx_set_persistent(1 if enable else 0))

@@ -88,6 +88,16 @@ def test_different_active_set(tmp_path):
     mismatch(tmp_path, 3, call, ["PE_size is 2 on PE 0 but 3 on PE 1", "PE_size is 3 on PE 1 but 2 on PE 0"])
 
 
+def test_different_fused_threshold(tmp_path):
+    """shmemx_set_fused_max_bytes is a collective setting: a PE that set another
+    threshold would take another schedule than its peers (round 4)."""
+    call = ("shm.set_fused_max(1 << 20 if me == 0 else 2 << 20)\n"
+            "    shm.to_all('sum', 'double', p, p, 0, 0, 0, npes)")
+    mismatch(tmp_path, 2, call, ["fused-kernel threshold in bytes (SHMEM_FUSED_MAX_BYTES / shmemx_set_fused_max_bytes) "
+                                 "is 1048576 on PE 0 but 2097152 on PE 1",
+                                 "is 2097152 on PE 1 but 1048576 on PE 0"])
+
+
 def test_different_stride(tmp_path):
     call = "shm.to_all('sum', 'double', p, p, 0, 0, 0 if me != 2 else 1, 2)\n    shm.barrier_all()"
     # PEs 0, 1 call over (0, 0, 2), a correct collective of theirs; PE 2 over

@@ -134,6 +134,13 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
     pp = c["producer_path"]
     assert pp["ran"] and all(pp[k] for k in ("fused_sysload", "fused_after_acquire", "host_after_acquire")), pp
     assert c["fused_acquires_skipped"] == (c["sysload_fresh"] and pp["fused_sysload"]), c
+    # fused vs multi-launch and one-shot vs two-shot per size, schedules as forced, results exact
+    ts = d["threshold_sweep"]
+    assert ts["check"].startswith("bit-exact") and len(ts["fused_vs_multi_launch"]) == 6, ts
+    for r in ts["fused_vs_multi_launch"]:
+        assert r["fused_schedule"].startswith("fused") and r["multi_launch_schedule"] == "p2p", r
+    for r in ts["oneshot_vs_twoshot"]:
+        assert r["oneshot_schedule"] == "fused-oneshot" and r["twoshot_schedule"] == "fused-twoshot", r
     # the fused small calls' results, every element on every PE
     assert d["small_call"]["check"].startswith("bit-exact"), d["small_call"]
     # every leg's wall time, and no optional leg failed
