@@ -944,8 +944,9 @@ def main():
                 tq = time.perf_counter()
                 loop(dst, src, nel, 0, 0, npes, None, shm._psync_ptr, calls)
                 shm.sync()
-                t = max_over_pes((time.perf_counter() - tq) / calls)
-                sched = shm.last_call_info()["schedule"]
+                t_loc = (time.perf_counter() - tq) / calls
+                sched = shm.last_call_info()["schedule"]   # before max_over_pes: its own call replaces it
+                t = max_over_pes(t_loc)
                 m = min(nel, 4096)
                 sidx = np.arange(m, dtype=np.uint64)
                 got = shm.get(dst, m, "double")
