@@ -64,7 +64,7 @@ enum shmemx_reduce_algorithm {
 };
 int shmemx_set_reduce_algorithm (int algorithm); /* returns the previous one */
 int shmemx_get_reduce_algorithm (void);
-/* The schedule thresholds at run time (defaults: SHMEM_FUSED_MAX_BYTES = 1 MiB,
+/* The schedule thresholds at run time (defaults: SHMEM_FUSED_MAX_BYTES = 2 MiB,
  * SHMEM_ONESHOT_MAX_BYTES = 64 KiB): messages up to fused_max bytes per PE
  * take the one-launch fused kernel (capped at 1 GiB; 0 = never), those up to
  * oneshot_max of them its one-shot fold. Collective settings like the

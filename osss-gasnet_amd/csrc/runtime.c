@@ -1348,7 +1348,7 @@ void pshmem_init (void)
     signal_init ();
     sigmem_init ();
     server_init ();
-    shmemi.fused_max = env_size ("SHMEM_FUSED_MAX_BYTES", (size_t) 1 << 20);
+    shmemi.fused_max = env_size ("SHMEM_FUSED_MAX_BYTES", (size_t) 2 << 20);
     /* the fused kernel's folds address a member's buffer with 32-bit byte
      * offsets (fused.hip ld16_sys_at) */
     if (shmemi.fused_max > ((size_t) 1 << 30))

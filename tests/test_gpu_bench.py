@@ -89,7 +89,7 @@ def test_bench_one_gpu_line():
     for leg in fp["legs"].values():
         assert leg["check"].startswith("bit-exact") and leg["us_per_call"] > 0, leg
     sp = d["small_call_persistent"]
-    assert sp["us_per_call"] > 0 and sp["served"] >= sp["calls"] - 2 and sp["servers_launched"] >= 1, sp
+    assert sp["us_per_call"] > 0 and sp["served"] >= sp["calls"] - 16 and sp["servers_launched"] >= 1, sp
 
 
 @pytest.mark.multipe
@@ -124,7 +124,9 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
     # the opt-in persistent server at N > 1 (a child job of one PE per rank)
     sp = d["small_call_persistent"]
     assert "error" not in sp, sp
-    assert sp["opt_in"] and sp["check"].startswith("bit-exact") and sp["served"] >= sp["calls"] - 2, sp
+    # (a host pause longer than SHMEM_PERSISTENT_IDLE_US lets a server idle out: the next call is launched and
+    # restarts it, so a few of the 4096 calls may be launched ones)
+    assert sp["opt_in"] and sp["check"].startswith("bit-exact") and sp["served"] >= sp["calls"] - 16, sp
     assert sp["schedule"] == "persistent" and "fused_server<0, double>" in sp["kernel"], sp
     # the init coherence test ran on the real layout (here: one GPU) and passed
     c = d["coherence_selftest"]
