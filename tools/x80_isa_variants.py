@@ -74,12 +74,34 @@ RULES = {
 }
 
 
+def kernel_lengths(lines):
+    """instructions per target kernel (for the slice rules)"""
+    n, inside, cur = {}, False, None
+    for ln in lines:
+        for k in KERNELS:
+            if ln.startswith(k + ":"):
+                inside, cur = True, k
+                n[k] = 0
+        if inside and (ln.startswith(".Lfunc_end") or "s_endpgm" in ln):
+            inside = False
+        elif inside and INSN.match(ln):
+            n[cur] += 1
+    return n
+
+
 def transform(lines, rule, nops):
-    out, inside, sites = [], False, 0
+    """rule: a RULES name, or slice/I/K: every instruction in the I-th of K equal slices of each
+    target kernel (by instruction count)"""
+    out, inside, sites, idx, cur = [], False, 0, 0, None
+    sl = None
+    if rule.startswith("slice/"):
+        _, i, k = rule.split("/")
+        sl, lens = (int(i), int(k)), kernel_lengths(lines)
     for ln in lines:
         out.append(ln)
         if any(ln.startswith(k + ":") for k in KERNELS):
-            inside = True
+            inside, idx = True, 0
+            cur = next(k for k in KERNELS if ln.startswith(k + ":"))
             continue
         if inside and (ln.startswith(".Lfunc_end") or "s_endpgm" in ln):
             inside = False
@@ -90,7 +112,13 @@ def transform(lines, rule, nops):
         if m is None:
             continue
         op, ops = m.group(1), operands(m.group(2))
-        if RULES[rule](op, ops):
+        idx += 1
+        if sl is not None:
+            n = lens[cur]
+            hit = sl[0] * n // sl[1] <= idx - 1 < (sl[0] + 1) * n // sl[1] and not op.startswith(NO_NOP_AFTER)
+        else:
+            hit = RULES[rule](op, ops)
+        if hit:
             out.append("\ts_nop %d\n" % nops)
             sites += 1
     return out, sites
@@ -105,7 +133,7 @@ def main():
         rule, _, n = spec.partition(":")
         nops = int(n) if n else 4
         var, sites = transform(lines, rule, nops)
-        base = os.path.join(outdir, "general_%s%s" % (rule, "_%d" % nops if n else ""))
+        base = os.path.join(outdir, "general_%s%s" % (rule.replace("/", "-"), "_%d" % nops if n else ""))
         open(base + ".s", "w").writelines(var)
         subprocess.check_call([LLVM + "/clang", "-x", "assembler", "-target", "amdgcn-amd-amdhsa", "-mcpu=gfx950",
                                "-c", base + ".s", "-o", base + ".o"])
