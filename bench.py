@@ -460,6 +460,8 @@ def main():
     ap.add_argument("--host", action="store_true",
                     help="source/target in host memory (shmem_malloc, page-locked): the rate includes the "
                          "H2D/D2H staging copies (DESIGN.md); not the headline metric")
+    ap.add_argument("--no-collectives", action="store_true",
+                    help="N > 1: skip the shmem_broadcast64 / shmem_fcollect64 leg")
     ap.add_argument("--no-threshold-sweep", action="store_true",
                     help="N > 1: skip the fused / multi-launch and one-shot / two-shot per-size comparison")
     ap.add_argument("--no-host-staged", action="store_true",
@@ -1030,6 +1032,57 @@ def main():
                                       + ("; the PEs share ONE GPU here: local HBM copies, not link rates"
                                          if shared_gpu else "")}
 
+    # N > 1: the data-movement collectives beside the reduction (SURVEY 8f row 4,
+    # coll.c): shmem_broadcast64 from PE 0 and shmem_fcollect64, 64 KiB (one
+    # fused_pull launch) and 4 MiB per PE (copy kernels / peer copies), each
+    # checked bit-exact on every PE
+    collectives = None
+    if npes > 1 and not args.host and not args.no_collectives:
+        with timed_leg("collectives"):
+            import ctypes
+            vp, sz, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+            bc, fc = shm.lib.shmem_broadcast64, shm.lib.shmem_fcollect64
+            bc.argtypes, bc.restype = [vp, vp, sz, ci, ci, ci, ci, vp], None
+            fc.argtypes, fc.restype = [vp, vp, sz, ci, ci, ci, vp], None
+            collectives, bad_total = {}, 0
+            for nb in (64 << 10, 4 << 20):
+                nw = nb // 8
+                csrc, cdst = shm.malloc_device(nb), shm.malloc_device(npes * nb)
+                if not csrc or not cdst:
+                    raise RuntimeError("shmemx_malloc_device for the collectives leg failed")
+                mine_w = synth(me, np.arange(nw, dtype=np.uint64)).view(np.int64)
+                shm.put(csrc, mine_w)
+                rec = {}
+                for name, call, moved in (
+                        ("broadcast64", lambda: bc(cdst, csrc, nw, 0, 0, 0, npes, shm._psync_ptr), nb),
+                        ("fcollect64", lambda: fc(cdst, csrc, nw, 0, 0, npes, shm._psync_ptr), npes * nb)):
+                    reps = 20
+                    call()
+                    shm.barrier_all()
+                    tq = time.perf_counter()
+                    for _ in range(reps):
+                        call()
+                    shm.sync()
+                    t_loc = (time.perf_counter() - tq) / reps
+                    if name == "broadcast64":   # PE 0's target is not written (OpenSHMEM broadcast)
+                        want = synth(0, np.arange(nw, dtype=np.uint64)).view(np.int64) if me != 0 else None
+                        got = shm.get(cdst, nw, "longlong") if me != 0 else None
+                    else:
+                        want = np.concatenate([synth(p, np.arange(nw, dtype=np.uint64)).view(np.int64)
+                                               for p in range(npes)])
+                        got = shm.get(cdst, npes * nw, "longlong")
+                    bad = 0 if want is None else int((got != want).sum())
+                    bad_total += int(max_over_pes(bad))
+                    t = max_over_pes(t_loc)
+                    rec[name] = {"us_per_call": round(t * 1e6, 2), "GB_s_into_each_pe": round(moved / t / 1e9, 1)}
+                collectives[str(nb)] = rec
+                shm.barrier_all()
+                shm.free_device(cdst)
+                shm.free_device(csrc)
+            collectives["check"] = "bit-exact on every PE" if bad_total == 0 else "MISMATCH in %d words" % bad_total
+            collectives["note"] = ("shmem_broadcast64 (root PE 0) and shmem_fcollect64 over the whole job, 20 blocking "
+                                   "calls per size, max over PEs; GB/s = bytes landing in each PE's target / time")
+
     # dominant kernel and its algorithmic bytes per launch, from the schedule
     # the library reports for the timed calls (shmemx_last_call_info)
     launches = max(1, info["launches"])
@@ -1170,6 +1223,7 @@ def main():
             "fused_same_gpu_persistent": fused_p,
             "host_staged": host_staged,
             "threshold_sweep": threshold_sweep,
+            "collectives": collectives,
         }
         for name, err in leg_errors.items():   # optional legs that raised
             out[name] = {"error": err}

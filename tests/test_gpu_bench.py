@@ -143,6 +143,9 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
         assert r["fused_schedule"].startswith("fused") and r["multi_launch_schedule"] == "p2p", r
     for r in ts["oneshot_vs_twoshot"]:
         assert r["oneshot_schedule"] == "fused-oneshot" and r["twoshot_schedule"] == "fused-twoshot", r
+    # broadcast / fcollect beside the reduction
+    co = d["collectives"]
+    assert co["check"] == "bit-exact on every PE" and co[str(4 << 20)]["fcollect64"]["GB_s_into_each_pe"] > 0, co
     # the fused small calls' results, every element on every PE
     assert d["small_call"]["check"].startswith("bit-exact"), d["small_call"]
     # every leg's wall time, and no optional leg failed
