@@ -602,6 +602,12 @@ def main():
     shm.kernel_timing(False)
     # what the library ran for these calls: schedule, dominant kernel, bytes
     info = shm.last_call_info()
+    # the per-call distribution (SURVEY 8d asks for the median over the timed
+    # reps): the same K calls once more, each timed alone, outside the region
+    # that yields `value`
+    call_times = shmem_reduce.bench_call_times()
+    shm.barrier_all()
+    t_calls = call_times(dst, src, n, 0, 0, npes, shm._psync_ptr, args.steps)
     legs_s["headline"] = round(time.perf_counter() - t_head0, 2)
 
     # the many-small-bucket regime (BASELINE config 5 shape: 64 KiB per call)
@@ -618,6 +624,7 @@ def main():
             t_small = (time.perf_counter() - ts0) / small_calls
             small_info = shm.last_call_info()
             shm.barrier_all()
+            t_small_calls = call_times(dst, src, small_n, 0, 0, npes, shm._psync_ptr, small_calls)
             # the last small call's result on every element: at N > 1 these calls run the fused
             # kernel, with its per-block acquires skipped when the init test allowed it
             # (coherence_selftest.fused_acquires_skipped), so the driver's multi-GPU line pins
@@ -768,6 +775,12 @@ def main():
 
     t_check0 = time.perf_counter()
     t_step = max_over_pes(t_local) / args.steps
+    per_call = {"median_us": round(max_over_pes(float(np.median(t_calls))), 2),
+                "p10_us": round(max_over_pes(float(np.percentile(t_calls, 10))), 2),
+                "p90_us": round(max_over_pes(float(np.percentile(t_calls, 90))), 2),
+                "max_us": round(max_over_pes(float(t_calls.max())), 2), "calls": int(len(t_calls)),
+                "note": "the headline call timed one by one (CLOCK_MONOTONIC around each blocking call, a separate "
+                        "run of K calls); each statistic is the max over PEs of that PE's statistic"}
     if small_graph is not None:
         t_sg = max_over_pes(small_graph.pop("t_local"))
         bad = small_graph.pop("bad")
@@ -777,6 +790,8 @@ def main():
 
     if t_small is not None:
         t_small = max_over_pes(t_small)
+        small_dist = {"median_us": round(max_over_pes(float(np.median(t_small_calls))), 2),
+                      "p99_us": round(max_over_pes(float(np.percentile(t_small_calls, 99))), 2)}
         small_check = "skipped" if args.no_check else \
             "bit-exact vs the reference's per-PE order, every element, every PE" \
             if int(max_over_pes(small_bad)) == 0 else "MISMATCH"
@@ -1198,6 +1213,7 @@ def main():
                        "algorithm": "rccl (fallback: P2P self-test failed)" if rccl_fallback else args.algorithm,
                        "parallelism": f"pe{npes}"},
             "per_pe_gib_s": round(S / t_step / GIB, 2),
+            "per_call": per_call,
             "roofline": roofline,
             "xgmi": xgmi,
             "rccl_compare": rccl,
@@ -1205,6 +1221,7 @@ def main():
             "small_call": None if t_small is None else
             {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small * 1e6, 2), "calls": small_calls,
              "schedule": small_info["schedule"], "kernel": small_info["kernel"], "check": small_check,
+             "per_call": small_dist,
              "note": "BASELINE config 5 shape: 4096 back-to-back 64 KiB shmem_double_sum_to_all calls, max over PEs"},
             "small_call_persistent": small_p_child if world > 1 else None if t_small_p is None else
             {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small_p * 1e6, 2), "calls": small_calls,

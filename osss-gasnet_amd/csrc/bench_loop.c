@@ -9,7 +9,9 @@
  * The caller (bench.py) still brackets the loop with shmem_barrier_all and a
  * device synchronize on both sides and takes its own wall clock around it.
  */
+#define _POSIX_C_SOURCE 199309L /* clock_gettime under -std=c11 */
 #include <stddef.h>
+#include <time.h>
 
 #include <shmem.h>
 
@@ -20,6 +22,23 @@ void shmemb_double_sum_loop (double *target, double *source, int nreduce, int PE
 {
     for (int i = 0; i < iters; ++i)
         shmem_double_sum_to_all (target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync);
+}
+
+/* The same calls, each timed on its own (CLOCK_MONOTONIC, entry to return):
+ * us[i] = call i's duration in microseconds. For the distribution (median,
+ * tails) beside the bracketed mean of the loop above (median over
+ * the timed reps); a separate run, so the clock reads stay out of the
+ * headline's timed region. */
+void shmemb_double_sum_times (double *target, double *source, int nreduce, int PE_start, int logPE_stride,
+                              int PE_size, double *pWrk, long *pSync, int iters, double *us)
+{
+    struct timespec t0, t1;
+    for (int i = 0; i < iters; ++i) {
+        clock_gettime (CLOCK_MONOTONIC, &t0);
+        shmem_double_sum_to_all (target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync);
+        clock_gettime (CLOCK_MONOTONIC, &t1);
+        us[i] = (double) (t1.tv_sec - t0.tv_sec) * 1e6 + (double) (t1.tv_nsec - t0.tv_nsec) * 1e-3;
+    }
 }
 
 /* BASELINE config 4's op-coverage pair, same shape of loop */

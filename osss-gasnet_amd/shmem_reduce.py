@@ -368,6 +368,24 @@ def bench_loop(path=BENCH_LIB_PATH, name="double_sum"):
     return f
 
 
+def bench_call_times(path=BENCH_LIB_PATH):
+    """csrc/bench_loop.c shmemb_double_sum_times: K shmem_double_sum_to_all
+    calls, each timed alone; returns f(target, source, nreduce, PE_start,
+    logPE_stride, PE_size, k) -> numpy array of k durations in us"""
+    import numpy as np
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    f = ctypes.CDLL(path).shmemb_double_sum_times
+    f.argtypes = [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _vp]
+    f.restype = None
+
+    def run(target, source, nreduce, pe_start, log_stride, pe_size, psync, k):
+        out = np.zeros(k)
+        f(target, source, nreduce, pe_start, log_stride, pe_size, None, psync, k, out.ctypes.data)
+        return out
+    return run
+
+
 def kernel_code_hash(path=LIB_PATH):
     """sha256 (16 hex digits) of the gfx950 code objects the library carries
     (its .hip_fatbin ELF section): the machine code PMC counter profiles

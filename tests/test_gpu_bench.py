@@ -38,6 +38,9 @@ def run(cmd, timeout=240, env=None):
 
 def common(d, n):
     assert "legs_s" in d and d["legs_s"]["total_before_print"] > 0, d.get("legs_s")
+    pc = d["per_call"]
+    assert 0 < pc["p10_us"] <= pc["median_us"] <= pc["p90_us"] <= pc["max_us"] and pc["calls"] == d["steps"], pc
+    assert d["small_call"]["per_call"]["median_us"] > 0, d["small_call"]
     assert d["metric"] == METRIC and d["unit"] == "GiB/s" and d["n_gpus"] == n
     assert d["value"] > 0 and d["ms_per_step"] > 0 and d["higher_is_better"] is True
     assert d["check"].startswith("bit-exact"), d["check"]
