@@ -775,7 +775,7 @@ def main():
 
     t_check0 = time.perf_counter()
     t_step = max_over_pes(t_local) / args.steps
-    per_call = {"median_us": round(max_over_pes(float(np.median(t_calls))), 2),
+    call_dist = {"median_us": round(max_over_pes(float(np.median(t_calls))), 2),
                 "p10_us": round(max_over_pes(float(np.percentile(t_calls, 10))), 2),
                 "p90_us": round(max_over_pes(float(np.percentile(t_calls, 90))), 2),
                 "max_us": round(max_over_pes(float(t_calls.max())), 2), "calls": int(len(t_calls)),
@@ -1213,7 +1213,7 @@ def main():
                        "algorithm": "rccl (fallback: P2P self-test failed)" if rccl_fallback else args.algorithm,
                        "parallelism": f"pe{npes}"},
             "per_pe_gib_s": round(S / t_step / GIB, 2),
-            "per_call": per_call,
+            "per_call": call_dist,
             "roofline": roofline,
             "xgmi": xgmi,
             "rccl_compare": rccl,
