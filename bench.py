@@ -949,9 +949,7 @@ def main():
     if npes > 1 and not args.host and not args.no_threshold_sweep and not rccl_fallback:
         with timed_leg("threshold_sweep"):
             import oracle
-            f0, o0 = shm.set_fused_max(1 << 30), shm.set_oneshot_max(64 << 10)
-            shm.set_fused_max(f0)
-            shm.set_oneshot_max(o0)
+            f0, o0 = shm.thresholds()
 
             def per_call(nel, fused_max, oneshot_max, calls=200):
                 shm.set_fused_max(fused_max)

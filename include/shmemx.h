@@ -73,6 +73,8 @@ int shmemx_get_reduce_algorithm (void);
  * init self-test turned off stays off. */
 size_t shmemx_set_fused_max_bytes (size_t bytes);
 size_t shmemx_set_oneshot_max_bytes (size_t bytes);
+size_t shmemx_get_fused_max_bytes (void);
+size_t shmemx_get_oneshot_max_bytes (void);
 
 /* Whose result the P2P schedules (and the stream-ordered calls) deliver
  * (env SHMEM_REDUCE_ORDER=reference|pe_start sets the default at init):

@@ -1596,6 +1596,9 @@ size_t shmemx_set_fused_max_bytes (size_t bytes)
     return old;
 }
 
+size_t shmemx_get_fused_max_bytes (void) { return shmemi.fused_max; }
+size_t shmemx_get_oneshot_max_bytes (void) { return shmemi.oneshot_max; }
+
 size_t shmemx_set_oneshot_max_bytes (size_t bytes)
 {
     const size_t old = shmemi.oneshot_max;

@@ -151,6 +151,12 @@ class Shmem:
         f.argtypes, f.restype = [ctypes.c_size_t], ctypes.c_size_t
         return int(f(nbytes))
 
+    def thresholds(self):
+        """(fused_max, oneshot_max) in bytes per PE (shmemx.h)"""
+        for name in ("shmemx_get_fused_max_bytes", "shmemx_get_oneshot_max_bytes"):
+            getattr(self.lib, name).restype = ctypes.c_size_t
+        return int(self.lib.shmemx_get_fused_max_bytes()), int(self.lib.shmemx_get_oneshot_max_bytes())
+
     def set_oneshot_max(self, nbytes):
         """one-shot threshold in bytes per PE (collective setting, shmemx.h); returns the previous"""
         f = self.lib.shmemx_set_oneshot_max_bytes
