@@ -239,6 +239,46 @@ def persistent_child(rank, world, calls):
     return leg
 
 
+def extra_legs_child(rank, world, mib, steps, algorithm, flags):
+    """N > 1: external_buffers, link_probe and collectives, run by one child PE
+    process per rank on the rank's own GPU (tools/extra_legs.py), started
+    before this process touches the GPU, like persistent_child: none of them
+    had run with one GPU per PE before the driver's 8-GPU node, and a fatal
+    error in one (the library aborts the PE) or a hang would otherwise end
+    this rank before the headline line is printed. Returns rank 0's records,
+    or {"error": ...} under each leg's name."""
+    import subprocess
+    names = [k for k, f in (("external_buffers", "--no-external"), ("link_probe", "--no-link-probe"),
+                            ("collectives", "--no-collectives")) if f not in flags]
+    if not names:
+        return {}
+    job = "xl%s-%d" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
+    env = dict(os.environ, SHMEM_PE=str(rank), SHMEM_NPES=str(world), SHMEM_JOB_ID=job,
+               SHMEM_DEVICE=os.environ.get("LOCAL_RANK", str(rank)), SHMEM_BARRIER_TIMEOUT="60")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "SHMEM_DEVICE_HEAP_SIZE", "SHMEM_DEVICE_SCRATCH_SIZE"):
+        env.pop(k, None)
+    script = os.path.join(ROOT, "tools", "extra_legs.py")
+    p = subprocess.Popen([sys.executable, script, str(mib), str(steps), algorithm, *flags], env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+
+    def failed(msg):
+        return {k: {"error": msg} for k in names}
+    try:
+        out, err = p.communicate(timeout=240)
+    except subprocess.TimeoutExpired:
+        p.kill()
+        p.communicate()
+        return failed("child job timed out after 240 s")
+    if p.returncode != 0:
+        return failed(f"child job: PE {rank} rc {p.returncode}: {err[-400:]}")
+    if rank != 0:
+        return {}
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    if not lines:
+        return failed("child job: no result line from PE 0")
+    return json.loads(lines[-1])
+
+
 def host_staged_leg(shm, loop, S, me, npes, k, check):
     """north_star's second rate: the symmetric-heap buffers in HOST memory, as
     the reference's heap is (symmem.c:212-236, comms-inline.h:797-807):
@@ -500,6 +540,14 @@ def main():
     if world > 1 and not args.no_small and not args.host:
         with timed_leg("small_call_persistent"):
             small_p_child = persistent_child(rank, world, 4096)
+    # N > 1: the legs never run with one GPU per PE before, in a child job too
+    extra = {}
+    if world > 1 and not args.host:
+        with timed_leg("extra_legs_child"):
+            extra = extra_legs_child(rank, world, args.mib, args.steps, args.algorithm,
+                                     [f for f, on in (("--no-check", args.no_check), ("--no-external", args.no_external),
+                                                      ("--no-link-probe", args.no_link_probe),
+                                                      ("--no-collectives", args.no_collectives)) if on])
     # CPU baseline, before this process initialises the GPU; at N > 1 the
     # other ranks wait for rank 0 in the bootstrap (SHMEM_BARRIER_TIMEOUT)
     cpu = None
@@ -522,8 +570,8 @@ def main():
     # library's diagnostic (the library default, 600 s, suits long jobs)
     os.environ.setdefault("SHMEM_BARRIER_TIMEOUT", "120")
     # N > 1: ranks 1.. wait at init for rank 0, which first times the CPU
-    # baseline (and, like every rank, waits for its persistent-leg child, at
-    # most 240 s): the bootstrap wait covers both
+    # baseline (and, like every rank, waits for its two child jobs, at most
+    # 240 s each): the bootstrap wait covers both
     os.environ.setdefault("SHMEM_BOOTSTRAP_TIMEOUT", "600")
     shm = shmem_reduce.Shmem()
     shm.init()
@@ -896,48 +944,17 @@ def main():
                            "64 MiB per PE, GiB/s reduced whole job; longlong words with bits 1 at p = 7/8")
 
     # N > 1: the same call on plain hipMalloc buffers (a framework's tensors,
-    # outside the symmetric heap): the members map each other's allocations
-    # for the call (csrc/extmap.c) instead of staging them through scratch
-    with timed_leg("external_buffers"):
-        external = None
-        if npes > 1 and not args.host and not args.no_external and not rccl_fallback:
-            import ctypes
-            hip = ctypes.CDLL("libamdhip64.so")
-            bufs = [ctypes.c_void_p(), ctypes.c_void_p()]
-            if all(hip.hipMalloc(ctypes.byref(b), ctypes.c_size_t(S)) == 0 for b in bufs):
-                esrc, edst = bufs[0].value, bufs[1].value
-                shm.put(esrc, synth(me, np.arange(n, dtype=np.uint64)))  # the op-coverage leg rewrote src
-                k = max(5, args.steps // 4)
-                loop(edst, esrc, n, 0, 0, npes, None, shm._psync_ptr, 3)
-                shm.barrier_all()
-                shm.sync()
-                te0 = time.perf_counter()
-                loop(edst, esrc, n, 0, 0, npes, None, shm._psync_ptr, k)
-                shm.sync()
-                t_ext_local = time.perf_counter() - te0
-                einfo = shm.last_call_info()   # before max_over_pes: its own call replaces it
-                t_ext = max_over_pes(t_ext_local) / k
-                ck = "skipped"
-                if not args.no_check:
-                    import oracle
-                    idx = np.unique(np.random.default_rng(50 + me).integers(0, n, 1 << 14)).astype(np.uint64)
-                    got = shm.get(edst, n, "double")[idx.astype(np.int64)]
-                    want = oracle.reduce_pe("sum", "double", [synth(p, idx) for p in range(npes)], me)
-                    bad = int(max_over_pes(int((got.view(np.uint64) != want.view(np.uint64)).sum())))
-                    ck = "bit-exact, %d samples" % len(idx) if bad == 0 else "MISMATCH %d samples" % bad
-                shm.barrier_all()
-                mapped, opened, closed = shm.external_map_stats()
-                external = {"bytes_per_pe": S, "steps": k, "us_per_call": round(t_ext * 1e6, 2),
-                            "value": round(npes * S / t_ext / GIB, 2), "over_heap_buffers": round(t_ext / t_step, 3),
-                            "schedule": einfo["schedule"], "mappings_opened": opened, "check": ck,
-                            "note": "the headline call on plain hipMalloc buffers (outside the symmetric heap): "
-                                    "the members map each other's allocations for the call (IPC, cached) instead "
-                                    "of staging them through scratch (SHMEM_EXTERNAL_MAP)"}
-            else:
-                external = {"error": "hipMalloc of the two buffers failed"}
-            for b in bufs:
-                if b.value:
-                    hip.hipFree(b)
+    # outside the symmetric heap: the members map each other's allocations for
+    # the call, csrc/extmap.c), PE 0's one-peer-at-a-time link rates and the
+    # broadcast / fcollect collectives -- measured in the child job before
+    # this process touched the GPU (extra_legs_child); their records here
+    external = extra.get("external_buffers")
+    if external and "us_per_call" in external:
+        external["over_heap_buffers"] = round(external["us_per_call"] * 1e-6 / t_step, 3)
+    link_probe = extra.get("link_probe")
+    if link_probe and shared_gpu and "note" in link_probe:
+        link_probe["note"] += "; the PEs share ONE GPU here: local HBM copies, not link rates"
+    collectives = extra.get("collectives")
 
     # N > 1: where the fused one-launch kernel stops paying, on this layout --
     # the same calls per message size with the fused path forced on (fused_max
@@ -996,105 +1013,6 @@ def main():
                 "note": "us per shmem_double_sum_to_all call (200 calls, max over PEs) with the fused path forced "
                         "on (shmemx_set_fused_max_bytes(1 GiB)) and off (0: multi-launch), and inside the fused "
                         "kernel one-shot vs two-shot (shmemx_set_oneshot_max_bytes)"}
-
-    # N > 1: what one link carries alone -- PE 0 pulls 64 MiB from each peer's
-    # heap with shmem_getmem (the copy kernel reading the peer mapping, as the
-    # all-gather leg does) and pushes it back with shmem_putmem (the runtime's
-    # P2P copy), one peer at a time, the others waiting in a barrier. Beside
-    # xgmi.ag_kernel_remote_read_GB_s (all peers at once) it says whether the
-    # schedule is bound by the links or by how it drives them.
-    with timed_leg("link_probe"):
-        link_probe = None
-        if npes > 1 and not args.host and not args.no_link_probe:
-            import ctypes
-            # two 16 MiB buffers fit the heap's 64 MiB beside the headline's
-            nbp, reps = min(S, 16 << 20), 10
-            psym, ploc = shm.malloc_device(nbp), shm.malloc_device(nbp)
-            if not psym or not ploc:
-                raise SystemExit("link probe: shmemx_malloc_device of 2 x %d bytes failed" % nbp)
-            shm.put(psym, synth(me, np.arange(nbp // 8, dtype=np.uint64)))
-            shm.barrier_all()
-            get, put = shm.lib.shmem_getmem, shm.lib.shmem_putmem
-            for f in (get, put):
-                f.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-                f.restype = None
-            peers = {}
-            if me == 0:
-                for q in range(1, npes):
-                    rec = {}
-                    for name, f, a, b in (("get_GB_s", get, ploc, psym), ("put_GB_s", put, psym, ploc)):
-                        f(a, b, nbp, q)
-                        tq0 = time.perf_counter()
-                        for _ in range(reps):
-                            f(a, b, nbp, q)
-                        shm.sync()
-                        rec[name] = round(nbp * reps / (time.perf_counter() - tq0) / 1e9, 1)
-                    peers[str(q)] = rec
-                ok = True
-                if not args.no_check:   # the last get brought PE npes-1's bytes
-                    got = shm.get(ploc, 1 << 16, "double").view(np.uint64)
-                    ok = bool((got == synth(npes - 1, np.arange(1 << 16, dtype=np.uint64)).view(np.uint64)).all())
-            shm.barrier_all()
-            shm.free_device(ploc)
-            shm.free_device(psym)
-            if me == 0:
-                link_probe = {"bytes": nbp, "reps": reps, "from_pe0": peers,
-                              "check": "skipped" if args.no_check else "bit-exact" if ok else "MISMATCH",
-                              "note": "PE 0 alone, one peer at a time: shmem_getmem (copy kernel pulling over the "
-                                      "peer mapping) and shmem_putmem (HIP P2P copy) of 16 MiB, blocking calls"
-                                      + ("; the PEs share ONE GPU here: local HBM copies, not link rates"
-                                         if shared_gpu else "")}
-
-    # N > 1: the data-movement collectives beside the reduction (SURVEY 8f row 4,
-    # coll.c): shmem_broadcast64 from PE 0 and shmem_fcollect64, 64 KiB (one
-    # fused_pull launch) and 4 MiB per PE (copy kernels / peer copies), each
-    # checked bit-exact on every PE
-    collectives = None
-    if npes > 1 and not args.host and not args.no_collectives:
-        with timed_leg("collectives"):
-            import ctypes
-            vp, sz, ci = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
-            bc, fc = shm.lib.shmem_broadcast64, shm.lib.shmem_fcollect64
-            bc.argtypes, bc.restype = [vp, vp, sz, ci, ci, ci, ci, vp], None
-            fc.argtypes, fc.restype = [vp, vp, sz, ci, ci, ci, vp], None
-            collectives, bad_total = {}, 0
-            for nb in (64 << 10, 4 << 20):
-                nw = nb // 8
-                csrc, cdst = shm.malloc_device(nb), shm.malloc_device(npes * nb)
-                if not csrc or not cdst:
-                    raise RuntimeError("shmemx_malloc_device for the collectives leg failed")
-                mine_w = synth(me, np.arange(nw, dtype=np.uint64)).view(np.int64)
-                shm.put(csrc, mine_w)
-                rec = {}
-                for name, call, moved in (
-                        ("broadcast64", lambda: bc(cdst, csrc, nw, 0, 0, 0, npes, shm._psync_ptr), nb),
-                        ("fcollect64", lambda: fc(cdst, csrc, nw, 0, 0, npes, shm._psync_ptr), npes * nb)):
-                    reps = 20
-                    call()
-                    shm.barrier_all()
-                    tq = time.perf_counter()
-                    for _ in range(reps):
-                        call()
-                    shm.sync()
-                    t_loc = (time.perf_counter() - tq) / reps
-                    if name == "broadcast64":   # PE 0's target is not written (OpenSHMEM broadcast)
-                        want = synth(0, np.arange(nw, dtype=np.uint64)).view(np.int64) if me != 0 else None
-                        got = shm.get(cdst, nw, "longlong") if me != 0 else None
-                    else:
-                        want = np.concatenate([synth(p, np.arange(nw, dtype=np.uint64)).view(np.int64)
-                                               for p in range(npes)])
-                        got = shm.get(cdst, npes * nw, "longlong")
-                    bad = 0 if want is None else int((got != want).sum())
-                    bad_total += int(max_over_pes(bad))
-                    t = max_over_pes(t_loc)
-                    rec[name] = {"us_per_call": round(t * 1e6, 2), "GB_s_into_each_pe": round(moved / t / 1e9, 1)}
-                collectives[str(nb)] = rec
-                shm.barrier_all()
-                shm.free_device(cdst)
-                shm.free_device(csrc)
-            collectives["check"] = "bit-exact on every PE" if bad_total == 0 else "MISMATCH in %d words" % bad_total
-            collectives["note"] = ("shmem_broadcast64 (root PE 0) and shmem_fcollect64 over the whole job, 20 blocking "
-                                   "calls per size, max over PEs; GB/s = bytes landing in each PE's target / time")
 
     # dominant kernel and its algorithmic bytes per launch, from the schedule
     # the library reports for the timed calls (shmemx_last_call_info)

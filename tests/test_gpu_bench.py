@@ -157,6 +157,10 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
     # the same call on plain hipMalloc buffers: mapped by the peers, not staged
     e = d["external_buffers"]
     assert e["schedule"] == "mapped-p2p" and e["check"].startswith("bit-exact") and e["mappings_opened"] >= 1, e
+    assert e["fallbacks"] == 0 and e["over_heap_buffers"] > 0, e
     # PE 0's one-peer-at-a-time get/put rates (local HBM copies on this layout)
     lp = d["link_probe"]
     assert lp["check"] == "bit-exact" and lp["from_pe0"]["1"]["get_GB_s"] > 0 and lp["from_pe0"]["1"]["put_GB_s"] > 0, lp
+    assert "share ONE GPU" in lp["note"], lp
+    # those three legs ran in the child job (tools/extra_legs.py), before the rank touched the GPU
+    assert d["legs_s"]["extra_legs_child"] > 0, d["legs_s"]
