@@ -15,6 +15,21 @@
 #include "mi355_reduce.h"
 #include "ops.h"
 
+// Long double every-member fold, build-time forms measured against each other
+// (tools/build_x80_variants.sh): chains kept one after the other by an empty
+// asm dependence, each member's output stored as soon as its chain ends
+// instead of after the wave vote, and an occupancy floor (waves per SIMD) for
+// the orders kernels.
+#ifndef MI355_X80_SERIAL_CHAINS
+#define MI355_X80_SERIAL_CHAINS 1
+#endif
+#ifndef MI355_X80_EARLY_STORE
+#define MI355_X80_EARLY_STORE 1
+#endif
+#ifndef MI355_X80_WAVES
+#define MI355_X80_WAVES 0
+#endif
+
 namespace mi355k {
 
 using namespace mi355;
@@ -255,20 +270,42 @@ __device__ __forceinline__ void x80_orders_vector(const OrdersParams &p, uint64_
             continue;
         }
         x80d::xu a = u[q];
+#if MI355_X80_SERIAL_CHAINS
         // one chain after the other: interleaved by the scheduler, the
         // chains' select masks outgrow the SGPRs and spill to VGPR lanes
         if (q > 0) asm volatile("" : "+v"(a.m) : "v"(res[q - 1].m));
+#endif
 #pragma unroll
         for (int j = 0; j + 1 < NSRC; ++j) {
             x80d::xu r;
-            ok &= OP == MI355_OP_SUM ? x80d::add_fast_u<false>(a, u[j < q ? j : j + 1], r)
-                                     : x80d::mul_fast_u<false>(a, u[j < q ? j : j + 1], r);
+            const x80d::xu &b = u[j < q ? j : j + 1];
+            ok &= OP == MI355_OP_SUM ? x80d::add_fast_u<false>(a, b, r) : x80d::mul_fast_u<false>(a, b, r);
             a = r;
         }
         res[q] = a;
+#if MI355_X80_EARLY_STORE
+        // the fast result goes out now (its registers free for the next
+        // chain); a wave that fails the vote below rewrites every output
+        // from the general path (which works from v[], in registers, so an
+        // output aliasing its source is still safe)
+#pragma unroll
+        for (int w = 0; w < (q == 0 && NSRC > 1 ? 2 : 1); ++w) {
+            if (!ALL && p.dst[q + w] == nullptr) continue;
+            Pack<x80> o;
+            o.e[0] = x80d::pack(a, v[q + w]);
+            st16_fold((u32x4 *)p.dst[q + w] + i, o.v);
+        }
+#endif
+#if MI355_X80_SERIAL_CHAINS
         asm volatile("" : "+v"(ok));  // a VGPR, not lane masks kept (and spilled) across the chains
+#endif
     }
+#if MI355_X80_EARLY_STORE
+    if (__all(ok)) return;
+    if (false) {
+#else
     if (__all(ok)) {
+#endif
 #pragma unroll
         for (int q = 0; q < NSRC; ++q) {
             if (!ALL && p.dst[q] == nullptr) continue;
@@ -326,7 +363,11 @@ __device__ __forceinline__ bool single_fold_ok(const T &v) {
 }
 
 template <int OP, typename T, int NSRC, int UNROLL, int POL, bool ALL>
-__global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
+__global__ __launch_bounds__(kBlock)
+#if MI355_X80_WAVES
+__attribute__((amdgpu_waves_per_eu(MI355_X80_WAVES)))
+#endif
+void combine_orders_vec(OrdersParams p) {
     constexpr int V = 16 / sizeof(T);
     const uint64_t nvec = p.nvec;
     const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
