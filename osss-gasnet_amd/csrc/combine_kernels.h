@@ -18,8 +18,8 @@
 // Long double every-member fold, build-time forms measured against each other
 // (tools/build_x80_variants.sh): chains kept one after the other by an empty
 // asm dependence, each member's output stored as soon as its chain ends
-// instead of after the wave vote, and an occupancy floor (waves per SIMD) for
-// the orders kernels.
+// instead of after the wave vote, an occupancy floor (waves per SIMD) for the
+// orders kernels, and non-temporal source loads (the other folds' policy).
 #ifndef MI355_X80_SERIAL_CHAINS
 #define MI355_X80_SERIAL_CHAINS 1
 #endif
@@ -28,6 +28,9 @@
 #endif
 #ifndef MI355_X80_WAVES
 #define MI355_X80_WAVES 0
+#endif
+#ifndef MI355_X80_NT_LOADS
+#define MI355_X80_NT_LOADS 1
 #endif
 
 namespace mi355k {
@@ -240,11 +243,22 @@ __device__ __forceinline__ void orders_element(const OrdersParams &p, int64_t i)
 // output that aliases its source (in place) is safe. (Round 2 before this:
 // each member's fold re-read the sources from L2 one dependent load per
 // operation.)
-template <int OP, int NSRC, bool ALL>
-__device__ __forceinline__ void x80_orders_vector(const OrdersParams &p, uint64_t i) {
-    x80 v[NSRC];
+template <int NSRC>
+__device__ __forceinline__ void x80_load(const OrdersParams &p, uint64_t i, x80 (&v)[NSRC]) {
 #pragma unroll
-    for (int k = 0; k < NSRC; ++k) v[k] = ((const x80 *)p.src[k])[i];
+    for (int k = 0; k < NSRC; ++k) {
+#if MI355_X80_NT_LOADS
+        Pack<x80> w;
+        w.v = ld16<POL_NT_LOAD>((const u32x4 *)p.src[k] + i);
+        v[k] = w.e[0];
+#else
+        v[k] = ((const x80 *)p.src[k])[i];
+#endif
+    }
+}
+
+template <int OP, int NSRC, bool ALL>
+__device__ __forceinline__ void x80_orders_vector(const OrdersParams &p, uint64_t i, const x80 (&v)[NSRC]) {
     // Member 1's order (s1, s0, s2, ...) gives member 0's value (s0, s1, s2,
     // ...): x87 + and * commute, NaN and signed-zero rules included, and the
     // rest of the two chains is the same -- one chain fewer per element.
@@ -372,8 +386,13 @@ void combine_orders_vec(OrdersParams p) {
     const uint64_t nvec = p.nvec;
     const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
     if constexpr (std::is_same<T, x80>::value && (OP == MI355_OP_SUM || OP == MI355_OP_PROD)) {
-        for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nvec; i += (uint64_t)gridDim.x * kBlock)
-            x80_orders_vector<OP, NSRC, ALL>(p, i);
+        const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+        uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+        for (; i < nvec; i += stride) {
+            x80 v[NSRC];
+            x80_load<NSRC>(p, i, v);
+            x80_orders_vector<OP, NSRC, ALL>(p, i, v);
+        }
         signal_done(p.sig, false);
         return;
     }

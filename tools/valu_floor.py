@@ -1,0 +1,72 @@
+#!/usr/bin/env python3
+"""VALU-issue floor of one kernel's per-element instruction stream: the
+kernel's opcode histogram between its first vector load and first vector
+store (the per-element body of a grid-stride fold; see STORES), each opcode priced at the
+chip-wide saturated rate tools/valu_rate.hip measured for its kind
+(profiles/r04/valu_rate.jsonl, 8 waves per SIMD), times the element-waves of
+one launch. Measurement tool: the VALU roofline of the long double
+every-member fold.
+usage: valu_floor.py OBJECT 'KERNEL SUBSTRING' RATES.jsonl ELEMENTS_PER_LAUNCH [STORES]
+STORES: the body ends at the STORES-th vector store (default 1; the every-
+member fold stores each output when its chain ends: one per output)"""
+import collections
+import json
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import check_residency as cr  # noqa: E402
+
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+
+def kind(op):
+    """the probe kind whose measured rate prices this opcode"""
+    if re.match(r"v_(add_co|addc_co|sub_co|subb_co|subrev_co|subbrev_co)_u32", op):
+        return "v_add_co+v_addc_co"
+    if re.match(r"v_(lshlrev|lshrrev|ashrrev)_(b|i)64|v_lshl_add_u64", op):
+        return "v_lshlrev_b64"
+    if re.match(r"v_cmp_\w+_(u|i)64", op):
+        return "v_cmp_gt_u64(sgpr)"
+    if op.startswith("v_cndmask") or op.startswith("v_cmp"):
+        return "v_cndmask_b32(sgpr mask)"   # lane-mask producers / consumers
+    return "v_add_u32"
+
+
+def main():
+    obj, sub, rates_path, elements = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    stores = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+    rates = {}
+    for ln in open(rates_path):
+        d = json.loads(ln)
+        if d["waves_per_simd"] == 8:
+            rates[d["kind"]] = d["chip_wave_insts_per_s"]
+    with tempfile.TemporaryDirectory() as t:
+        co = cr.code_object(obj, t)
+        dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--demangle", co], capture_output=True, text=True,
+                             check=True).stdout.splitlines()
+    start = next(i for i, ln in enumerate(dis) if re.match(r"^[0-9a-f]+ <", ln) and sub in ln)
+    end = next((i for i in range(start + 1, len(dis)) if re.match(r"^[0-9a-f]+ <", dis[i])), len(dis))
+    body = [ln.strip().split("//")[0].split()[0] for ln in dis[start + 1:end] if ln.startswith("\t")]
+    lo = next(i for i, op in enumerate(body) if op.startswith(("global_load", "buffer_load")))
+    hi = [i for i, op in enumerate(body) if op.startswith(("global_store", "buffer_store"))][stores - 1]
+    ops = collections.Counter(op for op in body[lo:hi] if op.startswith("v_"))
+    per_kind = collections.Counter()
+    for op, c in ops.items():
+        per_kind[kind(op)] += c
+    secs = sum(c / rates[k] for k, c in per_kind.items())   # chip-seconds per element-wave
+    waves = elements / 64
+    print(json.dumps({"kernel": sub, "valu_per_element_wave": sum(ops.values()), "by_kind": dict(per_kind),
+                      "salu_per_element_wave": sum(1 for op in body[lo:hi] if op.startswith("s_") and op != "s_nop"),
+                      "s_nop": sum(1 for op in body[lo:hi] if op == "s_nop"),
+                      "floor_us": round(secs * waves * 1e6, 1),
+                      "stores": stores,
+                      "note": "each opcode priced at its kind's saturated chip rate (valu_rate.jsonl, 8 waves/SIMD); "
+                              "body = first vector load to the STORES-th vector store"}))
+
+
+if __name__ == "__main__":
+    main()
