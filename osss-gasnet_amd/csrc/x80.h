@@ -136,11 +136,17 @@ __device__ __forceinline__ x80 quiet(x80 a) {
     a.m |= 0x4000000000000000ull;
     return a;
 }
-// NaN result of an operation with at least one NaN operand.
+// NaN result of an operation with at least one NaN operand, by the 387's
+// rule: one NaN -> it, quieted; a signalling and a quiet NaN -> the quiet one,
+// whatever the significands; two of the same kind -> the larger significand
+// (equal: the positive one), quieted. (Before round 4 a signalling/quiet pair
+// took the larger quieted significand too: tests/native/x80_host_check.cpp's
+// NaN-pair loop pins the rule against the host x87.)
 __device__ __forceinline__ x80 nan_result(const x80 &a, const x80 &b) {
     const bool na = is_nan(a), nb = is_nan(b);
+    const bool qa = ((a.m >> 62) & 1) != 0, qb = ((b.m >> 62) & 1) != 0;
     const uint64_t ma = a.m | 0x4000000000000000ull, mb = b.m | 0x4000000000000000ull;
-    const bool take_a = (na & nb) ? (ma != mb ? ma > mb : sign(a) == 0) : na;
+    const bool take_a = (na & nb) ? (qa != qb ? qa : ma != mb ? ma > mb : sign(a) == 0) : na;
     return quiet(pick(take_a, a, b));
 }
 

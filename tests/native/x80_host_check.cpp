@@ -98,7 +98,7 @@ int main(int argc, char **argv) {
         case 1: e = 0; m = g() >> (1 + g() % 63); break;                      // denormal
         case 2: e = 0; break;                                                 // pseudo-denormal
         case 3: e = 0x7FFF; m = 1ull << 63; break;                            // infinity
-        case 4: e = 0x7FFF; m = (1ull << 63) | (g() >> 2) | 1; break;         // NaN
+        case 4: e = 0x7FFF; m = (1ull << 63) | (g() >> 1) | 1; break;         // NaN, quiet or signalling
         case 5: e = 1 + (int)(g() % 0x7FFE); m = g() >> 1; break;             // unnormal
         case 6: e = 0x7FFF; m = g() >> 1; break;                              // pseudo-inf / pseudo-NaN
         default: break;                                                       // normal near e0
@@ -149,5 +149,40 @@ int main(int argc, char **argv) {
         }
     }
     printf("general: %ld pairs, %ld mismatches\n", ng, badg);
-    return bad != 0 || badc != 0 || badg != 0;
+    // two NaN operands (the 387's rule: two quiet or two signalling NaNs give
+    // the larger significand, a signalling and a quiet NaN give the quiet one,
+    // whatever the significands), quiet bits, signs and significands picked so
+    // that the quieted significands are often equal or ordered either way;
+    // and one NaN against a number, an infinity or a zero
+    long nn = 0, badn = 0;
+    for (long i = 0; i < per / 4; ++i) {
+        const uint64_t base = (1ull << 63) | (g() >> 2) | 1;
+        auto nan = [&](void) {
+            x80 r;
+            memset(&r, 0, sizeof r);
+            uint64_t m = g() % 3 ? base : (1ull << 63) | (g() >> 2) | 1;
+            m ^= (g() % 4 == 0) ? (g() & 0xFF) & ~1ull : 0;
+            m |= (g() & 1) ? (1ull << 62) : 0;                                // quiet or signalling
+            r.m = m;
+            r.se = (uint16_t)(((g() & 1) << 15) | 0x7FFF);
+            return r;
+        };
+        x80 a = nan(), b = g() % 4 ? nan() : any(1 + (int)(g() % 0x7FFE));
+        if (g() % 2) { x80 t = a; a = b; b = t; }
+        long double la, lb;
+        memset(&la, 0, sizeof la);
+        memset(&lb, 0, sizeof lb);
+        memcpy(&la, &a, 10);
+        memcpy(&lb, &b, 10);
+        volatile long double s = la + lb, p = la * lb;
+        ++nn;
+        if (!same(x80d::add_general(a, b), s) || !same(x80d::mul_general(a, b), p)) {
+            if (badn < 5)
+                printf("NaN-pair mismatch: %04x %016llx, %04x %016llx\n", a.se, (unsigned long long)a.m, b.se,
+                       (unsigned long long)b.m);
+            ++badn;
+        }
+    }
+    printf("NaN pairs: %ld pairs, %ld mismatches\n", nn, badn);
+    return bad != 0 || badc != 0 || badg != 0 || badn != 0;
 }

@@ -252,6 +252,16 @@ def test_combine_orders_x87_chains(shm, dev, op, nsrc, case):
     for q, g in got.items():
         assert_match(g, want[q], op, "longdouble", ctx=f"{case} nsrc={nsrc} member {q}")
     dev.free()
+    if case == "sparse":
+        # each member's output is stored as its chain ends, before the wave
+        # vote; a wave that fails it rewrites them from the general path: with
+        # an output skipped (member 1, whose value the first chain also gives)
+        # and one in place (the early store lands on its own source)
+        got = gpu_orders(shm, dev, op, "longdouble", srcs, skip=(1,), inplace=0 if nsrc == 2 else nsrc - 1)
+        assert sorted(got) == [q for q in range(nsrc) if q != 1]
+        for q, g in got.items():
+            assert_match(g, want[q], op, "longdouble", ctx=f"{case} nsrc={nsrc} member {q} skip/in place")
+        dev.free()
 
 
 @pytest.mark.parametrize("op,dtype", [("sum", "double"), ("xor", "int"), ("max", "float"), ("prod", "complexf"),
