@@ -372,7 +372,14 @@ KERNEL_LEGS = [
     ("fold_k8_float_max", "combine_vec<max,float,8>", "max", "float", 8, 64 << 20, False),
     ("fold_k8_longlong_and", "combine_vec<and,longlong,8>", "and", "longlong", 8, 64 << 20, False),
     ("rs_shard_n8_float_max", "combine_orders_vec<max,float,8>", "max", "float", 8, 8 << 20, True),
+    # long double (x87 arithmetic in software, x80.h): the sum is VALU-bound, the product HBM-bound
+    ("rs_shard_n8_longdouble_sum", "combine_orders_vec<sum,x80,8>", "sum", "longdouble", 8, 32 << 20, True),
+    ("rs_shard_n8_longdouble_prod", "combine_orders_vec<prod,x80,8>", "prod", "longdouble", 8, 32 << 20, True),
 ]
+# the long double sum's roofline is VALU issue: its per-element instruction
+# stream in this build priced at the measured issue rates -- computed by the
+# library's build (csrc/Makefile, tools/valu_floor.py) into lib/valu_floor.json
+VALU_FLOOR = {"rs_shard_n8_longdouble_sum": os.path.join(ROOT, "osss-gasnet_amd", "lib", "valu_floor.json")}
 
 
 def kernel_legs(shm, reps, check):
@@ -387,8 +394,10 @@ def kernel_legs(shm, reps, check):
                    sources of one shard, 8 outputs (every member's reference
                    order), algorithmic bytes 16 x shard bytes.
     Sources: (uniform - 0.5) doubles, full mantissa (the float/longlong legs
-    read the same bytes as their type). Checked bit-exact against the oracle
-    on a sample of every output."""
+    read the same bytes as their type; the long double legs the same values
+    widened to x87). Checked bit-exact (value bytes) against the oracle on a
+    sample of every output. The long double sum also carries its VALU
+    roofline (VALU_FLOOR)."""
     import ctypes
     import oracle
     L = shm.lib
@@ -421,6 +430,10 @@ def kernel_legs(shm, reps, check):
         es = np.dtype(shmem_reduce.NP[dtype]).itemsize
         n = nbytes // es
         nout = k if orders else 1
+        if dtype == "longdouble":   # realistic x87 operands, not doubles' bytes read as x87
+            lds = [hosts[p][:n].astype(np.longdouble) for p in range(k)]
+            for p in range(k):
+                shm.put(srcs[p], lds[p])
 
         def launch():
             if orders:
@@ -445,19 +458,33 @@ def kernel_legs(shm, reps, check):
         ck = "skipped"
         if check:
             idx = np.unique(np.random.default_rng(5).integers(0, n, 1 << 14))
-            samp = [np.ascontiguousarray(h.view(np.uint8)[:nbytes].view(shmem_reduce.NP[dtype])[idx])
-                    for h in hosts[:k]]
+            if dtype == "longdouble":
+                samp = [np.ascontiguousarray(x[idx]) for x in lds]
+            else:
+                samp = [np.ascontiguousarray(h.view(np.uint8)[:nbytes].view(shmem_reduce.NP[dtype])[idx])
+                        for h in hosts[:k]]
             bad = 0
             for q in range(nout):
                 got = shm.get(outs[q], n, dtype)[idx]
                 want = oracle.reduce_pe(op, dtype, samp, q)
-                bad += int((got.view(np.uint8) != want.view(np.uint8)).sum())
+                bad += int((oracle.as_value_bytes(got, dtype) != oracle.as_value_bytes(want, dtype)).sum())
             ck = (f"bit-exact vs the oracle, {len(idx)} samples x {nout} output(s)" if bad == 0
                   else f"MISMATCH in {bad} bytes")
         res[name] = {"kernel": kname, "sources": k, "outputs": nout, "bytes_per_source": nbytes,
                      "alg_bytes_per_launch": alg, "kernel_avg_us": round(t * 1e6, 2),
                      "kernel_median_us": round(float(np.median(ts)) * 1e6, 2), "launches": reps,
                      "achieved_GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "check": ck}
+        if name in VALU_FLOOR:
+            try:
+                fl = json.load(open(VALU_FLOOR[name]))
+                res[name].update({"bound": "valu", "valu_floor_us": fl["floor_us"],
+                                  "valu_frac": round(fl["floor_us"] / (t * 1e6), 4),
+                                  "valu_per_element_wave": fl["valu_per_element_wave"],
+                                  "valu_note": "VALU-bound (x87 arithmetic in integer code): floor = this build's "
+                                               "per-element instruction stream priced at the issue rates measured by "
+                                               "tools/valu_rate.hip (profiles/r04/valu); frac above is the HBM view"})
+            except (OSError, ValueError, KeyError) as e:   # the leg stands without its floor
+                res[name]["valu_floor_error"] = f"{type(e).__name__}: {e}"
     for e in ev:
         L.hipEventDestroy(e)
     for d in srcs + outs:

@@ -36,9 +36,8 @@ def kind(op):
     return "v_add_u32"
 
 
-def main():
-    obj, sub, rates_path, elements = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
-    stores = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+def floor(obj, sub, rates_path, elements, stores=1):
+    """the record main() prints, as a dict"""
     rates = {}
     for ln in open(rates_path):
         d = json.loads(ln)
@@ -59,13 +58,19 @@ def main():
         per_kind[kind(op)] += c
     secs = sum(c / rates[k] for k, c in per_kind.items())   # chip-seconds per element-wave
     waves = elements / 64
-    print(json.dumps({"kernel": sub, "valu_per_element_wave": sum(ops.values()), "by_kind": dict(per_kind),
-                      "salu_per_element_wave": sum(1 for op in body[lo:hi] if op.startswith("s_") and op != "s_nop"),
-                      "s_nop": sum(1 for op in body[lo:hi] if op == "s_nop"),
-                      "floor_us": round(secs * waves * 1e6, 1),
-                      "stores": stores,
-                      "note": "each opcode priced at its kind's saturated chip rate (valu_rate.jsonl, 8 waves/SIMD); "
-                              "body = first vector load to the STORES-th vector store"}))
+    return {"kernel": sub, "valu_per_element_wave": sum(ops.values()), "by_kind": dict(per_kind),
+            "salu_per_element_wave": sum(1 for op in body[lo:hi] if op.startswith("s_") and op != "s_nop"),
+            "s_nop": sum(1 for op in body[lo:hi] if op == "s_nop"),
+            "floor_us": round(secs * waves * 1e6, 1),
+            "stores": stores,
+            "note": "each opcode priced at its kind's saturated chip rate (valu_rate.jsonl, 8 waves/SIMD); "
+                    "body = first vector load to the STORES-th vector store"}
+
+
+def main():
+    obj, sub, rates_path, elements = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
+    stores = int(sys.argv[5]) if len(sys.argv) > 5 else 1
+    print(json.dumps(floor(obj, sub, rates_path, elements, stores)))
 
 
 if __name__ == "__main__":
