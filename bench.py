@@ -376,10 +376,11 @@ KERNEL_LEGS = [
     ("rs_shard_n8_longdouble_sum", "combine_orders_vec<sum,x80,8>", "sum", "longdouble", 8, 32 << 20, True),
     ("rs_shard_n8_longdouble_prod", "combine_orders_vec<prod,x80,8>", "prod", "longdouble", 8, 32 << 20, True),
 ]
-# the long double sum's roofline is VALU issue: its per-element instruction
-# stream in this build priced at the measured issue rates -- computed by the
-# library's build (csrc/Makefile, tools/valu_floor.py) into lib/valu_floor.json
-VALU_FLOOR = {"rs_shard_n8_longdouble_sum": os.path.join(ROOT, "osss-gasnet_amd", "lib", "valu_floor.json")}
+# the long double legs' VALU floor: their per-element instruction streams in
+# this build priced at the measured issue rates -- computed by the library's
+# build (csrc/Makefile, tools/valu_floor.py --bench-legs) into lib/valu_floor.json;
+# a leg's bound is the larger of its VALU floor and its bytes at the HBM peak
+VALU_FLOOR = os.path.join(ROOT, "osss-gasnet_amd", "lib", "valu_floor.json")
 
 
 def kernel_legs(shm, reps, check):
@@ -396,8 +397,8 @@ def kernel_legs(shm, reps, check):
     Sources: (uniform - 0.5) doubles, full mantissa (the float/longlong legs
     read the same bytes as their type; the long double legs the same values
     widened to x87). Checked bit-exact (value bytes) against the oracle on a
-    sample of every output. The long double sum also carries its VALU
-    roofline (VALU_FLOOR)."""
+    sample of every output. The long double legs also carry their VALU
+    floor and the bound it implies (VALU_FLOOR)."""
     import ctypes
     import oracle
     L = shm.lib
@@ -474,15 +475,18 @@ def kernel_legs(shm, reps, check):
                      "alg_bytes_per_launch": alg, "kernel_avg_us": round(t * 1e6, 2),
                      "kernel_median_us": round(float(np.median(ts)) * 1e6, 2), "launches": reps,
                      "achieved_GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "check": ck}
-        if name in VALU_FLOOR:
+        if dtype == "longdouble":
             try:
-                fl = json.load(open(VALU_FLOOR[name]))
-                res[name].update({"bound": "valu", "valu_floor_us": fl["floor_us"],
+                fl = json.load(open(VALU_FLOOR))[name]
+                hbm_floor_us = alg / (HBM_PEAK_GBS * 1e9) * 1e6
+                res[name].update({"bound": "valu" if fl["floor_us"] > hbm_floor_us else "hbm",
+                                  "valu_floor_us": fl["floor_us"], "hbm_floor_us": round(hbm_floor_us, 1),
                                   "valu_frac": round(fl["floor_us"] / (t * 1e6), 4),
                                   "valu_per_element_wave": fl["valu_per_element_wave"],
-                                  "valu_note": "VALU-bound (x87 arithmetic in integer code): floor = this build's "
-                                               "per-element instruction stream priced at the issue rates measured by "
-                                               "tools/valu_rate.hip (profiles/r04/valu); frac above is the HBM view"})
+                                  "valu_note": "x87 arithmetic in integer code: valu_floor = this build's per-element "
+                                               "instruction stream priced at the issue rates measured by "
+                                               "tools/valu_rate.hip (profiles/r04/valu); bound = the larger of it and "
+                                               "hbm_floor (alg bytes at 8 TB/s); frac above is the HBM view"})
             except (OSError, ValueError, KeyError) as e:   # the leg stands without its floor
                 res[name]["valu_floor_error"] = f"{type(e).__name__}: {e}"
     for e in ev:

@@ -87,6 +87,8 @@ def test_bench_one_gpu_line():
     # the x87 sum's own roofline: VALU issue, from this build's instruction stream
     ls = k["rs_shard_n8_longdouble_sum"]
     assert ls["bound"] == "valu" and 0.3 < ls["valu_frac"] < 1.05 and ls["valu_per_element_wave"] > 1000, ls
+    lp = k["rs_shard_n8_longdouble_prod"]
+    assert lp["bound"] in ("valu", "hbm") and 0.3 < lp["valu_frac"] < 1.05 and lp["hbm_floor_us"] > 0, lp
     f = d["fused_same_gpu"]
     assert "error" not in f, f
     for leg in f["legs"].values():

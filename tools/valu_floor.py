@@ -3,10 +3,11 @@
 kernel's opcode histogram between its first vector load and first vector
 store (the per-element body of a grid-stride fold; see STORES), each opcode priced at the
 chip-wide saturated rate tools/valu_rate.hip measured for its kind
-(profiles/r04/valu_rate.jsonl, 8 waves per SIMD), times the element-waves of
+(profiles/r04/valu/valu_rate.jsonl, 8 waves per SIMD), times the element-waves of
 one launch. Measurement tool: the VALU roofline of the long double
 every-member fold.
 usage: valu_floor.py OBJECT 'KERNEL SUBSTRING' RATES.jsonl ELEMENTS_PER_LAUNCH [STORES]
+       valu_floor.py --bench-legs OBJECT RATES.jsonl   (bench.py's long double kernel legs, one JSON dict)
 STORES: the body ends at the STORES-th vector store (default 1; the every-
 member fold stores each output when its chain ends: one per output)"""
 import collections
@@ -33,6 +34,11 @@ def kind(op):
         return "v_cmp_gt_u64(sgpr)"
     if op.startswith("v_cndmask") or op.startswith("v_cmp"):
         return "v_cndmask_b32(sgpr mask)"   # lane-mask producers / consumers
+    for m in ("v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32"):
+        if op.startswith(m):
+            return m
+    # the rest at the 32-bit add's rate (measured the same in the 4- and
+    # 8-byte encodings: v_add_u32_e64 1.03e12, v_mov_b32 1.05e12)
     return "v_add_u32"
 
 
@@ -67,7 +73,19 @@ def floor(obj, sub, rates_path, elements, stores=1):
                     "body = first vector load to the STORES-th vector store"}
 
 
+# bench.py's kernel legs on the long double every-member fold: 8 sources x
+# 32 MiB (2 Mi x87 elements), 8 outputs, each stored when its chain ends
+BENCH_LEGS = {
+    "rs_shard_n8_longdouble_sum": ("combine_orders_vec<0, x80, 8, 1, 1, true>", 2097152, 8),
+    "rs_shard_n8_longdouble_prod": ("combine_orders_vec<1, x80, 8, 1, 1, true>", 2097152, 8),
+}
+
+
 def main():
+    if sys.argv[1] == "--bench-legs":
+        print(json.dumps({leg: floor(sys.argv[2], sub, sys.argv[3], n, st)
+                          for leg, (sub, n, st) in BENCH_LEGS.items()}))
+        return
     obj, sub, rates_path, elements = sys.argv[1], sys.argv[2], sys.argv[3], int(sys.argv[4])
     stores = int(sys.argv[5]) if len(sys.argv) > 5 else 1
     print(json.dumps(floor(obj, sub, rates_path, elements, stores)))

@@ -23,9 +23,11 @@
 constexpr int kIters = 2048;
 constexpr int kPerIter = 16;  // instructions per loop iteration (8 chains x 2)
 
-enum Kind { ADD32, XOR32, SHL64, ADDC, CNDMASK, CMP64, MIX, NKIND };
+enum Kind { ADD32, XOR32, SHL64, ADDC, CNDMASK, CMP64, MIX, MAD64, MULLO, MULHI, MOV, ADD32_E64, XOR32_E64, NKIND };
 static const char *kNames[NKIND] = {"v_add_u32", "v_xor_b32", "v_lshlrev_b64", "v_add_co+v_addc_co",
-                                    "v_cndmask_b32(sgpr mask)", "v_cmp_gt_u64(sgpr)", "x87-add mix"};
+                                    "v_cndmask_b32(sgpr mask)", "v_cmp_gt_u64(sgpr)", "x87-add mix",
+                                    "v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mov_b32",
+                                    "v_add_u32_e64", "v_xor_b32_e64"};
 
 template <int K>
 __global__ __launch_bounds__(256) void rate(uint64_t *out, uint64_t *cyc, uint32_t seed) {
@@ -72,6 +74,33 @@ __global__ __launch_bounds__(256) void rate(uint64_t *out, uint64_t *cyc, uint32
 #undef OP2
             a0 ^= (uint32_t)m0;
             a1 ^= (uint32_t)m1;
+        } else if constexpr (K == MAD64) {
+#define OP2(x) asm volatile("v_mad_u64_u32 %0, vcc, %1, %1, %0\n\tv_mad_u64_u32 %0, vcc, %1, %1, %0" : "+v"(x) \
+                            : "v"(k) : "vcc")
+            OP2(b0); OP2(b1); OP2(b2); OP2(b3); OP2(b4); OP2(b5); OP2(b6); OP2(b7);
+#undef OP2
+        } else if constexpr (K == MULLO) {
+#define OP2(x) asm volatile("v_mul_lo_u32 %0, %0, %1\n\tv_mul_lo_u32 %0, %0, %1" : "+v"(x) : "v"(k))
+            OP2(a0); OP2(a1); OP2(a2); OP2(a3); OP2(a4); OP2(a5); OP2(a6); OP2(a7);
+#undef OP2
+        } else if constexpr (K == MULHI) {
+#define OP2(x) asm volatile("v_mul_hi_u32 %0, %0, %1\n\tv_mul_hi_u32 %0, %0, %1" : "+v"(x) : "v"(k))
+            OP2(a0); OP2(a1); OP2(a2); OP2(a3); OP2(a4); OP2(a5); OP2(a6); OP2(a7);
+#undef OP2
+        } else if constexpr (K == ADD32_E64) {
+            // the same operation as ADD32 in the 8-byte (VOP3) encoding
+#define OP2(x) asm volatile("v_add_u32_e64 %0, %0, %1\n\tv_add_u32_e64 %0, %0, %1" : "+v"(x) : "v"(k))
+            OP2(a0); OP2(a1); OP2(a2); OP2(a3); OP2(a4); OP2(a5); OP2(a6); OP2(a7);
+#undef OP2
+        } else if constexpr (K == XOR32_E64) {
+#define OP2(x) asm volatile("v_xor_b32_e64 %0, %0, %1\n\tv_xor_b32_e64 %0, %0, %1" : "+v"(x) : "v"(k))
+            OP2(a0); OP2(a1); OP2(a2); OP2(a3); OP2(a4); OP2(a5); OP2(a6); OP2(a7);
+#undef OP2
+        } else if constexpr (K == MOV) {
+#define OP2(x, y) asm volatile("v_mov_b32 %0, %1\n\tv_mov_b32 %1, %0" : "+v"(x), "+v"(y))
+            OP2(a0, a1); OP2(a2, a3); OP2(a4, a5); OP2(a6, a7);
+            OP2(a1, a2); OP2(a3, a4); OP2(a5, a6); OP2(a7, a0);
+#undef OP2
         } else {
             // the x87 fast add's mix per 16: 2 addc-pairs, 2 xor, 2 cndmask,
             // 2 sub, 2 64-bit shifts, 1 or, 1 ffbh, 1 cmp64, 1 max, 1 and
@@ -155,5 +184,11 @@ int main(int argc, char **argv) {
     sweep<CNDMASK>(argc, argv, cus);
     sweep<CMP64>(argc, argv, cus);
     sweep<MIX>(argc, argv, cus);
+    sweep<MAD64>(argc, argv, cus);
+    sweep<MULLO>(argc, argv, cus);
+    sweep<MULHI>(argc, argv, cus);
+    sweep<MOV>(argc, argv, cus);
+    sweep<ADD32_E64>(argc, argv, cus);
+    sweep<XOR32_E64>(argc, argv, cus);
     return 0;
 }
