@@ -15,8 +15,8 @@
 //   * operands the 387+ rejects (unnormals, pseudo-infinities, pseudo-NaNs)
 //     and invalid operations (inf - inf, 0 * inf) give the x87 "real
 //     indefinite" QNaN (sign 1, exponent 0x7FFF, significand 0xC000...);
-//   * NaN operands propagate quietened (the one with the larger significand
-//     when both are NaN);
+//   * NaN operands propagate quietened (when both are NaN: the quiet one
+//     beside a signalling one, else the one with the larger significand);
 //   * min/max select an operand's bits unchanged; an unordered compare is
 //     false, so the second operand is returned (as on the host).
 #pragma once
@@ -340,13 +340,38 @@ __device__ __forceinline__ x80 add(const x80 &a, const x80 &b) {
     return add_general(a, b);
 }
 
+// The 128-bit product of two 64-bit significands from 32-bit limbs, each
+// partial product a 32 x 32 -> 64 multiply-add whose 64-bit addend carries the
+// previous one's upper half (no sum overflows 64 bits: (2^32-1)^2 + 2 (2^32-1)
+// = 2^64 - 1); the low word is assembled from the partial products' halves.
+// (__umul64hi next to a * b compiled to the same four multiply-adds plus two
+// 32-bit multiplies and an add recomputing the low word's upper half.)
+#ifndef MI355_X80_MUL128
+#define MI355_X80_MUL128 1
+#endif
+__device__ __forceinline__ void mul64x64(uint64_t a, uint64_t b, uint64_t &hi, uint64_t &lo) {
+#if MI355_X80_MUL128
+    const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
+    const uint64_t p00 = (uint64_t)a0 * b0;
+    const uint64_t p01 = (uint64_t)a0 * b1 + (p00 >> 32);
+    const uint64_t p10 = (uint64_t)a1 * b0 + (uint32_t)p01;
+    const uint64_t p11 = (uint64_t)a1 * b1 + (p01 >> 32);
+    hi = p11 + (p10 >> 32);
+    lo = (p10 << 32) | (uint32_t)p00;
+#else
+    hi = __umul64hi(a, b);
+    lo = a * b;
+#endif
+}
+
 template <bool RANGE = true>
 __device__ __forceinline__ bool mul_fast_u(const xu &a, const xu &b, xu &r) {
     // straight-line like add_fast_u: the 128-bit product's leading bit is at
     // 127 or 126 (one conditional left shift, as a select), one rounding (a
     // round up that wraps the significand takes the general path)
     const int E = a.e + b.e - kBias + 1;  // biased exponent, leading bit at 127
-    const uint64_t hi = __umul64hi(a.m, b.m), lo = a.m * b.m;
+    uint64_t hi, lo;
+    mul64x64(a.m, b.m, hi, lo);
     const bool low = (hi >> 63) == 0;  // leading bit at 126
     const uint64_t nhi = low ? (hi << 1) | (lo >> 63) : hi;
     const uint64_t nlo = low ? lo << 1 : lo;
@@ -371,7 +396,9 @@ __device__ __forceinline__ x80 mul_general(const x80 &a, const x80 &b) {
     const int s = sign(a) ^ sign(b);
     const int za = is_zero(a), zb = is_zero(b), ia = is_inf(a), ib = is_inf(b);  // ints: no branches
     const int na = is_nan(a), nb = is_nan(b), ua = unsupported(a), ub = unsupported(b);
-    const u128 P = mk(__umul64hi(a.m, b.m), a.m * b.m);
+    uint64_t phi, plo;
+    mul64x64(a.m, b.m, phi, plo);
+    const u128 P = mk(phi, plo);
     x80 r = round_pack(s, P, exp_of(a) + exp_of(b), false, a);
     r = pick(za | zb, make(s, 0, 0, a), r);
     const x80 inf_r = pick(za | zb, indefinite(a), make(s, kEmaxField, 0x8000000000000000ull, a));  // 0 x inf
