@@ -32,6 +32,12 @@
 #ifndef MI355_X80_NT_LOADS
 #define MI355_X80_NT_LOADS 1
 #endif
+// Float complex products in the every-member fold: plain products and one
+// wave vote on Annex G's recovery case instead of its branch after every
+// product.
+#ifndef MI355_CPLX_VOTE
+#define MI355_CPLX_VOTE 1
+#endif
 
 namespace mi355k {
 
@@ -437,6 +443,38 @@ void combine_orders_vec(OrdersParams p) {
                     continue;
                 }
             }
+#if MI355_CPLX_VOTE
+            if constexpr (OP == MI355_OP_PROD && std::is_same<T, cplxf>::value) {
+                // Annex G's recovery (ops.h cmul) changes a product only when
+                // both parts come out NaN: every member's chain with the plain
+                // products first, each output stored as its chain ends, and
+                // one wave vote on whether any product of any lane hit that
+                // case -- then the wave redoes its chains with cmul (from
+                // registers, so an output aliasing its source is safe) and
+                // rewrites them; the same bits either way. Float only: 8
+                // sources x 32 MiB, 97.5 -> 91.8 us; double complex went the
+                // other way, 87.0 -> 94.0 (profiles/r04/cplx_vote/)
+                int hit = 0;
+#pragma unroll
+                for (int q = 0; q < NSRC; ++q) {
+                    if (!ALL && p.dst[q] == nullptr) continue;
+                    Pack<T> acc = x[u][q];
+#pragma unroll
+                    for (int k = 0; k < NSRC; ++k) {
+                        if (k == q) continue;
+#pragma unroll
+                        for (int e = 0; e < V; ++e) {
+                            const auto a = acc.e[e], b = x[u][k].e[e];
+                            acc.e[e].re = a.re * b.re - a.im * b.im;
+                            acc.e[e].im = a.re * b.im + a.im * b.re;
+                            hit |= __builtin_isnan(acc.e[e].re) & __builtin_isnan(acc.e[e].im);
+                        }
+                    }
+                    st16_fold((u32x4 *)p.dst[q] + i, acc.v);
+                }
+                if (__all(!hit)) continue;
+            }
+#endif
 #pragma unroll
             for (int q = 0; q < NSRC; ++q) {
                 if (!ALL && p.dst[q] == nullptr) continue;
