@@ -170,3 +170,22 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
     assert "share ONE GPU" in lp["note"], lp
     # those three legs ran in the child job (tools/extra_legs.py), before the rank touched the GPU
     assert d["legs_s"]["extra_legs_child"] > 0, d["legs_s"]
+
+
+@pytest.mark.multipe
+def test_bench_line_survives_a_dying_extra_legs_job():
+    """The N > 1 legs that had never run with one GPU per PE run in a child
+    job (tools/extra_legs.py) so that a fatal error there cannot cost the
+    driver its line: with every child PE aborting after init (as a fatal
+    library error ends a PE), rank 0 still prints one line, with an error
+    entry under exactly those three legs and the headline intact."""
+    env = dict(os.environ, SHMEM_TEST_EXTRA_LEGS_ABORT="1")
+    d = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+             "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "2", "--steps",
+             "5", "--warmup", "2", "--no-cpu-baseline", "--no-small", "--no-ops", "--no-threshold-sweep",
+             "--no-rccl-compare"], env=env)
+    assert d["value"] > 0 and d["check"].startswith("bit-exact"), d
+    for leg in ("external_buffers", "link_probe", "collectives"):
+        assert set(d[leg]) == {"error"} and "child job" in d[leg]["error"], (leg, d[leg])
+    assert not any(isinstance(v, dict) and "error" in v for k, v in d.items()
+                   if k not in ("external_buffers", "link_probe", "collectives")), d

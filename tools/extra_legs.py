@@ -45,6 +45,10 @@ def main():
         and algorithm != "rccl"
     shm.set_algorithm(algorithm)
     me, npes = shm.my_pe(), shm.n_pes()
+    # test hook (tests/test_gpu_bench.py): the PE dies as a fatal library
+    # error would end it, after init -- bench.py must still print its line
+    if os.environ.get("SHMEM_TEST_EXTRA_LEGS_ABORT") == "1":
+        os.abort()
     loop = shmem_reduce.bench_loop()
     out = {}
 
