@@ -392,6 +392,35 @@ def test_complex_prod_annex_g_cases(shm, dev):
         dev.free()
 
 
+@pytest.mark.parametrize("nsrc", [3, 8])
+@pytest.mark.parametrize("dtype", ["complexf", "complexd"])
+def test_complex_prod_annex_g_every_member(shm, dev, dtype, nsrc):
+    """The every-member complex product (combine_kernels.h: float complex
+    chains with plain products and one wave vote on Annex G's recovery case,
+    double complex with the recovery after each product): the Annex G operands
+    planted sparsely among finite values, so one launch has waves that pass
+    the vote and waves that redo their chains; every member against the
+    reference's order, with one output skipped and one in place."""
+    inf, nan = np.inf, np.nan
+    specials = [complex(inf, nan), complex(nan, inf), complex(inf, inf), complex(nan, nan), complex(0, 0),
+                complex(-0.0, inf), complex(1e30, 1e30), complex(nan, 0), complex(0, -inf)]
+    rng = np.random.default_rng(31 * nsrc + len(dtype))
+    n = 30000
+    srcs = []
+    for k in range(nsrc):
+        x = (rng.uniform(-1.5, 1.5, n) + 1j * rng.uniform(-1.5, 1.5, n)).astype(np.complex128)
+        pos = rng.integers(0, n, 40)
+        x[pos] = [specials[(k + j) % len(specials)] for j in range(len(pos))]
+        srcs.append(x.astype(oracle.NP[dtype]))
+    want = oracle.reduce_all("prod", dtype, srcs)
+    for skip, inplace in (((), None), ((1,), nsrc - 1)):
+        got = gpu_orders(shm, dev, "prod", dtype, srcs, skip=skip, inplace=inplace)
+        assert sorted(got) == [q for q in range(nsrc) if q not in skip]
+        for q, g in got.items():
+            assert_match(g, want[q], "prod", dtype, ctx=f"nsrc={nsrc} member {q} skip={skip}")
+        dev.free()
+
+
 def test_full_size_256mib_properties(shm, dev):
     """At the benchmark size (2^25 doubles = 256 MiB per source):
     - 2-source double sum equals numpy's IEEE a + b bit for bit,
