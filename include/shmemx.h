@@ -102,11 +102,13 @@ int shmemx_get_reduce_order (void);
  * or gather version areas its peers never wrote. Init aborts when the PEs'
  * environment settings differ; SHMEM_DEBUG=1 also checks every call (below).
  * With 2 PEs, floating-point sum and product are computed once (a + b is
- * b + a) and both PEs get the same bits; where both operands are NaNs with
- * different payloads, the reference's PE 1 would keep its own operand's
- * payload (x86 SSE returns the first operand's), so the payload -- not the
- * NaN-ness -- may differ from the reference's there (tests/_compare.py
- * compares NaN with NaN whatever the payload).
+ * b + a) and both PEs get the same bits; for float and double (and their
+ * complex types), where both operands are NaNs with different payloads, the
+ * reference's PE 1 would keep its own operand's payload (x86 SSE returns the
+ * first operand's), so the payload -- not the NaN-ness -- may differ from the
+ * reference's there (tests/_compare.py compares those NaNs whatever the
+ * payload). Long double is exact, payloads included: the x87 picks between
+ * two NaNs by their kind and significand, not by operand position.
  *
  * SHMEM_DEBUG=1: every *_to_all call (host API and stream-ordered) first
  * exchanges its arguments with the other members of its active set -- op,
