@@ -23,11 +23,13 @@
 constexpr int kIters = 2048;
 constexpr int kPerIter = 16;  // instructions per loop iteration (8 chains x 2)
 
-enum Kind { ADD32, XOR32, SHL64, ADDC, CNDMASK, CMP64, MIX, MAD64, MULLO, MULHI, MOV, ADD32_E64, XOR32_E64, NKIND };
+enum Kind { ADD32, XOR32, SHL64, ADDC, CNDMASK, CMP64, MIX, MAD64, MULLO, MULHI, MOV, ADD32_E64, XOR32_E64,
+            CNDMASK_VCC, CMP32, CNDMASK_VCC_STATIC, NKIND };
 static const char *kNames[NKIND] = {"v_add_u32", "v_xor_b32", "v_lshlrev_b64", "v_add_co+v_addc_co",
                                     "v_cndmask_b32(sgpr mask)", "v_cmp_gt_u64(sgpr)", "x87-add mix",
                                     "v_mad_u64_u32", "v_mul_lo_u32", "v_mul_hi_u32", "v_mov_b32",
-                                    "v_add_u32_e64", "v_xor_b32_e64"};
+                                    "v_add_u32_e64", "v_xor_b32_e64", "v_cndmask_b32_e32(vcc)", "v_cmp_gt_u32(sgpr)",
+                                    "v_cndmask_b32_e32(vcc set before the loop)"};
 
 template <int K>
 __global__ __launch_bounds__(256) void rate(uint64_t *out, uint64_t *cyc, uint32_t seed) {
@@ -35,6 +37,8 @@ __global__ __launch_bounds__(256) void rate(uint64_t *out, uint64_t *cyc, uint32
              a6 = a0 * 17, a7 = a0 * 19;
     uint64_t b0 = a0, b1 = a1, b2 = a2, b3 = a3, b4 = a4, b5 = a5, b6 = a6, b7 = a7;
     const uint32_t k = seed | 1;
+    if constexpr (K == CNDMASK_VCC_STATIC)
+        asm volatile("v_cmp_gt_u32 vcc, %0, %1\n\ts_nop 4" : : "v"(a0), "v"(k) : "vcc");
     uint64_t t0;
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0));
     for (int it = 0; it < kIters; ++it) {
@@ -96,6 +100,28 @@ __global__ __launch_bounds__(256) void rate(uint64_t *out, uint64_t *cyc, uint32
 #define OP2(x) asm volatile("v_xor_b32_e64 %0, %0, %1\n\tv_xor_b32_e64 %0, %0, %1" : "+v"(x) : "v"(k))
             OP2(a0); OP2(a1); OP2(a2); OP2(a3); OP2(a4); OP2(a5); OP2(a6); OP2(a7);
 #undef OP2
+        } else if constexpr (K == CNDMASK_VCC) {
+            // the VOP2 form: the lane mask in VCC, written once per iteration
+            asm volatile("v_cmp_gt_u32 vcc, %0, %1" : : "v"(a0), "v"(k) : "vcc");
+#define OP2(x) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc\n\tv_cndmask_b32_e32 %0, %1, %0, vcc" \
+                            : "+v"(x) : "v"(k) : "vcc")
+            OP2(a1); OP2(a2); OP2(a3); OP2(a4); OP2(a5); OP2(a6); OP2(a7); OP2(a0);
+#undef OP2
+        } else if constexpr (K == CNDMASK_VCC_STATIC) {
+            // VCC read only, written once before the timed loop
+#define OP2(x) asm volatile("v_cndmask_b32_e32 %0, %0, %1, vcc\n\tv_cndmask_b32_e32 %0, %1, %0, vcc" \
+                            : "+v"(x) : "v"(k))
+            OP2(a1); OP2(a2); OP2(a3); OP2(a4); OP2(a5); OP2(a6); OP2(a7); OP2(a0);
+#undef OP2
+        } else if constexpr (K == CMP32) {
+            uint64_t m0, m1;
+#define OP2(x, y) asm volatile("v_cmp_gt_u32 %0, %2, %3\n\tv_cmp_gt_u32 %1, %3, %2" : "=s"(m0), "=s"(m1) \
+                               : "v"(x), "v"(y))
+            OP2(a0, a1); OP2(a2, a3); OP2(a4, a5); OP2(a6, a7);
+            OP2(a1, a2); OP2(a3, a4); OP2(a5, a6); OP2(a7, a0);
+#undef OP2
+            a0 ^= (uint32_t)m0;
+            a1 ^= (uint32_t)m1;
         } else if constexpr (K == MOV) {
 #define OP2(x, y) asm volatile("v_mov_b32 %0, %1\n\tv_mov_b32 %1, %0" : "+v"(x), "+v"(y))
             OP2(a0, a1); OP2(a2, a3); OP2(a4, a5); OP2(a6, a7);
@@ -190,5 +216,8 @@ int main(int argc, char **argv) {
     sweep<MOV>(argc, argv, cus);
     sweep<ADD32_E64>(argc, argv, cus);
     sweep<XOR32_E64>(argc, argv, cus);
+    sweep<CNDMASK_VCC>(argc, argv, cus);
+    sweep<CMP32>(argc, argv, cus);
+    sweep<CNDMASK_VCC_STATIC>(argc, argv, cus);
     return 0;
 }
