@@ -131,7 +131,7 @@ def cpu_baseline(S, n_gpus, budget_s):
 
 
 def fused_same_gpu(npes, calls, persistent=False):
-    """The fused one-launch schedule (fused.hip), which every call up to 1 MiB
+    """The fused one-launch schedule (fused.hip), which every call up to 2 MiB
     per PE takes at N > 1, measured on this box's one GPU: `npes` PE processes
     of tools/fused_bench.py sharing it (started from this process before it
     touches the GPU). Per-call time for BASELINE config 5's 64 KiB calls
@@ -991,7 +991,7 @@ def main():
     # the same calls per message size with the fused path forced on (fused_max
     # 1 GiB) and off (0, the multi-launch schedule), and one-shot vs two-shot
     # inside the fused kernel: the data to set SHMEM_FUSED_MAX_BYTES /
-    # SHMEM_ONESHOT_MAX_BYTES from one GPU per PE (defaults 1 MiB / 64 KiB were
+    # SHMEM_ONESHOT_MAX_BYTES from one GPU per PE (defaults 2 MiB / 64 KiB were
     # set with the PEs sharing one GPU)
     threshold_sweep = None
     if npes > 1 and not args.host and not args.no_threshold_sweep and not rccl_fallback:
