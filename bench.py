@@ -375,6 +375,8 @@ KERNEL_LEGS = [
     # long double (x87 arithmetic in software, x80.h): the sum is VALU-bound, the product HBM-bound
     ("rs_shard_n8_longdouble_sum", "combine_orders_vec<sum,x80,8>", "sum", "longdouble", 8, 32 << 20, True),
     ("rs_shard_n8_longdouble_prod", "combine_orders_vec<prod,x80,8>", "prod", "longdouble", 8, 32 << 20, True),
+    # float complex product (C99 Annex G multiply; one wave vote on its recovery case)
+    ("rs_shard_n8_complexf_prod", "combine_orders_vec<prod,cplxf,8>", "prod", "complexf", 8, 32 << 20, True),
 ]
 # the long double legs' VALU floor: their per-element instruction streams in
 # this build priced at the measured issue rates -- computed by the library's
@@ -435,6 +437,10 @@ def kernel_legs(shm, reps, check):
             lds = [hosts[p][:n].astype(np.longdouble) for p in range(k)]
             for p in range(k):
                 shm.put(srcs[p], lds[p])
+        if dtype == "complexf":     # finite complex operands of magnitude ~1 (products stay finite)
+            lds = [(hosts[p][:n] + 1j * hosts[p][n:2 * n]).astype(np.complex64) * np.float32(2) for p in range(k)]
+            for p in range(k):
+                shm.put(srcs[p], lds[p])
 
         def launch():
             if orders:
@@ -459,7 +465,7 @@ def kernel_legs(shm, reps, check):
         ck = "skipped"
         if check:
             idx = np.unique(np.random.default_rng(5).integers(0, n, 1 << 14))
-            if dtype == "longdouble":
+            if dtype in ("longdouble", "complexf"):
                 samp = [np.ascontiguousarray(x[idx]) for x in lds]
             else:
                 samp = [np.ascontiguousarray(h.view(np.uint8)[:nbytes].view(shmem_reduce.NP[dtype])[idx])

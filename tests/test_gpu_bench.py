@@ -81,7 +81,7 @@ def test_bench_one_gpu_line():
     k = d["kernels"]
     for name in ("fold_k2_double_sum", "fold_k8_double_sum", "rs_shard_n8_double_sum", "fold_k8_float_max",
                  "fold_k8_longlong_and", "rs_shard_n8_float_max", "rs_shard_n8_longdouble_sum",
-                 "rs_shard_n8_longdouble_prod"):
+                 "rs_shard_n8_longdouble_prod", "rs_shard_n8_complexf_prod"):
         assert k[name]["check"].startswith("bit-exact"), (name, k[name])
         assert 0 < k[name]["frac"] < 1.2 and k[name]["kernel_avg_us"] > 0, (name, k[name])
     # the x87 sum's own roofline: VALU issue, from this build's instruction stream

@@ -39,6 +39,7 @@ kernel_fold_k8_longlong_and combine_vec<2,~long,~8, 1000
 kernel_rs_shard_n8_float_max combine_orders_vec<6,~float,~8, 1000
 kernel_rs_shard_n8_longdouble_sum combine_orders_vec<0,~x80,~8, 1000
 kernel_rs_shard_n8_longdouble_prod combine_orders_vec<1,~x80,~8, 1000
+kernel_rs_shard_n8_complexf_prod combine_orders_vec<1,~mi355::cplxf,~8, 1000
 EOF
 cp "$(find "$OUT/trace" -name '*kernel_stats.csv' -print -quit)" "$DST/rocprof_kernel_stats_bench_n1.csv"
 cp "$(find "$OUT/fetch" -name '*counter_collection.csv' -print -quit)" "$DST/pmc/fetch_size_counter_collection.csv"
