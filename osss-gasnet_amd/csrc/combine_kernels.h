@@ -38,6 +38,9 @@
 #ifndef MI355_CPLX_VOTE
 #define MI355_CPLX_VOTE 1
 #endif
+#ifndef MI355_ALU_GRID_DYNAMIC
+#define MI355_ALU_GRID_DYNAMIC 1
+#endif
 
 namespace mi355k {
 
@@ -735,9 +738,15 @@ int launch_orders_fixed(void *const *dsts, const void *const *srcs, size_t n, hi
         for (int k = 0; k < NSRC; ++k) all = all && dsts[k] != nullptr;
         auto k = all ? combine_orders_vec<OP, T, NSRC, S::unroll, S::policy, true>
                      : combine_orders_vec<OP, T, NSRC, S::unroll, S::policy, false>;
-        const int bpc = !S::alu_heavy || S::blocks_per_cu < resident_blocks((const void *)k)
-                            ? S::blocks_per_cu
-                            : resident_blocks((const void *)k);
+        int bpc = !S::alu_heavy || S::blocks_per_cu < resident_blocks((const void *)k)
+                      ? S::blocks_per_cu
+                      : resident_blocks((const void *)k);
+#if MI355_ALU_GRID_DYNAMIC
+        // the ALU-heavy folds (x87, complex products): one vector per lane,
+        // every block queued at once, so the hardware hands out the last
+        // round's work as slots free instead of a resident grid's fixed rounds
+        if (S::alu_heavy || S::cplx) bpc = 1 << 20;
+#endif
         const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, bpc);
         return launch(k, dim3(grid), st, p);
     }
