@@ -41,6 +41,9 @@
 #ifndef MI355_ALU_GRID_DYNAMIC
 #define MI355_ALU_GRID_DYNAMIC 1
 #endif
+#ifndef MI355_ALU_GRID_DYNAMIC_FOLD
+#define MI355_ALU_GRID_DYNAMIC_FOLD 0
+#endif
 
 namespace mi355k {
 
@@ -697,9 +700,12 @@ int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, b
         p.nvec = n / V;
         p.tail = (uint32_t)(n % V);
         auto k = combine_vec<OP, T, NSRC, S::unroll, S::policy>;
-        const int bpc = !S::alu_heavy || S::blocks_per_cu < resident_blocks((const void *)k)
-                            ? S::blocks_per_cu
-                            : resident_blocks((const void *)k);
+        int bpc = !S::alu_heavy || S::blocks_per_cu < resident_blocks((const void *)k)
+                      ? S::blocks_per_cu
+                      : resident_blocks((const void *)k);
+#if MI355_ALU_GRID_DYNAMIC_FOLD
+        if (S::alu_heavy) bpc = 1 << 20;  // as in launch_orders_fixed below
+#endif
         const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, bpc);
         return launch(k, dim3(grid), st, p, final);
     }

@@ -20,7 +20,7 @@ import oracle  # noqa: E402
 import shmem_reduce  # noqa: E402
 
 SHARD = 32 << 20
-K = 8
+K = int(os.environ.get("ORDERS_SWEEP_SOURCES", "8"))   # sources (the N = K shape)
 
 
 def values(rng, dtype, n):
