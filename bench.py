@@ -15,9 +15,11 @@ ran (shmemx_last_call_info: its name as rocprofv3 prints it, its sources,
 outputs and bytes), its algorithmic bytes per launch / its average duration
 from HIP events recorded by the library on its own stream.
 cpu_baseline: the reference algorithm restated in C (oracle/liboracle.so) as
-max(2, N) PE processes, one pinned host core each, on a bounded sample, run
-by rank 0 before any rank's PE joins the job (the other ranks wait in the
-bootstrap), at every N.
+N PE processes (the headline's shape; 1 PE on 1 core at N = 1), one pinned
+host core each, on a bounded sample, run by rank 0 before any rank's PE joins
+the job (the other ranks wait in the bootstrap), at every N; vs_cpu_baseline
+= value / cpu_baseline.value (vs_baseline stays null: BASELINE.md holds no
+published number for this metric).
 """
 import argparse
 import contextlib
@@ -39,6 +41,9 @@ HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md, chip table)
 XGMI_LINK_GBS = 153.0      # per link, 7 links per GPU (AMD's per-link figure)
 XGMI_LINK_DIR_GBS = 76.8   # one direction of a link, if 153.6 counts both directions (as MI300X's 128 = 2 x 64)
 GIB = float(1 << 30)
+# headline_rotating: disjoint source/target pairs taken in turn; 5 x 2 x 256
+# MiB = 2.5 GiB of footprint, ~10x the 256 MiB Infinity Cache
+ROT_PAIRS = 5
 
 
 def synth(pe, idx):
@@ -81,15 +86,15 @@ def cpu_baseline(S, n_gpus, budget_s):
     """The reference algorithm (reduce-op.c:226-266 restated in C,
     oracle/reduce_oracle.c: copy loop, barrier, 64-element pWrk chunks folded
     with one indirect operator call per element, barrier) on this box's host
-    cores, in this run, before the GPU is touched: N = max(2, n_gpus) forked
-    PE processes, each pinned to a CPU of its own (the third allowed CPU on:
-    CPU 0 takes most interrupts), shared-memory transport. Bounded sample: as
-    many calls as fit in about budget_s. Sub-records: the 1-PE call (the N = 1
-    headline's workload), 8 PEs (SURVEY 8d's N in {2, 8}; BASELINE config 3's
-    shape), BASELINE config 1 (int sum, 2 PEs, 4 KiB) and config 5's call
-    (64 KiB double sum at 8 PEs)."""
+    cores, in this run, before the GPU is touched: forked PE processes, each
+    pinned to a CPU of its own (the third allowed CPU on: CPU 0 takes most
+    interrupts), shared-memory transport. Bounded sample: as many calls as fit
+    in about budget_s. `value` has the headline's own shape: n_gpus PEs x S
+    (at N = 1 one PE on one core). Sub-records: the other PE counts of SURVEY
+    8d (2 and 8 PEs; 8 = BASELINE config 3's shape), the 1-PE call at N > 1,
+    BASELINE config 1 (int sum, 2 PEs, 4 KiB) and config 5's call (64 KiB
+    double sum at 8 PEs)."""
     import oracle
-    npes = max(2, n_gpus)
     n = S // 8
 
     def timed(op, dtype, pes, nel, share):
@@ -98,12 +103,11 @@ def cpu_baseline(S, n_gpus, budget_s):
         t, cpus = oracle.cpu_baseline(op, dtype, pes, nel, 1, reps)
         return t, reps, cpus
 
-    t, reps, cpus = timed("sum", "double", npes, n, 0.4 * budget_s)
-    t1, reps1, cpus1 = timed("sum", "double", 1, n, 0.2 * budget_s)
-    if npes == 8:   # the headline's own N: the same run
-        t8, reps8, cpus8 = t, reps, cpus
-    else:
-        t8, reps8, cpus8 = timed("sum", "double", 8, n, 0.25 * budget_s)
+    runs = {}   # PE count -> (t, reps, cpus)
+    runs[n_gpus] = timed("sum", "double", n_gpus, n, 0.4 * budget_s)
+    for pes, share in ((1, 0.15), (2, 0.15), (8, 0.15)):
+        if pes not in runs:
+            runs[pes] = timed("sum", "double", pes, n, share * budget_s)
     tc, repsc, cpusc = timed("sum", "int", 2, 1024, 0.05 * budget_s)
     t5, reps5, cpus5 = timed("sum", "double", 8, 8192, 0.1 * budget_s)
     try:
@@ -111,23 +115,31 @@ def cpu_baseline(S, n_gpus, budget_s):
     except AttributeError:
         allowed = None
     mib = S >> 20
-    return {"value": round(npes * S / t / GIB, 4), "unit": "GiB/s", "cores": npes, "kind": "port",
-            "sample": f"{reps} calls of shmem_double_sum_to_all's reference algorithm (restated in C, "
-                      f"oracle/reduce_oracle.c) on {npes} PE processes x {mib} MiB, one pinned core each "
-                      f"(CPUs {cpus}); median per call {t * 1e3:.1f} ms, max over PEs; whole-job GiB/s",
-            "ms_per_call": round(t * 1e3, 3), "per_pe_gib_s": round(S / t / GIB, 4),
-            "one_pe": {"value": round(S / t1 / GIB, 4), "cores": 1, "calls": reps1, "ms_per_call": round(t1 * 1e3, 3),
-                       "cpus": cpus1, "note": f"1 PE x {mib} MiB: the N = 1 headline's workload"},
-            "eight_pe": {"value": round(8 * S / t8 / GIB, 4), "cores": 8, "calls": reps8,
-                         "ms_per_call": round(t8 * 1e3, 3), "per_pe_gib_s": round(S / t8 / GIB, 4), "cpus": cpus8,
-                         "note": f"8 PEs x {mib} MiB (BASELINE config 3's shape on host cores), whole-job GiB/s"},
-            "config1": {"workload": "shmem_int_sum_to_all, 2 PEs, 4 KiB (BASELINE config 1; shared-memory "
-                                    "transport in place of GASNet udp/mpi loopback)",
-                        "us_per_call": round(tc * 1e6, 3), "per_pe_gib_s": round(4096 / tc / GIB, 4), "calls": repsc,
-                        "cores": 2, "cpus": cpusc},
-            "config5": {"workload": "shmem_double_sum_to_all, 8 PEs, 64 KiB per call (BASELINE config 5's call)",
-                        "us_per_call": round(t5 * 1e6, 3), "calls": reps5, "cores": 8, "cpus": cpus5},
-            "host": {"nproc": os.cpu_count(), "allowed_cpus": allowed, "cpu_model": cpu_model()}}
+    t, reps, cpus = runs[n_gpus]
+
+    def sub(pes, note):
+        tp, rp, cp = runs[pes]
+        return {"value": round(pes * S / tp / GIB, 4), "cores": pes, "calls": rp, "ms_per_call": round(tp * 1e3, 3),
+                "per_pe_gib_s": round(S / tp / GIB, 4), "cpus": cp, "note": note}
+    out = {"value": round(n_gpus * S / t / GIB, 4), "unit": "GiB/s", "cores": n_gpus, "kind": "port",
+           "sample": f"{reps} calls of shmem_double_sum_to_all's reference algorithm (restated in C, "
+                     f"oracle/reduce_oracle.c) on {n_gpus} PE process{'es' if n_gpus > 1 else ''} x {mib} MiB, "
+                     f"one pinned core each (CPUs {cpus}); median per call {t * 1e3:.1f} ms, max over PEs; "
+                     f"whole-job GiB/s, the headline's shape",
+           "ms_per_call": round(t * 1e3, 3), "per_pe_gib_s": round(S / t / GIB, 4)}
+    for pes, key in ((1, "one_pe"), (2, "two_pe"), (8, "eight_pe")):
+        if pes != n_gpus:
+            out[key] = sub(pes, f"{pes} PE{'s' if pes > 1 else ''} x {mib} MiB, whole-job GiB/s"
+                           + (" (BASELINE config 3's shape on host cores)" if pes == 8 else ""))
+    out.update({
+        "config1": {"workload": "shmem_int_sum_to_all, 2 PEs, 4 KiB (BASELINE config 1; shared-memory "
+                                "transport in place of GASNet udp/mpi loopback)",
+                    "us_per_call": round(tc * 1e6, 3), "per_pe_gib_s": round(4096 / tc / GIB, 4), "calls": repsc,
+                    "cores": 2, "cpus": cpusc},
+        "config5": {"workload": "shmem_double_sum_to_all, 8 PEs, 64 KiB per call (BASELINE config 5's call)",
+                    "us_per_call": round(t5 * 1e6, 3), "calls": reps5, "cores": 8, "cpus": cpus5},
+        "host": {"nproc": os.cpu_count(), "allowed_cpus": allowed, "cpu_model": cpu_model()}})
+    return out
 
 
 def fused_same_gpu(npes, calls, persistent=False):
@@ -361,6 +373,68 @@ def host_staged_leg(shm, loop, S, me, npes, k, check):
                     "device-resident. pcie_frac = per-PE S / t against the same run's two-way hipMemcpyAsync rate"}
 
 
+def rotating_leg(shm, S, me, npes, src, dst, k, check):
+    """N = 1: the headline's call, shmem_double_sum_to_all on S bytes, over
+    ROT_PAIRS disjoint (source, target) pairs of the device heap taken in turn
+    (csrc/bench_loop.c shmemb_double_sum_rotating): between two uses of a line
+    (ROT_PAIRS - 1) x 2 S of other traffic goes by, 4x the Infinity Cache, so
+    every call's bytes come from HBM (MI355X_MICROARCH.md: a line stays
+    resident only while the traffic between two uses of it fits in ~256 MiB).
+    The headline loop re-reads ONE pair, whose 512 MiB partly stay on-die: this
+    leg is its HBM-only figure. Timed like the headline (C loop, barrier +
+    device synchronize on both sides), then again with HIP events on every
+    dominant launch; every pair's target checked bit-exact on a sample."""
+    n = S // 8
+    srcs, dsts = [src], [dst]
+    x = synth(me, np.arange(n, dtype=np.uint64))
+    try:
+        for _ in range(ROT_PAIRS - 1):
+            srcs.append(shm.malloc_device(S))
+            dsts.append(shm.malloc_device(S))
+            shm.put(srcs[-1], x)
+        run = shmem_reduce.bench_rotating()
+        k = max(k, 4 * ROT_PAIRS)
+        run(dsts, srcs, n, 0, 0, npes, shm._psync_ptr, 2 * ROT_PAIRS)
+        shm.barrier_all()
+        shm.sync()
+        t0 = time.perf_counter()
+        run(dsts, srcs, n, 0, 0, npes, shm._psync_ptr, k)
+        shm.sync()
+        t = (time.perf_counter() - t0) / k
+        shm.barrier_all()
+        shm.kernel_timing(True)
+        run(dsts, srcs, n, 0, 0, npes, shm._psync_ptr, k)
+        shm.sync()
+        nk, _, k_avg_ms = shm.kernel_timing_stats()
+        shm.kernel_timing(False)
+        info = shm.last_call_info()
+        ck = "skipped"
+        if check:
+            import oracle
+            idx = np.unique(np.random.default_rng(400 + me).integers(0, n, 1 << 14)).astype(np.uint64)
+            want = oracle.reduce_pe("sum", "double", [synth(p, idx) for p in range(npes)], me)
+            bad = 0
+            for d in dsts:
+                got = shm.get(d, n, "double")[idx.astype(np.int64)]
+                bad += int((got.view(np.uint64) != want.view(np.uint64)).sum())
+            ck = (f"bit-exact vs the reference, {len(idx)} samples x {len(dsts)} targets" if bad == 0
+                  else f"MISMATCH in {bad} samples")
+    finally:
+        for d in srcs[1:] + dsts[1:]:
+            shm.free_device(d)
+    alg = info["alg_bytes"] // max(1, info["launches"])
+    kt = k_avg_ms * 1e-3
+    achieved = alg / kt / 1e9 if kt > 0 else 0.0
+    return {"value": round(npes * S / t / GIB, 2), "unit": "GiB/s", "ms_per_step": round(t * 1e3, 4), "steps": k,
+            "pairs": ROT_PAIRS, "footprint_MiB": ROT_PAIRS * 2 * S >> 20, "schedule": info["schedule"],
+            "kernel": info["kernel"], "kernel_avg_us": round(k_avg_ms * 1e3, 2), "launches_timed": nk,
+            "alg_bytes_per_launch": alg, "achieved_GB_s": round(achieved, 1),
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "check": ck,
+            "note": "the headline call over %d disjoint 256 MiB source/target pairs taken in turn (%d MiB "
+                    "footprint): every call streams from HBM; the headline re-reads one pair, part of which "
+                    "the 256 MiB Infinity Cache serves" % (ROT_PAIRS, ROT_PAIRS * 2 * S >> 20)}
+
+
 # ---------------------------------------------------------------------------
 # kernel legs (N = 1): the fold kernels themselves, timed on one GPU
 # ---------------------------------------------------------------------------
@@ -377,7 +451,14 @@ KERNEL_LEGS = [
     ("rs_shard_n8_longdouble_prod", "combine_orders_vec<prod,x80,8>", "prod", "longdouble", 8, 32 << 20, True),
     # float complex product (C99 Annex G multiply; one wave vote on its recovery case)
     ("rs_shard_n8_complexf_prod", "combine_orders_vec<prod,cplxf,8>", "prod", "complexf", 8, 32 << 20, True),
+    # what each GPU folds in BASELINE config 4's longlong and at N = 8: 8 shards of 8 MiB (64 MiB / 8);
+    # bitwise and is order-free, so the P2P schedule runs the plain fold, one output per shard
+    ("rs_shard_n8_longlong_and", "combine_vec<and,longlong,8>", "and", "longlong", 8, 8 << 20, False),
 ]
+# each leg is timed twice: warm (the same buffers every launch, as the leg's
+# own loop re-reads them) and cold (rotating disjoint buffer sets, >= 2 GiB of
+# footprint, so no byte is still in the 256 MiB Infinity Cache)
+COLD_FOOTPRINT = 2304 << 20
 # the long double legs' VALU floor: their per-element instruction streams in
 # this build priced at the measured issue rates -- computed by the library's
 # build (csrc/Makefile, tools/valu_floor.py --bench-legs) into lib/valu_floor.json;
@@ -462,6 +543,53 @@ def kernel_legs(shm, reps, check):
         t = float(np.mean(ts))
         alg = (k + nout) * nbytes
         gbs = alg / t / 1e9
+        # cold: `sets` disjoint copies of the leg's buffers taken in turn
+        set_bytes = (k + nout) * nbytes
+        sets = max(1, -(-COLD_FOOTPRINT // set_bytes))
+        cold_bufs = []
+        if sets > 1:
+            pool = dmalloc((sets - 1) * set_bytes)
+            cold_bufs.append(pool)
+            for j in range(sets - 1):
+                base = pool + j * set_bytes
+                for q in range(k):   # the same source bytes as set 0
+                    if L.hipMemcpy(vp(base + q * nbytes), vp(srcs[q]), ctypes.c_size_t(nbytes), 3) != 0:
+                        raise RuntimeError("hipMemcpy failed")
+
+        def launch_set(j):
+            if j == 0:
+                return launch()
+            base = cold_bufs[0] + (j - 1) * set_bytes
+            cs = [base + q * nbytes for q in range(k)]
+            co = [base + (k + q) * nbytes for q in range(nout)]
+            if orders:
+                return shm.combine_orders(op, dtype, co, cs, n)
+            return shm.combine(op, dtype, co[0], cs, n)
+
+        creps = max(2 * sets, min(reps, 20)) if sets > 1 else min(reps, 20)
+        cev = [vp() for _ in range(2 * creps)]
+        for e in cev:
+            L.hipEventCreate(ctypes.byref(e))
+        for j in range(sets):
+            assert launch_set(j) == 0
+        shm.sync()
+        for r in range(creps):
+            L.mi355_time_next_launch(cev[2 * r], cev[2 * r + 1])
+            assert launch_set(r % sets) == 0
+        shm.sync()
+        cts = []
+        for r in range(creps):
+            ms = ctypes.c_float()
+            L.hipEventElapsedTime(ctypes.byref(ms), cev[2 * r], cev[2 * r + 1])
+            cts.append(ms.value * 1e-3)
+        for e in cev:
+            L.hipEventDestroy(e)
+        for b in cold_bufs:
+            L.hipFree(vp(b))
+        tc = float(np.mean(cts))
+        cold = {"kernel_avg_us": round(tc * 1e6, 2), "achieved_GB_s": round(alg / tc / 1e9, 1),
+                "frac": round(alg / tc / 1e9 / HBM_PEAK_GBS, 4), "sets": sets, "launches": creps,
+                "footprint_MiB": sets * set_bytes >> 20}
         ck = "skipped"
         if check:
             idx = np.unique(np.random.default_rng(5).integers(0, n, 1 << 14))
@@ -480,7 +608,8 @@ def kernel_legs(shm, reps, check):
         res[name] = {"kernel": kname, "sources": k, "outputs": nout, "bytes_per_source": nbytes,
                      "alg_bytes_per_launch": alg, "kernel_avg_us": round(t * 1e6, 2),
                      "kernel_median_us": round(float(np.median(ts)) * 1e6, 2), "launches": reps,
-                     "achieved_GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "check": ck}
+                     "achieved_GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "check": ck,
+                     "cold": cold}
         if dtype == "longdouble":
             try:
                 fl = json.load(open(VALU_FLOOR))[name]
@@ -500,7 +629,9 @@ def kernel_legs(shm, reps, check):
     for d in srcs + outs:
         L.hipFree(vp(d))
     res["note"] = ("fold kernels timed alone (HIP event pair per launch on its stream), algorithmic bytes = "
-                   "(sources + outputs) x bytes; frac against the 8 TB/s HBM peak")
+                   "(sources + outputs) x bytes; frac against the 8 TB/s HBM peak; warm = the same buffers every "
+                   "launch (a set under ~256 MiB stays in the Infinity Cache), cold = disjoint copies taken in "
+                   "turn over >= 2 GiB: every byte from HBM")
     return res
 
 
@@ -532,6 +663,8 @@ def main():
     ap.add_argument("--no-link-probe", action="store_true",
                     help="N > 1: skip PE 0's one-peer-at-a-time shmem_getmem / shmem_putmem rates")
     ap.add_argument("--kernel-reps", type=int, default=50)
+    ap.add_argument("--no-rotating", action="store_true",
+                    help="N = 1: skip headline_rotating (the same call over %d disjoint pairs, HBM-only)" % ROT_PAIRS)
     ap.add_argument("--no-fused", action="store_true",
                     help="N = 1: skip the fused-kernel leg (2 PE processes sharing this GPU, 64 KiB and 1 MiB calls)")
     ap.add_argument("--host", action="store_true",
@@ -547,7 +680,11 @@ def main():
     args = ap.parse_args()
 
     # wall time of every leg (legs_s in the line), and optional legs that fail
-    # become an {"error": ...} entry instead of ending the headline line
+    # become an {"error": ...} entry instead of ending the headline line. A leg
+    # that makes collective calls is optional only with one PE: at N > 1 a PE
+    # that raised and went on would pair its next collective call with a
+    # different call on its peers (a hang or a barrier-timeout abort), so
+    # there it ends the run; such legs pass optional=solo.
     legs_s, leg_errors = {}, {}
 
     @contextlib.contextmanager
@@ -601,7 +738,9 @@ def main():
             fused_p = fused_same_gpu(2, 4096 if args.no_small is False else 512, persistent=True)
     t_init0 = time.perf_counter()
 
-    os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(2 * S + (64 << 20)))
+    # N = 1: room for headline_rotating's extra pairs too
+    pairs = ROT_PAIRS if world == 1 and not args.host and not args.no_rotating else 1
+    os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(2 * S * pairs + (64 << 20)))
     os.environ.setdefault("SHMEM_DEVICE_SCRATCH_SIZE", str(96 << 20))
     # a PE that never arrives ends the bench within two minutes with the
     # library's diagnostic (the library default, 600 s, suits long jobs)
@@ -620,6 +759,7 @@ def main():
         and args.algorithm != "rccl"
     shm.set_algorithm(args.algorithm)
     me, npes = shm.my_pe(), shm.n_pes()
+    solo = npes == 1
     # the init-time coherence test of peer-heap reads (runtime.c): on the
     # driver's 8-GPU node it proves or refutes the acquire protocol the P2P
     # schedules rely on
@@ -695,10 +835,16 @@ def main():
     t_calls = call_times(dst, src, n, 0, 0, npes, shm._psync_ptr, args.steps)
     legs_s["headline"] = round(time.perf_counter() - t_head0, 2)
 
+    # N = 1: the same call with every byte from HBM (rotating_leg)
+    rotating = None
+    if npes == 1 and not args.host and not args.no_rotating:
+        with timed_leg("headline_rotating"):
+            rotating = rotating_leg(shm, S, me, npes, src, dst, args.steps, not args.no_check)
+
     # the many-small-bucket regime (BASELINE config 5 shape: 64 KiB per call)
     small_n, small_calls = 8192, 0 if args.no_small else 4096   # BASELINE config 5: 4096 x 64 KiB
     t_small = None
-    with timed_leg("small_call"):
+    with timed_leg("small_call", optional=solo):
         if small_calls:
             steps(20, small_n)
             shm.barrier_all()
@@ -745,7 +891,7 @@ def main():
     # them captured once into a HIP graph and the graph replayed: how a caller
     # that batches small buckets into a graph (e.g. torch.cuda.graph) sees
     # them; the graph launch and its wait amortised over its 64 calls.
-    with timed_leg("small_call_graph"):
+    with timed_leg("small_call_graph", optional=solo):
         small_graph = None
         if small_calls and not args.host and not rccl_fallback:
             per_graph, replays = 64, max(1, small_calls // 64)
@@ -943,7 +1089,7 @@ def main():
     # BASELINE config 4 (op coverage): shmem_float_max_to_all and
     # shmem_longlong_and_to_all on 64 MiB per PE, timed like the headline
     # (C loop, max over PEs) and checked bit-exact on a sample
-    with timed_leg("op_coverage"):
+    with timed_leg("op_coverage", optional=solo):
         ops = None
         if not args.no_ops and not args.host:
             import oracle
@@ -1001,7 +1147,7 @@ def main():
     # set with the PEs sharing one GPU)
     threshold_sweep = None
     if npes > 1 and not args.host and not args.no_threshold_sweep and not rccl_fallback:
-        with timed_leg("threshold_sweep"):
+        with timed_leg("threshold_sweep", optional=solo):
             import oracle
             f0, o0 = shm.thresholds()
 
@@ -1024,22 +1170,23 @@ def main():
                 return round(t * 1e6, 2), sched, bad
 
             shm.put(src, synth(me, np.arange(n, dtype=np.uint64)))  # the op-coverage leg rewrote src
-            rows, bad_total = [], 0
-            for nb in (64 << 10, 256 << 10, 1 << 20, 2 << 20, 4 << 20, 8 << 20):
-                fu, fs, b1 = per_call(nb // 8, 1 << 30, o0)
-                mu, ms, b2 = per_call(nb // 8, 0, o0)
-                bad_total += b1 + b2
-                rows.append({"bytes": nb, "fused_us": fu, "fused_schedule": fs, "multi_launch_us": mu,
-                             "multi_launch_schedule": ms})
-            oneshot = []
-            for nb in (16 << 10, 64 << 10, 256 << 10):
-                ou, osch, b1 = per_call(nb // 8, 1 << 30, 1 << 30)
-                tu, tsch, b2 = per_call(nb // 8, 1 << 30, 0)
-                bad_total += b1 + b2
-                oneshot.append({"bytes": nb, "oneshot_us": ou, "oneshot_schedule": osch, "twoshot_us": tu,
-                                "twoshot_schedule": tsch})
-            shm.set_fused_max(f0)
-            shm.set_oneshot_max(o0)
+            rows, bad_total, oneshot = [], 0, []
+            try:
+                for nb in (64 << 10, 256 << 10, 1 << 20, 2 << 20, 4 << 20, 8 << 20):
+                    fu, fs, b1 = per_call(nb // 8, 1 << 30, o0)
+                    mu, ms, b2 = per_call(nb // 8, 0, o0)
+                    bad_total += b1 + b2
+                    rows.append({"bytes": nb, "fused_us": fu, "fused_schedule": fs, "multi_launch_us": mu,
+                                 "multi_launch_schedule": ms})
+                for nb in (16 << 10, 64 << 10, 256 << 10):
+                    ou, osch, b1 = per_call(nb // 8, 1 << 30, 1 << 30)
+                    tu, tsch, b2 = per_call(nb // 8, 1 << 30, 0)
+                    bad_total += b1 + b2
+                    oneshot.append({"bytes": nb, "oneshot_us": ou, "oneshot_schedule": osch, "twoshot_us": tu,
+                                    "twoshot_schedule": tsch})
+            finally:   # the thresholds in force for any later call, whatever happened
+                shm.set_fused_max(f0)
+                shm.set_oneshot_max(o0)
             wins = [r["bytes"] for r in rows if r["fused_us"] < r["multi_launch_us"]]
             threshold_sweep = {
                 "fused_vs_multi_launch": rows, "oneshot_vs_twoshot": oneshot,
@@ -1068,6 +1215,16 @@ def main():
                     "kernel_avg_us": round(k_avg_ms * 1e3, 2),
                     "launches_timed": nk, "ms_per_step_with_events": round(t_local_ev / args.steps * 1e3, 4),
                     "call": sched}
+        if rotating and "frac" in rotating:
+            # which figure is HBM: the timed region re-reads one pair, the
+            # rotating leg streams every byte from HBM
+            roofline["hbm_only"] = {k: rotating[k] for k in ("kernel_avg_us", "achieved_GB_s", "frac",
+                                                             "footprint_MiB", "launches_timed")}
+            roofline["attribution"] = (
+                "frac is the timed region's: the same 256 MiB source/target pair every call (512 MiB per call), "
+                "part of which the 256 MiB Infinity Cache serves, so it is a device-memory rate, not HBM alone; "
+                "hbm_only is the same kernel over %d disjoint pairs taken in turn (headline_rotating, %d MiB "
+                "footprint): every byte from HBM" % (ROT_PAIRS, rotating["footprint_MiB"]))
     else:
         # N > 1: the reduce-scatter fold reads N-1 of its N shard sources from
         # peers over xGMI, so its bound is the links into this GPU: achieved =
@@ -1095,24 +1252,28 @@ def main():
                                                                  "this PE's target shard")}}
         if shared_gpu:
             # PEs sharing ONE GPU (test layout): the 'remote' reads are this
-            # GPU's own HBM, so the bound is HBM; the link view is kept aside
+            # GPU's own HBM, so the bound is HBM; the link view is kept aside.
+            # The device rate counts every PE's fold bytes on this GPU over a
+            # window that holds all of their launches: each call's wall time
+            # (t_step, max over PEs) -- every PE's folds ran between the
+            # call's first entry and its last return, so this is a lower
+            # bound on the rate the folds achieved together (<= 1 of HBM by
+            # construction). One launch's own rate is kept as per_launch_*.
             xv = {k: roofline.pop(k) for k in ("bound", "achieved", "peak", "frac", "alg_bytes_per_launch",
                                                "peak_note")}
             h = roofline.pop("hbm")
-            # the PEs' folds run at once (they start after the same device
-            # barrier and take the same time), so the GPU's HBM carries
-            # pes_on_gpu launches' bytes in one kernel duration
-            dev = h["achieved"] * pes_on_gpu
+            dev = pes_on_gpu * alg_bytes / t_step / 1e9
             roofline = {"bound": "hbm", "achieved": round(dev, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(dev / HBM_PEAK_GBS, 4), "traffic": None,
                         "alg_bytes_per_launch": h["bytes_per_launch"], "pes_on_gpu": pes_on_gpu,
                         "per_launch_achieved": h["achieved"], "per_launch_frac": h["frac"],
                         **roofline, "hbm_note": h["note"], "xgmi_view": xv,
                         "note": "the PEs share ONE GPU (test layout): every 'remote' read is this GPU's own HBM, "
-                                "so the fold is HBM-bound here; its %d PEs' folds run concurrently, so achieved = "
-                                "%d x one launch's bytes / its duration (per_launch_* = one PE's share); "
-                                "xgmi_view is what the line reports with one GPU per PE (not a link rate here)"
-                                % (pes_on_gpu, pes_on_gpu)}
+                                "so the fold is HBM-bound here; achieved = %d PEs x one call's fold bytes / the "
+                                "call's wall time (max over PEs), a window holding every PE's launches: a lower "
+                                "bound on their combined rate; per_launch_* = one launch's bytes over its own "
+                                "duration; xgmi_view is what the line reports with one GPU per PE (not a link "
+                                "rate here)" % pes_on_gpu}
     roofline["traffic_note"] = traffic_for(roofline, f"n{npes}_{args.mib}mib", args.host)
 
     # N > 1: bus bandwidth of the reduce-scatter + all-gather exchange against
@@ -1171,6 +1332,8 @@ def main():
             "xgmi": xgmi,
             "rccl_compare": rccl,
             "cpu_baseline": cpu,
+            "vs_cpu_baseline": round(npes * S / t_step / GIB / cpu["value"], 1) if cpu and cpu.get("value") else None,
+            "headline_rotating": rotating,
             "small_call": None if t_small is None else
             {"bytes_per_pe": small_n * 8, "us_per_call": round(t_small * 1e6, 2), "calls": small_calls,
              "schedule": small_info["schedule"], "kernel": small_info["kernel"], "check": small_check,

@@ -14,6 +14,14 @@ and manifest.json lists the cases. Inputs include the edge values the path
 must survive: integer overflow, NaN / +-0 / +-Inf / denormals, complex
 Inf/NaN products, x87 denormal / unnormal / NaN encodings.
 
+NaN-payload families golden_nan_<op>_<dtype>.npz (sum/prod of float, double,
+float complex, double complex; manifest "nan_cases"): operands rich in NaNs of
+every sign, payload and quiet/signalling kind, infinities, zeros and values
+whose sums overflow, so that which NaN comes out -- the SSE rule: the first
+NaN operand, quieted, or the negative "indefinite" NaN of an invalid
+operation -- and libgcc's complex-multiply operand order are pinned by the
+reference's compiled code.
+
 Usage: python3 oracle/gen_golden.py [outdir]   (needs oracle/_ref built)
 """
 import json
@@ -29,6 +37,9 @@ import oracle  # noqa: E402
 # (npes, n) cases per pair; n covers 0, 1, chunk edges 63/64/65, 127/128, a
 # few hundred, and npes covers 1,2,3,4,5,8
 CASES = [(1, 65), (2, 300), (3, 127), (4, 64), (8, 130), (2, 0), (5, 1), (8, 63), (3, 128)]
+# the NaN-payload families: npes up to 9 (a fold beyond one launch's 8 sources)
+NAN_CASES = [(2, 515), (3, 257), (5, 130), (8, 300), (9, 67)]
+NAN_PAIRS = [(op, t) for op in ("sum", "prod") for t in ("float", "double", "complexf", "complexd")]
 
 
 def fp_values(rng, n, np_t):
@@ -42,6 +53,41 @@ def fp_values(rng, n, np_t):
     m = rng.random(n) < 0.08
     x[m] = rng.choice(specials, int(m.sum()))
     return x
+
+
+def nan_rich(rng, n, np_t):
+    """Bit patterns of np_t (float32/float64): 35 % NaNs (random sign and
+    payload, quiet or signalling), 10 % +-inf, 10 % +-0, 15 % huge values
+    (their sums overflow: inf - inf later), the rest ordinary numbers."""
+    u_t = np.uint32 if np_t == np.float32 else np.uint64
+    bits = 32 if np_t == np.float32 else 64
+    mbits = 23 if np_t == np.float32 else 52
+    exp_all = u_t(((1 << (bits - 1 - mbits)) - 1) << mbits)
+    quiet = u_t(1 << (mbits - 1))
+    sign = u_t(1 << (bits - 1))
+    x = (rng.uniform(-4, 4, n)).astype(np_t).view(u_t).copy()
+    r = rng.random(n)
+    payload = rng.integers(1, 1 << (mbits - 1), n, dtype=np.uint64).astype(u_t)
+    sgn = np.where(rng.random(n) < 0.5, sign, u_t(0)).astype(u_t)
+    qnan = exp_all | quiet | payload | sgn
+    snan = exp_all | payload | sgn                       # quiet bit clear, payload != 0
+    fi = np.finfo(np_t)
+    huge = (np.where(rng.random(n) < 0.5, fi.max, -fi.max) * rng.uniform(0.5, 1, n)).astype(np_t).view(u_t)
+    x = np.where(r < 0.25, qnan, x)
+    x = np.where((r >= 0.25) & (r < 0.35), snan, x)
+    x = np.where((r >= 0.35) & (r < 0.45), exp_all | sgn, x)    # +-inf
+    x = np.where((r >= 0.45) & (r < 0.55), sgn, x)              # +-0
+    x = np.where((r >= 0.55) & (r < 0.70), huge, x)
+    return x.astype(u_t).view(np_t)
+
+
+def nan_values(rng, dtype, n):
+    if dtype in ("float", "double"):
+        return nan_rich(rng, n, oracle.NP[dtype])
+    base = np.float32 if dtype == "complexf" else np.float64
+    out = np.empty(n, dtype=oracle.NP[dtype])
+    out.real, out.imag = nan_rich(rng, n, base), nan_rich(rng, n, base)
+    return out
 
 
 def int_values(rng, n, np_t, op):
@@ -134,6 +180,21 @@ def main():
             cases.append({"npes": npes, "n": n})
         np.savez_compressed(os.path.join(outdir, f"golden_{op}_{dtype}.npz"), **arrays)
         manifest["cases"][f"{op}_{dtype}"] = cases
+    manifest["nan_cases"] = {}
+    seed = 20261018
+    for op, dtype in NAN_PAIRS:
+        rng = np.random.default_rng(seed)
+        seed += 1
+        arrays = {}
+        cases = []
+        for k, (npes, n) in enumerate(NAN_CASES):
+            srcs = [nan_values(rng, dtype, n) for _ in range(npes)]
+            outs = [oracle.ref_reduce_pe(op, dtype, srcs, me) for me in range(npes)]
+            arrays[f"in_{k}"] = np.stack(srcs)
+            arrays[f"out_{k}"] = np.stack(outs)
+            cases.append({"npes": npes, "n": n})
+        np.savez_compressed(os.path.join(outdir, f"golden_nan_{op}_{dtype}.npz"), **arrays)
+        manifest["nan_cases"][f"{op}_{dtype}"] = cases
     with open(os.path.join(outdir, "manifest.json"), "w") as f:
         json.dump(manifest, f, indent=1)
     print(f"wrote {len(oracle.PAIRS)} fixture files to {outdir}")

@@ -8,9 +8,13 @@
  * compiled unmodified with the reference's own headers. Its static operator
  * functions `<op>_<type>_func` (reduce-op.c:79-158) are reachable from here
  * and are wrapped below in one fold loop per operator:
- *     acc[i] = <op>_<type>_func (acc[i], src[i])
+ *     acc[i] = (*the_op) (acc[i], src[i]),   the_op = <op>_<type>_func
  * -- exactly the call `write_to[ti] = (*the_op)(write_to[ti], pWrk[j])` of
- * reduce-op.c:247-248.
+ * reduce-op.c:247-248, through a pointer gcc cannot see through (volatile),
+ * so the operator runs as the reference's own build runs it: the out-of-line
+ * function, called indirectly. (Inlined into the loop instead, gcc gives the
+ * double complex add its operands in the other order -- same values, another
+ * NaN payload -- so an inlined wrapper would not pin NaN payloads.)
  *
  * What is NOT taken from the reference: its schedule shmemi_udr_*_to_all
  * (:179-276) needs shmem_getmem/shmem_barrier over GASNet, which this image
@@ -25,8 +29,9 @@
 #define REF_FOLD(OpCall, Name, Type)                                              \
     EXPORT void ref_##OpCall##_##Name (Type *acc, const Type *src, long n)         \
     {                                                                             \
+        Type (*volatile the_op) (Type, Type) = OpCall##_##Name##_func;           \
         for (long i = 0; i < n; ++i)                                              \
-            acc[i] = OpCall##_##Name##_func (acc[i], src[i]);                     \
+            acc[i] = (*the_op) (acc[i], src[i]);                                  \
     }
 
 #define REF_ARITH(Name, Type) REF_FOLD (sum, Name, Type) REF_FOLD (prod, Name, Type)

@@ -24,6 +24,18 @@ void shmemb_double_sum_loop (double *target, double *source, int nreduce, int PE
         shmem_double_sum_to_all (target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync);
 }
 
+/* K calls taking npairs disjoint (target, source) pairs in turn: call i
+ * reduces sources[i % npairs] into targets[i % npairs]. With npairs x 2 S
+ * well beyond the 256 MiB Infinity Cache, every call streams its buffers from
+ * HBM (bench.py's headline_rotating leg); otherwise the same call. */
+void shmemb_double_sum_rotating (double **targets, double **sources, int npairs, int nreduce, int PE_start,
+                                 int logPE_stride, int PE_size, double *pWrk, long *pSync, int iters)
+{
+    for (int i = 0; i < iters; ++i)
+        shmem_double_sum_to_all (targets[i % npairs], sources[i % npairs], nreduce, PE_start, logPE_stride,
+                                 PE_size, pWrk, pSync);
+}
+
 /* The same calls, each timed on its own (CLOCK_MONOTONIC, entry to return):
  * us[i] = call i's duration in microseconds. For the distribution (median,
  * tails) beside the bracketed mean of the loop above (median over

@@ -15,36 +15,6 @@
 #include "mi355_reduce.h"
 #include "ops.h"
 
-// Long double every-member fold, build-time forms measured against each other
-// (tools/build_x80_variants.sh): chains kept one after the other by an empty
-// asm dependence, each member's output stored as soon as its chain ends
-// instead of after the wave vote, an occupancy floor (waves per SIMD) for the
-// orders kernels, and non-temporal source loads (the other folds' policy).
-#ifndef MI355_X80_SERIAL_CHAINS
-#define MI355_X80_SERIAL_CHAINS 1
-#endif
-#ifndef MI355_X80_EARLY_STORE
-#define MI355_X80_EARLY_STORE 1
-#endif
-#ifndef MI355_X80_WAVES
-#define MI355_X80_WAVES 0
-#endif
-#ifndef MI355_X80_NT_LOADS
-#define MI355_X80_NT_LOADS 1
-#endif
-// Float complex products in the every-member fold: plain products and one
-// wave vote on Annex G's recovery case instead of its branch after every
-// product.
-#ifndef MI355_CPLX_VOTE
-#define MI355_CPLX_VOTE 1
-#endif
-#ifndef MI355_ALU_GRID_DYNAMIC
-#define MI355_ALU_GRID_DYNAMIC 1
-#endif
-#ifndef MI355_ALU_GRID_DYNAMIC_FOLD
-#define MI355_ALU_GRID_DYNAMIC_FOLD 0
-#endif
-
 namespace mi355k {
 
 using namespace mi355;
@@ -159,7 +129,21 @@ __global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
 #pragma unroll
                 for (int k = 1; k < NSRC; ++k) {
 #pragma unroll
-                    for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[u][k].e[e]);
+                    for (int e = 0; e < V; ++e) acc.e[e] = apply_fast<OP>(acc.e[e], x[u][k].e[e]);
+                }
+                if constexpr (has_fast_form<OP, T>()) {
+                    // a NaN came out somewhere: the reference's operator, step by step
+                    bool redo = false;
+#pragma unroll
+                    for (int e = 0; e < V; ++e) redo |= redo_needed<OP>(acc.e[e]);
+                    if (redo) {
+                        acc = x[u][0];
+#pragma unroll
+                        for (int k = 1; k < NSRC; ++k) {
+#pragma unroll
+                            for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[u][k].e[e]);
+                        }
+                    }
                 }
                 st16_fold(d + i, acc.v);
             }
@@ -259,13 +243,9 @@ template <int NSRC>
 __device__ __forceinline__ void x80_load(const OrdersParams &p, uint64_t i, x80 (&v)[NSRC]) {
 #pragma unroll
     for (int k = 0; k < NSRC; ++k) {
-#if MI355_X80_NT_LOADS
         Pack<x80> w;
         w.v = ld16<POL_NT_LOAD>((const u32x4 *)p.src[k] + i);
         v[k] = w.e[0];
-#else
-        v[k] = ((const x80 *)p.src[k])[i];
-#endif
     }
 }
 
@@ -296,11 +276,9 @@ __device__ __forceinline__ void x80_orders_vector(const OrdersParams &p, uint64_
             continue;
         }
         x80d::xu a = u[q];
-#if MI355_X80_SERIAL_CHAINS
         // one chain after the other: interleaved by the scheduler, the
         // chains' select masks outgrow the SGPRs and spill to VGPR lanes
         if (q > 0) asm volatile("" : "+v"(a.m) : "v"(res[q - 1].m));
-#endif
 #pragma unroll
         for (int j = 0; j + 1 < NSRC; ++j) {
             x80d::xu r;
@@ -309,7 +287,6 @@ __device__ __forceinline__ void x80_orders_vector(const OrdersParams &p, uint64_
             a = r;
         }
         res[q] = a;
-#if MI355_X80_EARLY_STORE
         // the fast result goes out now (its registers free for the next
         // chain); a wave that fails the vote below rewrites every output
         // from the general path (which works from v[], in registers, so an
@@ -321,26 +298,9 @@ __device__ __forceinline__ void x80_orders_vector(const OrdersParams &p, uint64_
             o.e[0] = x80d::pack(a, v[q + w]);
             st16_fold((u32x4 *)p.dst[q + w] + i, o.v);
         }
-#endif
-#if MI355_X80_SERIAL_CHAINS
         asm volatile("" : "+v"(ok));  // a VGPR, not lane masks kept (and spilled) across the chains
-#endif
     }
-#if MI355_X80_EARLY_STORE
     if (__all(ok)) return;
-    if (false) {
-#else
-    if (__all(ok)) {
-#endif
-#pragma unroll
-        for (int q = 0; q < NSRC; ++q) {
-            if (!ALL && p.dst[q] == nullptr) continue;
-            Pack<x80> o;
-            o.e[0] = x80d::pack(res[q], v[q]);
-            st16_fold((u32x4 *)p.dst[q] + i, o.v);
-        }
-        return;
-    }
     x80 first = v[0];
     bool have_first = false;
 #pragma unroll 1
@@ -388,12 +348,29 @@ __device__ __forceinline__ bool single_fold_ok(const T &v) {
     }
 }
 
+// Member q's chain with the reference's operator over one vector of every
+// source held in registers, q a run-time value: operands picked with
+// compile-time indices and selects (q's own vector first, then the others in
+// member order), so the rolled member loop of the rare NaN path indexes no
+// register array (which would live in scratch memory).
+template <int OP, typename T, int NSRC>
+__device__ __forceinline__ Pack<T> member_chain(const Pack<T> (&x)[NSRC], int q) {
+    constexpr int V = 16 / sizeof(T);
+    Pack<T> acc = x[0];
+#pragma unroll
+    for (int k = 1; k < NSRC; ++k) acc.v = q == k ? x[k].v : acc.v;
+#pragma unroll
+    for (int j = 0; j + 1 < NSRC; ++j) {
+        Pack<T> b;
+        b.v = j < q ? x[j].v : x[j + 1].v;
+#pragma unroll
+        for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], b.e[e]);
+    }
+    return acc;
+}
+
 template <int OP, typename T, int NSRC, int UNROLL, int POL, bool ALL>
-__global__ __launch_bounds__(kBlock)
-#if MI355_X80_WAVES
-__attribute__((amdgpu_waves_per_eu(MI355_X80_WAVES)))
-#endif
-void combine_orders_vec(OrdersParams p) {
+__global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
     constexpr int V = 16 / sizeof(T);
     const uint64_t nvec = p.nvec;
     const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
@@ -449,38 +426,14 @@ void combine_orders_vec(OrdersParams p) {
                     continue;
                 }
             }
-#if MI355_CPLX_VOTE
-            if constexpr (OP == MI355_OP_PROD && std::is_same<T, cplxf>::value) {
-                // Annex G's recovery (ops.h cmul) changes a product only when
-                // both parts come out NaN: every member's chain with the plain
-                // products first, each output stored as its chain ends, and
-                // one wave vote on whether any product of any lane hit that
-                // case -- then the wave redoes its chains with cmul (from
-                // registers, so an output aliasing its source is safe) and
-                // rewrites them; the same bits either way. Float only: 8
-                // sources x 32 MiB, 97.5 -> 91.8 us; double complex went the
-                // other way, 87.0 -> 94.0 (profiles/r04/cplx_vote/)
-                int hit = 0;
-#pragma unroll
-                for (int q = 0; q < NSRC; ++q) {
-                    if (!ALL && p.dst[q] == nullptr) continue;
-                    Pack<T> acc = x[u][q];
-#pragma unroll
-                    for (int k = 0; k < NSRC; ++k) {
-                        if (k == q) continue;
-#pragma unroll
-                        for (int e = 0; e < V; ++e) {
-                            const auto a = acc.e[e], b = x[u][k].e[e];
-                            acc.e[e].re = a.re * b.re - a.im * b.im;
-                            acc.e[e].im = a.re * b.im + a.im * b.re;
-                            hit |= __builtin_isnan(acc.e[e].re) & __builtin_isnan(acc.e[e].im);
-                        }
-                    }
-                    st16_fold((u32x4 *)p.dst[q] + i, acc.v);
-                }
-                if (__all(!hit)) continue;
-            }
-#endif
+            // every member's chain with the fast operator forms (ops.h
+            // apply_fast), each output stored as its chain ends; a lane where
+            // any chain had a NaN come out redoes every chain with the
+            // reference's operator (member_chain, from registers, so an output
+            // aliasing its source is safe) and rewrites the outputs -- the
+            // same bits either way. For complex products this is also Annex G's recovery (the
+            // former float-only wave vote, now per lane and for every type).
+            bool redo = false;
 #pragma unroll
             for (int q = 0; q < NSRC; ++q) {
                 if (!ALL && p.dst[q] == nullptr) continue;
@@ -489,9 +442,23 @@ void combine_orders_vec(OrdersParams p) {
                 for (int k = 0; k < NSRC; ++k) {
                     if (k == q) continue;
 #pragma unroll
-                    for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[u][k].e[e]);
+                    for (int e = 0; e < V; ++e) acc.e[e] = apply_fast<OP>(acc.e[e], x[u][k].e[e]);
                 }
+#pragma unroll
+                for (int e = 0; e < V; ++e) redo |= redo_needed<OP>(acc.e[e]);
                 st16_fold((u32x4 *)p.dst[q] + i, acc.v);
+            }
+            if constexpr (has_fast_form<OP, T>()) {
+                if (redo) {
+#pragma unroll 1
+                    for (int q = 0; q < NSRC; ++q) {
+                        u32x4 *dq = (u32x4 *)p.dst[0];
+#pragma unroll
+                        for (int k = 1; k < NSRC; ++k) dq = q == k ? (u32x4 *)p.dst[k] : dq;
+                        if (!ALL && dq == nullptr) continue;
+                        st16_fold(dq + i, member_chain<OP, T, NSRC>(x[u], q).v);
+                    }
+                }
             }
         }
     }
@@ -700,12 +667,9 @@ int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, b
         p.nvec = n / V;
         p.tail = (uint32_t)(n % V);
         auto k = combine_vec<OP, T, NSRC, S::unroll, S::policy>;
-        int bpc = !S::alu_heavy || S::blocks_per_cu < resident_blocks((const void *)k)
-                      ? S::blocks_per_cu
-                      : resident_blocks((const void *)k);
-#if MI355_ALU_GRID_DYNAMIC_FOLD
-        if (S::alu_heavy) bpc = 1 << 20;  // as in launch_orders_fixed below
-#endif
+        const int bpc = !S::alu_heavy || S::blocks_per_cu < resident_blocks((const void *)k)
+                            ? S::blocks_per_cu
+                            : resident_blocks((const void *)k);
         const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, bpc);
         return launch(k, dim3(grid), st, p, final);
     }
@@ -747,12 +711,13 @@ int launch_orders_fixed(void *const *dsts, const void *const *srcs, size_t n, hi
         int bpc = !S::alu_heavy || S::blocks_per_cu < resident_blocks((const void *)k)
                       ? S::blocks_per_cu
                       : resident_blocks((const void *)k);
-#if MI355_ALU_GRID_DYNAMIC
-        // the ALU-heavy folds (x87, complex products): one vector per lane,
-        // every block queued at once, so the hardware hands out the last
-        // round's work as slots free instead of a resident grid's fixed rounds
-        if (S::alu_heavy || S::cplx) bpc = 1 << 20;
-#endif
+        // the measured ALU-heavy folds -- x87 sum/product, float complex
+        // product (profiles/r04/alu_grid/) -- one vector per lane, every
+        // block queued at once, so the hardware hands out the last round's
+        // work as slots free instead of a resident grid's fixed rounds
+        if ((S::alu_heavy && (OP == MI355_OP_SUM || OP == MI355_OP_PROD)) ||
+            (std::is_same<T, cplxf>::value && OP == MI355_OP_PROD))
+            bpc = 1 << 20;
         const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, bpc);
         return launch(k, dim3(grid), st, p);
     }

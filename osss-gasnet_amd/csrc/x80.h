@@ -346,11 +346,7 @@ __device__ __forceinline__ x80 add(const x80 &a, const x80 &b) {
 // = 2^64 - 1); the low word is assembled from the partial products' halves.
 // (__umul64hi next to a * b compiled to the same four multiply-adds plus two
 // 32-bit multiplies and an add recomputing the low word's upper half.)
-#ifndef MI355_X80_MUL128
-#define MI355_X80_MUL128 1
-#endif
 __device__ __forceinline__ void mul64x64(uint64_t a, uint64_t b, uint64_t &hi, uint64_t &lo) {
-#if MI355_X80_MUL128
     const uint32_t a0 = (uint32_t)a, a1 = (uint32_t)(a >> 32), b0 = (uint32_t)b, b1 = (uint32_t)(b >> 32);
     const uint64_t p00 = (uint64_t)a0 * b0;
     const uint64_t p01 = (uint64_t)a0 * b1 + (p00 >> 32);
@@ -358,10 +354,6 @@ __device__ __forceinline__ void mul64x64(uint64_t a, uint64_t b, uint64_t &hi, u
     const uint64_t p11 = (uint64_t)a1 * b1 + (p01 >> 32);
     hi = p11 + (p10 >> 32);
     lo = (p10 << 32) | (uint32_t)p00;
-#else
-    hi = __umul64hi(a, b);
-    lo = a * b;
-#endif
 }
 
 template <bool RANGE = true>

@@ -374,6 +374,23 @@ def bench_loop(path=BENCH_LIB_PATH, name="double_sum"):
     return f
 
 
+def bench_rotating(path=BENCH_LIB_PATH):
+    """csrc/bench_loop.c shmemb_double_sum_rotating: K calls over npairs
+    disjoint (target, source) pairs taken in turn; returns
+    f(targets, sources, nreduce, pe_start, log_stride, pe_size, psync, k)."""
+    if not os.path.exists(path):
+        raise RuntimeError(f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    f = ctypes.CDLL(path).shmemb_double_sum_rotating
+    f.argtypes = [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _i]
+    f.restype = None
+
+    def run(targets, sources, nreduce, pe_start, log_stride, pe_size, psync, k):
+        t = (_vp * len(targets))(*targets)
+        s = (_vp * len(sources))(*sources)
+        f(t, s, len(targets), nreduce, pe_start, log_stride, pe_size, None, psync, k)
+    return run
+
+
 def bench_call_times(path=BENCH_LIB_PATH):
     """csrc/bench_loop.c shmemb_double_sum_times: K shmem_double_sum_to_all
     calls, each timed alone; returns f(target, source, nreduce, PE_start,

@@ -283,7 +283,8 @@ def main():
         op, dtype, n = c["op"], c["dtype"], c["n"]
         es = np.dtype(shmem_reduce.NP[dtype]).itemsize
         if "golden" in c:  # the committed fixture's inputs (tests/golden/), member i's row
-            g = np.load(os.path.join(HERE, "golden", f"golden_{op}_{dtype}.npz"))
+            fam = c.get("family", "")   # "nan_": the NaN-payload families
+            g = np.load(os.path.join(HERE, "golden", f"golden_{fam}{op}_{dtype}.npz"))
             x = np.ascontiguousarray(g[f"in_{c['golden']}"][members(*mine).index(me)])
         else:
             x = source(op, dtype, n, c["seed"], me)

@@ -46,14 +46,15 @@ def common(d, n):
     assert d["check"].startswith("bit-exact"), d["check"]
     r = d["roofline"]
     if n == 1:
-        assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] < 1.2 and r["achieved"] > 0
+        assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] <= 1.0 and r["achieved"] > 0
     else:
         # N > 1: the reduce-scatter fold's remote reads against the links into the GPU; here
         # (PEs sharing the test GPU) its local-HBM view, the link view kept aside
         x = r["xgmi_view"]
         assert x["bound"] == "xgmi" and x["peak"] == (n - 1) * 153.0 and x["achieved"] > 0
         assert x["alg_bytes_per_launch"] == (n - 1) * (d["config"]["bytes_per_pe"] // n)
-        assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] < 1.2
+        assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] <= 1.0
+        assert 0 < r["per_launch_frac"] <= 1.0, r
     for name in ("float_max", "longlong_and"):
         assert d["op_coverage"][name]["check"].startswith("bit-exact"), d["op_coverage"]
     assert d["small_call"]["us_per_call"] > 0
@@ -66,13 +67,19 @@ def test_bench_one_gpu_line():
     d = run([sys.executable, "bench.py", "--steps", "5", "--warmup", "2", "--cpu-seconds", "1", "--kernel-reps", "5"])
     common(d, 1)
     cb = d["cpu_baseline"]
-    assert cb["kind"] == "port" and cb["cores"] == 2 and cb["value"] > 0
-    assert cb["one_pe"]["cores"] == 1 and cb["config1"]["us_per_call"] > 0 and cb["host"]["nproc"] >= 1
+    # the headline's shape: 1 PE on 1 core; the other PE counts as sub-records
+    assert cb["kind"] == "port" and cb["cores"] == 1 and cb["value"] > 0 and "one_pe" not in cb
+    assert cb["two_pe"]["cores"] == 2 and cb["config1"]["us_per_call"] > 0 and cb["host"]["nproc"] >= 1
+    assert d["vs_baseline"] is None and d["vs_cpu_baseline"] > 0
     assert cb["eight_pe"]["cores"] == 8 and cb["eight_pe"]["value"] > 0 and cb["config5"]["us_per_call"] > 0
     assert d["config"]["bytes_per_pe"] == 256 << 20
     r = d["roofline"]
     assert r["kernel"] == "void mi355k::copy_segments<4, 1>(mi355k::SegParams<1>)", r
     assert r["call"]["schedule"] == "identity" and r["alg_bytes_per_launch"] == 2 * (256 << 20), r
+    # the HBM-only figure: the same call over disjoint pairs taken in turn, >= 2 GiB of footprint
+    hr = d["headline_rotating"]
+    assert hr["check"].startswith("bit-exact") and hr["footprint_MiB"] >= 2048 and hr["kernel"] == r["kernel"], hr
+    assert 0 < hr["frac"] <= 1.0 and r["hbm_only"]["frac"] == hr["frac"] and "Infinity Cache" in r["attribution"]
     assert d["coherence_selftest"] is None
     # north_star's host-memory rate: page-locked host arrays, staged over PCIe in each call
     hs = d["host_staged"]
@@ -81,9 +88,10 @@ def test_bench_one_gpu_line():
     k = d["kernels"]
     for name in ("fold_k2_double_sum", "fold_k8_double_sum", "rs_shard_n8_double_sum", "fold_k8_float_max",
                  "fold_k8_longlong_and", "rs_shard_n8_float_max", "rs_shard_n8_longdouble_sum",
-                 "rs_shard_n8_longdouble_prod", "rs_shard_n8_complexf_prod"):
+                 "rs_shard_n8_longdouble_prod", "rs_shard_n8_complexf_prod", "rs_shard_n8_longlong_and"):
         assert k[name]["check"].startswith("bit-exact"), (name, k[name])
-        assert 0 < k[name]["frac"] < 1.2 and k[name]["kernel_avg_us"] > 0, (name, k[name])
+        assert 0 < k[name]["frac"] <= 1.0 and k[name]["kernel_avg_us"] > 0, (name, k[name])
+        assert 0 < k[name]["cold"]["frac"] <= 1.0 and k[name]["cold"]["footprint_MiB"] >= 2048, (name, k[name])
     # the x87 sum's own roofline: VALU issue, from this build's instruction stream
     ls = k["rs_shard_n8_longdouble_sum"]
     assert ls["bound"] == "valu" and 0.3 < ls["valu_frac"] < 1.05 and ls["valu_per_element_wave"] > 1000, ls
@@ -127,8 +135,10 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
     shard = S // 2
     assert r["call"]["schedule"] == "p2p" and r["call"]["sources"] == 2 and r["call"]["outputs"] == 1, r
     assert r["xgmi_view"]["alg_bytes_per_launch"] == shard and r["alg_bytes_per_launch"] == 3 * shard, r
-    # both PEs' folds share this GPU's HBM: the device rate is twice one launch's
-    assert r["pes_on_gpu"] == 2 and abs(r["achieved"] - 2 * r["per_launch_achieved"]) < 1.0, r
+    # both PEs' folds share this GPU's HBM: the device rate counts both PEs' bytes over the call's
+    # wall time (a window holding both launches), so it cannot pass the peak
+    assert r["pes_on_gpu"] == 2 and 0 < r["frac"] <= 1.0, r
+    assert abs(r["achieved"] - 2 * r["alg_bytes_per_launch"] / (d["ms_per_step"] * 1e-3) / 1e9) < 0.01 * r["achieved"], r
     assert "2 PEs share each GPU" in d["config"]["workload"], d["config"]
     # the opt-in persistent server at N > 1 (a child job of one PE per rank)
     sp = d["small_call_persistent"]

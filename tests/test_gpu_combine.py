@@ -495,3 +495,52 @@ def test_combine_target_and_sources_misaligned_differently(shm, dev):
     assert shm.combine("sum", "double", out, ptrs, n) == 0
     shm.sync()
     assert_match(shm.get(out, n, "double"), oracle.reduce_pe("sum", "double", srcs, 0), "sum", "double")
+
+
+# ---------------------------------------------------------------------------
+# NaN payloads: the golden_nan_* families (float, double and complex sum/prod
+# on NaN-rich operands, outputs of the reference's compiled operators) through
+# the fold, the every-member fold, their element-wise head/tail paths (offset
+# pointers) and the multi-launch fold beyond 8 sources; bit for bit.
+# ---------------------------------------------------------------------------
+from test_oracle_golden import NAN_PAIRS, load_nan_cases  # noqa: E402
+
+
+@pytest.mark.parametrize("off", [0, 1])
+@pytest.mark.parametrize("op,dtype", NAN_PAIRS)
+def test_nan_payloads_fold_every_pe(shm, dev, op, dtype, off):
+    for npes, ins, outs in load_nan_cases(op, dtype):
+        for me in range(npes):
+            order = [me] + [i for i in range(npes) if i != me]
+            got = gpu_fold(shm, dev, op, dtype, [ins[i] for i in order], offset_elems=off)
+            assert_match(got, outs[me], op, dtype, strict=True, ctx=f"nan golden npes={npes} me={me} off={off}")
+        dev.free()
+
+
+@pytest.mark.parametrize("off", [0, 1])
+@pytest.mark.parametrize("op,dtype", NAN_PAIRS)
+def test_nan_payloads_every_member_fold(shm, dev, op, dtype, off):
+    for npes, ins, outs in load_nan_cases(op, dtype):
+        got = gpu_orders(shm, dev, op, dtype, [ins[i] for i in range(npes)], offset_elems=off)
+        for me in range(npes):
+            assert_match(got[me], outs[me], op, dtype, strict=True, ctx=f"nan golden npes={npes} me={me} off={off}")
+        dev.free()
+
+
+@pytest.mark.parametrize("op,dtype", NAN_PAIRS)
+def test_nan_payloads_sparse_in_large_arrays(shm, dev, op, dtype):
+    """Few NaNs among many ordinary values: the streaming kernels' fast form
+    with the per-lane redo of only the chains that met a NaN (ops.h)."""
+    import gen_golden
+    rng = np.random.default_rng(4242)
+    n, k = 300000, 8
+    srcs = [gen_golden.values(rng, op, dtype, n) for _ in range(k)]
+    specials = [gen_golden.nan_values(rng, dtype, 200) for _ in range(k)]
+    for s, sp in zip(srcs, specials):
+        s[rng.integers(0, n, 200)] = sp
+    got = gpu_fold(shm, dev, op, dtype, srcs)
+    assert_match(got, oracle.reduce_pe(op, dtype, srcs, 0), op, dtype, strict=True, ctx="fold")
+    dev.free()
+    got = gpu_orders(shm, dev, op, dtype, srcs)
+    for q in range(k):
+        assert_match(got[q], oracle.reduce_pe(op, dtype, srcs, q), op, dtype, strict=True, ctx=f"member {q}")

@@ -129,6 +129,7 @@ def test_four_pes_all_44_pairs_p2p_and_exact(tmp_path, fused_max, oneshot_max):
 
 
 GOLDEN_ROWS = json.load(open(os.path.join(HERE, "golden", "manifest.json")))["cases"]
+NAN_ROWS = json.load(open(os.path.join(HERE, "golden", "manifest.json")))["nan_cases"]
 
 
 @pytest.mark.parametrize("fused_max,oneshot_max", [("1M", "64K"), ("1M", "0"), ("0", "0")],
@@ -156,6 +157,31 @@ def test_golden_fixtures_on_every_pe(tmp_path, fused_max, oneshot_max):
         for i in range(c["sets"][0][2]):
             assert_match(results[i][str(c["id"])], outs[i], c["op"], c["dtype"],
                          ctx=f"golden {c['op']}/{c['dtype']} case {c['golden']} PE {i}:")
+
+
+@pytest.mark.parametrize("fused_max,oneshot_max", [("1M", "64K"), ("2M", "0"), ("0", "0")],
+                         ids=["fused-oneshot", "fused-twoshot-2M", "multi-launch"])
+def test_nan_payload_fixtures_on_every_pe(tmp_path, fused_max, oneshot_max):
+    """The NaN-payload families (tests/golden/golden_nan_*: float, double and
+    complex sum/prod on operands full of NaNs of every sign, payload and kind,
+    infinities and overflowing values, outputs from the reference's compiled
+    operators) on 2-9 PE processes through the public entry points: every PE's
+    target must equal its fixture row bit for bit, NaN payloads included."""
+    cases, cid = [], 0
+    for key, rows in NAN_ROWS.items():
+        op, dtype = key.split("_")
+        for k, row in enumerate(rows):
+            cases.append({"id": cid, "op": op, "dtype": dtype, "n": row["n"], "sets": [[0, 0, row["npes"]]],
+                          "mode": "dev", "algorithm": "p2p", "seed": 0, "golden": k, "family": "nan_"})
+            cid += 1
+    results = run_pes(9, cases, tmp_path, extra_env={"SHMEM_FUSED_MAX_BYTES": fused_max,
+                                                     "SHMEM_ONESHOT_MAX_BYTES": oneshot_max})
+    for c in cases:
+        g = np.load(os.path.join(HERE, "golden", f"golden_nan_{c['op']}_{c['dtype']}.npz"))
+        outs = g[f"out_{c['golden']}"]
+        for i in range(c["sets"][0][2]):
+            assert_match(results[i][str(c["id"])], outs[i], c["op"], c["dtype"], strict=True,
+                         ctx=f"nan golden {c['op']}/{c['dtype']} case {c['golden']} PE {i}:")
 
 
 def test_pe_start_order_within_stated_fp_tolerance(tmp_path):

@@ -1,0 +1,297 @@
+// cold_probe.hip -- warm vs cold (rotating-footprint) rates of the reduction
+// path's streaming kernels (tuning tool, not part of the library).
+//
+// Why: every earlier HBM probe ran at 256 MiB per buffer, the size of the
+// Infinity Cache (MI355X_MICROARCH.md: a line stays resident only while the
+// traffic between two uses of it fits in ~256 MiB), and FETCH_SIZE counts
+// Infinity-Cache hits, so a warm figure alone cannot say "HBM".
+//   warm    the same buffer set every launch (what a benchmark loop does)
+//   rotate  R disjoint buffer sets taken in turn, R chosen so that the
+//           footprint is >= 2 GiB (8x the Infinity Cache): between two uses
+//           of a line, >= 1.75 GiB of other traffic went by
+// Kernels: the library's own (through its C ABI: mi355_copy_segments,
+// mi355_combine, mi355_combine_orders -- the product code objects) and, for
+// the copy, variants of its loop compiled here (load / store policy, blocks
+// per CU, vectors per lane).
+//
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/cold_probe.hip \
+//          -L osss-gasnet_amd/lib -lshmem_reduce -Wl,-rpath,$PWD/osss-gasnet_amd/lib -o tools/cold_probe
+// run:   tools/cold_probe [lib|copy|all]   (one JSON line per measurement)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <functional>
+#include <string>
+#include <vector>
+
+#include "mi355_reduce.h"
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
+    fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+static constexpr size_t MiB = 1ull << 20;
+static constexpr size_t kFootprint = 2304 * MiB;   // >= 2 GiB + one set
+
+// ---- copy variants (the library's copy_segments<4,1> loop, policies varied)
+enum { LD_PLAIN = 0, LD_NT = 1 };
+enum { ST_NT_SC1 = 0, ST_PLAIN = 1, ST_NT = 2, ST_SC1 = 3 };
+
+template <int LD>
+__device__ __forceinline__ u32x4 ld(const u32x4 *p) {
+    if constexpr (LD == LD_NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <int ST>
+__device__ __forceinline__ void st(u32x4 *p, u32x4 v) {
+    if constexpr (ST == ST_NT_SC1) asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (ST == ST_SC1) asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (ST == ST_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+template <int U, int LD, int ST>
+__global__ __launch_bounds__(256) void copy_pipe(const u32x4 *s, u32x4 *d, uint64_t nvec) {
+    const uint64_t step = (uint64_t)gridDim.x * 256 * U;
+    uint64_t base = (uint64_t)blockIdx.x * 256 * U + threadIdx.x;
+    u32x4 x[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const uint64_t i = base + (uint64_t)u * 256;
+        if (i < nvec) x[u] = ld<LD>(s + i);
+    }
+    while (base < nvec) {
+        const uint64_t next = base + step;
+        u32x4 y[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = next + (uint64_t)u * 256;
+            if (i < nvec) y[u] = ld<LD>(s + i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = base + (uint64_t)u * 256;
+            if (i < nvec) st<ST>(d + i, x[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = y[u];
+        base = next;
+    }
+}
+
+// each block copies one contiguous chunk of the buffer (the placement that
+// keeps a block's DRAM pages together), same pipelined inner loop
+template <int U, int LD, int ST>
+__global__ __launch_bounds__(256) void copy_chunk(const u32x4 *s, u32x4 *d, uint64_t nvec) {
+    const uint64_t per = (nvec + gridDim.x - 1) / gridDim.x;
+    const uint64_t lo = (uint64_t)blockIdx.x * per;
+    const uint64_t hi = lo + per < nvec ? lo + per : nvec;
+    for (uint64_t base = lo + threadIdx.x; base < hi; base += 256 * U) {
+        u32x4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = base + (uint64_t)u * 256;
+            if (i < hi) x[u] = ld<LD>(s + i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = base + (uint64_t)u * 256;
+            if (i < hi) st<ST>(d + i, x[u]);
+        }
+    }
+}
+
+// ---- timing
+static hipEvent_t g_a, g_b;
+static int g_cus = 256;
+
+struct Stat { double med_us, mean_us; };
+
+// launch(set) for set = 0..nsets-1 in turn; warm = always set 0
+static Stat timed(const std::function<void(int)> &launch, int nsets, bool rotate, int reps) {
+    for (int i = 0; i < (rotate ? nsets : 3); ++i) launch(rotate ? i % nsets : 0);
+    CHECK(hipDeviceSynchronize());
+    std::vector<float> t;
+    for (int r = 0; r < reps; ++r) {
+        const int s = rotate ? r % nsets : 0;
+        CHECK(hipEventRecord(g_a, 0));
+        launch(s);
+        CHECK(hipEventRecord(g_b, 0));
+        CHECK(hipEventSynchronize(g_b));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, g_a, g_b));
+        t.push_back(ms * 1e3f);
+    }
+    std::vector<float> s = t;
+    std::sort(s.begin(), s.end());
+    double sum = 0;
+    for (float x : t) sum += x;
+    return {s[s.size() / 2], sum / t.size()};
+}
+
+// with the library's own event stamps (mi355_time_next_launch): the kernel's
+// duration, no marker packets
+static Stat timed_lib(const std::function<void(int)> &launch, int nsets, bool rotate, int reps) {
+    for (int i = 0; i < (rotate ? nsets : 3); ++i) launch(rotate ? i % nsets : 0);
+    CHECK(hipDeviceSynchronize());
+    std::vector<float> t;
+    for (int r = 0; r < reps; ++r) {
+        const int s = rotate ? r % nsets : 0;
+        mi355_time_next_launch(g_a, g_b);
+        launch(s);
+        CHECK(hipEventSynchronize(g_b));
+        float ms;
+        CHECK(hipEventElapsedTime(&ms, g_a, g_b));
+        t.push_back(ms * 1e3f);
+    }
+    std::vector<float> s = t;
+    std::sort(s.begin(), s.end());
+    double sum = 0;
+    for (float x : t) sum += x;
+    return {s[s.size() / 2], sum / t.size()};
+}
+
+static char *g_pool;
+static size_t g_pool_bytes;
+
+static void emit(const char *kernel, const char *variant, size_t alg, int nsets, Stat w, Stat c) {
+    printf("{\"kernel\": \"%s\", \"variant\": \"%s\", \"alg_bytes\": %zu, \"sets\": %d, \"footprint_MiB\": %zu, "
+           "\"warm_us\": %.2f, \"warm_mean_us\": %.2f, \"warm_TB_s\": %.3f, \"cold_us\": %.2f, \"cold_mean_us\": %.2f, "
+           "\"cold_TB_s\": %.3f, \"cold_frac\": %.4f, \"warm_frac\": %.4f}\n",
+           kernel, variant, alg, nsets, nsets * alg / MiB, w.med_us, w.mean_us, alg / (w.mean_us * 1e-6) / 1e12,
+           c.med_us, c.mean_us, alg / (c.mean_us * 1e-6) / 1e12, alg / (c.mean_us * 1e-6) / 8e12,
+           alg / (w.mean_us * 1e-6) / 8e12);
+    fflush(stdout);
+}
+
+// sets of (nbuf buffers of `bytes`), carved from the pool
+static int sets_for(size_t set_bytes) {
+    int n = (int)((kFootprint + set_bytes - 1) / set_bytes);
+    if (n < 4) n = 4;
+    if ((size_t)n * set_bytes > g_pool_bytes) n = (int)(g_pool_bytes / set_bytes);
+    return n;
+}
+static char *buf(int set, int k, int nbuf, size_t bytes) {
+    return g_pool + ((size_t)set * nbuf + k) * bytes;
+}
+
+template <typename K>
+static void copy_variant(const char *name, K kern, int bpc, int u, size_t bytes, bool chunk = false) {
+    const uint64_t nvec = bytes / 16;
+    const int nsets = sets_for(2 * bytes);
+    uint64_t want = (nvec + 256ull * u - 1) / (256ull * u);
+    unsigned grid = (unsigned)std::min<uint64_t>(want, (uint64_t)g_cus * bpc);
+    if (chunk) grid = g_cus * bpc;
+    auto launch = [&](int s) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, (const u32x4 *)buf(s, 0, 2, bytes),
+                           (u32x4 *)buf(s, 1, 2, bytes), nvec);
+    };
+    Stat w = timed(launch, nsets, false, 30);
+    Stat c = timed(launch, nsets, true, 4 * nsets);
+    char v[96];
+    snprintf(v, sizeof v, "%s bpc=%d U=%d", name, bpc, u);
+    emit("copy", v, 2 * bytes, nsets, w, c);
+}
+
+static void lib_copy(size_t bytes) {
+    const int nsets = sets_for(2 * bytes);
+    auto launch = [&](int s) {
+        void *d[1] = {buf(s, 1, 2, bytes)};
+        const void *sr[1] = {buf(s, 0, 2, bytes)};
+        size_t nb[1] = {bytes};
+        if (mi355_copy_segments(d, sr, nb, 1, nullptr) != 0) exit(2);
+    };
+    Stat w = timed_lib(launch, nsets, false, 30);
+    Stat c = timed_lib(launch, nsets, true, 4 * nsets);
+    emit("copy_segments<4,1>", "library", 2 * bytes, nsets, w, c);
+}
+
+static void lib_fold(const char *name, int op, int dtype, int k, size_t bytes) {
+    const int nbuf = k + 1;
+    const int nsets = sets_for(nbuf * bytes);
+    const size_t n = bytes / mi355_dtype_size(dtype);
+    auto launch = [&](int s) {
+        const void *sr[8];
+        for (int j = 0; j < k; ++j) sr[j] = buf(s, j, nbuf, bytes);
+        if (mi355_combine(op, dtype, buf(s, k, nbuf, bytes), sr, k, n, nullptr) != 0) exit(2);
+    };
+    Stat w = timed_lib(launch, nsets, false, 30);
+    Stat c = timed_lib(launch, nsets, true, std::max(40, 2 * nsets));
+    char v[64];
+    snprintf(v, sizeof v, "library, %d x %zu MiB", k, bytes / MiB);
+    emit(name, v, (size_t)nbuf * bytes, nsets, w, c);
+}
+
+static void lib_orders(const char *name, int op, int dtype, int k, size_t bytes) {
+    const int nbuf = 2 * k;
+    const int nsets = sets_for(nbuf * bytes);
+    const size_t n = bytes / mi355_dtype_size(dtype);
+    auto launch = [&](int s) {
+        const void *sr[8];
+        void *ds[8];
+        for (int j = 0; j < k; ++j) {
+            sr[j] = buf(s, j, nbuf, bytes);
+            ds[j] = buf(s, k + j, nbuf, bytes);
+        }
+        if (mi355_combine_orders(op, dtype, ds, sr, k, n, nullptr) != 0) exit(2);
+    };
+    Stat w = timed_lib(launch, nsets, false, 30);
+    Stat c = timed_lib(launch, nsets, true, std::max(40, 2 * nsets));
+    char v[64];
+    snprintf(v, sizeof v, "library, %d x %zu MiB", k, bytes / MiB);
+    emit(name, v, (size_t)nbuf * bytes, nsets, w, c);
+}
+
+int main(int argc, char **argv) {
+    const std::string what = argc > 1 ? argv[1] : "all";
+    CHECK(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, 0));
+    CHECK(hipEventCreate(&g_a));
+    CHECK(hipEventCreate(&g_b));
+    g_pool_bytes = kFootprint + 1024 * MiB;
+    CHECK(hipMalloc(&g_pool, g_pool_bytes));
+    // full-mantissa-ish bytes everywhere (doubles in [-1, 1), no NaN)
+    {
+        std::vector<double> h(64 * MiB / 8);
+        uint64_t z = 0x9E3779B97F4A7C15ull;
+        for (auto &x : h) {
+            z ^= z >> 30; z *= 0xBF58476D1CE4E5B9ull; z ^= z >> 27; z *= 0x94D049BB133111EBull; z ^= z >> 31;
+            x = (double)(z >> 11) * 0x1p-53 - 0.5;
+        }
+        for (size_t off = 0; off < g_pool_bytes; off += 64 * MiB)
+            CHECK(hipMemcpy(g_pool + off, h.data(), std::min(64 * MiB, g_pool_bytes - off), hipMemcpyHostToDevice));
+    }
+    const size_t S = 256 * MiB;
+    if (what == "lib" || what == "all") {
+        lib_copy(S);                                                            // the N = 1 headline's kernel
+        lib_fold("combine_vec<sum,double,2>", MI355_OP_SUM, MI355_DOUBLE, 2, S);
+        lib_fold("combine_vec<sum,double,8>", MI355_OP_SUM, MI355_DOUBLE, 8, S);
+        lib_fold("combine_vec<and,longlong,8>", MI355_OP_AND, MI355_LONGLONG, 8, 64 * MiB);
+        lib_fold("combine_vec<and,longlong,8>", MI355_OP_AND, MI355_LONGLONG, 8, 8 * MiB);   // config 4 N = 8 shard
+        lib_fold("combine_vec<max,float,8>", MI355_OP_MAX, MI355_FLOAT, 8, 64 * MiB);
+        lib_orders("combine_orders_vec<sum,double,8>", MI355_OP_SUM, MI355_DOUBLE, 8, 32 * MiB);
+        lib_orders("combine_orders_vec<max,float,8>", MI355_OP_MAX, MI355_FLOAT, 8, 8 * MiB);
+    }
+    if (what == "copy" || what == "all") {
+        copy_variant("pipe ld=plain st=nt_sc1", copy_pipe<4, LD_PLAIN, ST_NT_SC1>, 1, 4, S);   // = library
+        copy_variant("pipe ld=plain st=nt_sc1", copy_pipe<4, LD_PLAIN, ST_NT_SC1>, 2, 4, S);
+        copy_variant("pipe ld=plain st=nt_sc1", copy_pipe<8, LD_PLAIN, ST_NT_SC1>, 1, 8, S);
+        copy_variant("pipe ld=plain st=nt_sc1", copy_pipe<2, LD_PLAIN, ST_NT_SC1>, 2, 2, S);
+        copy_variant("pipe ld=plain st=nt_sc1", copy_pipe<4, LD_PLAIN, ST_NT_SC1>, 4, 4, S);
+        copy_variant("pipe ld=nt st=nt_sc1", copy_pipe<4, LD_NT, ST_NT_SC1>, 1, 4, S);
+        copy_variant("pipe ld=nt st=nt_sc1", copy_pipe<4, LD_NT, ST_NT_SC1>, 2, 4, S);
+        copy_variant("pipe ld=plain st=nt", copy_pipe<4, LD_PLAIN, ST_NT>, 1, 4, S);
+        copy_variant("pipe ld=plain st=plain", copy_pipe<4, LD_PLAIN, ST_PLAIN>, 1, 4, S);
+        copy_variant("pipe ld=plain st=sc1", copy_pipe<4, LD_PLAIN, ST_SC1>, 1, 4, S);
+        copy_variant("pipe ld=nt st=sc1", copy_pipe<4, LD_NT, ST_SC1>, 1, 4, S);
+        copy_variant("chunk ld=plain st=nt_sc1", copy_chunk<4, LD_PLAIN, ST_NT_SC1>, 1, 4, S, true);
+        copy_variant("chunk ld=plain st=nt_sc1", copy_chunk<4, LD_PLAIN, ST_NT_SC1>, 2, 4, S, true);
+        copy_variant("chunk ld=nt st=nt_sc1", copy_chunk<4, LD_NT, ST_NT_SC1>, 2, 4, S, true);
+    }
+    CHECK(hipFree(g_pool));
+    return 0;
+}

@@ -8,7 +8,8 @@ entry records the hash of the gfx950 code objects it was taken from
 (shmem_reduce.kernel_code_hash): bench.py reports an entry's traffic only
 for a library with the same machine code.
 
-usage: pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR MIN_GRID KEY [out.json]
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR MIN_GRID[:MAX_GRID] KEY [out.json]
+(grid in threads: launches of one kernel at different sizes told apart)
 """
 import csv
 import glob
@@ -20,23 +21,25 @@ sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(
 import shmem_reduce  # noqa: E402  (kernel_code_hash only; the library is read, not loaded)
 
 
-def per_dispatch(d, counter, kname, min_grid):
+def per_dispatch(d, counter, kname, min_grid, max_grid=1 << 62):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     vals = {}
     for f in files:
         for r in csv.DictReader(open(f)):
-            if kname in r["Kernel_Name"] and int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0) >= min_grid \
-                    and r["Counter_Name"] == counter:
+            grid = int(r.get("Grid_Size", r.get("Grid_Size_X", 0)) or 0)
+            if kname in r["Kernel_Name"] and min_grid <= grid <= max_grid and r["Counter_Name"] == counter:
                 key = r["Dispatch_Id"]
                 vals[key] = vals.get(key, 0.0) + float(r["Counter_Value"])
     return list(vals.values())
 
 
 def main():
-    fdir, wdir, kname, min_grid, key = sys.argv[1:6]
+    fdir, wdir, kname, grid, key = sys.argv[1:6]
     out = sys.argv[6] if len(sys.argv) > 6 else None
-    f = per_dispatch(fdir, "FETCH_SIZE", kname, int(min_grid))
-    w = per_dispatch(wdir, "WRITE_SIZE", kname, int(min_grid))
+    lo, _, hi = grid.partition(":")
+    rng = (int(lo), int(hi) if hi else 1 << 62)
+    f = per_dispatch(fdir, "FETCH_SIZE", kname, *rng)
+    w = per_dispatch(wdir, "WRITE_SIZE", kname, *rng)
     if not f or not w:
         sys.exit(f"no dispatches of {kname}: fetch {len(f)} write {len(w)}")
     fetch = sorted(f)[len(f) // 2] * 1024

@@ -15,7 +15,7 @@ OUT=gpurun_out/prof_$R
 DST=gpurun_out/profiles/$R
 mkdir -p "$OUT" "$DST/pmc"
 export TMPDIR=/tmp
-BENCH=(bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-small --no-ops)
+BENCH=(bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-small --no-ops --no-rotating)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "${BENCH[@]}" \
     > "$OUT/bench_trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 "${BENCH[@]}" --no-check \
@@ -35,7 +35,8 @@ kernel_fold_k2_double_sum combine_vec<0,~double,~2, 1000
 kernel_fold_k8_double_sum combine_vec<0,~double,~8, 1000
 kernel_rs_shard_n8_double_sum combine_orders_vec<0,~double,~8, 1000
 kernel_fold_k8_float_max combine_vec<6,~float,~8, 1000
-kernel_fold_k8_longlong_and combine_vec<2,~long,~8, 1000
+kernel_fold_k8_longlong_and combine_vec<2,~long,~8, 300000
+kernel_rs_shard_n8_longlong_and combine_vec<2,~long,~8, 1000:300000
 kernel_rs_shard_n8_float_max combine_orders_vec<6,~float,~8, 1000
 kernel_rs_shard_n8_longdouble_sum combine_orders_vec<0,~x80,~8, 1000
 kernel_rs_shard_n8_longdouble_prod combine_orders_vec<1,~x80,~8, 1000
