@@ -174,10 +174,13 @@ void mi355_shard_bounds (size_t n, size_t es, int size, int i, size_t *lo, size_
 /* The reference's members disagree on this reduction: floating point (the
  * integer and bitwise operators wrap, select identical bits or are exact, so
  * any order gives the same bits), and either 3+ members (the rounding follows
- * the order) or min/max (`a < b ? a : b` picks by position when a NaN or a
- * +-0 pair is involved, reduce-op.c:138-150, from 2 members on). Two-member
- * sum/prod agree: IEEE (and x87, and the Annex G complex multiply) a + b and
- * a * b are commutative, NaN payloads aside. */
+ * the order), min/max (`a < b ? a : b` picks by position when a NaN or a +-0
+ * pair is involved, reduce-op.c:138-150, from 2 members on), or a two-member
+ * float, double or complex sum/prod: a + b and b + a have the same value, but
+ * where both operands are NaNs SSE returns the FIRST one (ops.h x86_result),
+ * so the two members' results differ in payload. x87 long double returns the
+ * NaN with the larger significand whatever the order (x80.h), so its
+ * two-member sum/prod agree. */
 static int order_sensitive (int op, int dtype, int size)
 {
     if (shmemi.order != SHMEMX_ORDER_REFERENCE || size < 2)
@@ -185,7 +188,7 @@ static int order_sensitive (int op, int dtype, int size)
     if (dtype != MI355_FLOAT && dtype != MI355_DOUBLE && dtype != MI355_LONGDOUBLE && dtype != MI355_COMPLEXF &&
         dtype != MI355_COMPLEXD)
         return 0;
-    return size > 2 || op == MI355_OP_MIN || op == MI355_OP_MAX;
+    return size > 2 || op == MI355_OP_MIN || op == MI355_OP_MAX || dtype != MI355_LONGDOUBLE;
 }
 
 /* The shard schedules deliver every member's order up to
