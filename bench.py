@@ -389,9 +389,13 @@ def rotating_leg(shm, S, me, npes, src, dst, k, check):
     x = synth(me, np.arange(n, dtype=np.uint64))
     try:
         for _ in range(ROT_PAIRS - 1):
-            srcs.append(shm.malloc_device(S))
-            dsts.append(shm.malloc_device(S))
-            shm.put(srcs[-1], x)
+            a, b = shm.malloc_device(S), shm.malloc_device(S)
+            srcs += [a] if a else []
+            dsts += [b] if b else []
+            if not a or not b:
+                raise RuntimeError("the device heap has no room for %d more %d-byte pairs (SHMEM_DEVICE_HEAP_SIZE)"
+                                   % (ROT_PAIRS - 1, S))
+            shm.put(a, x)
         run = shmem_reduce.bench_rotating()
         k = max(k, 4 * ROT_PAIRS)
         run(dsts, srcs, n, 0, 0, npes, shm._psync_ptr, 2 * ROT_PAIRS)

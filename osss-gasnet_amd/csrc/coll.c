@@ -19,9 +19,15 @@
  *   shmem_collect32/64     src/collect/collect-linear.c:60-156: like fcollect
  *       with per-PE counts; offsets are the running sum in active-set order
  *
- * The remote side of put/get, and every collective's source, must be in the
- * device symmetric heap (shmemx_malloc_device): that is where peers can read
- * it over xGMI. Local sides may be any host or device memory. A put into
+ * The remote side of put/get, and every collective's source, is symmetric:
+ * in the device symmetric heap (shmemx_malloc_device), which peers read over
+ * xGMI, or in shmem_malloc's symmetric host heap (hostheap.c), whose every
+ * PE's segment is mapped in every PE, as the reference's segment exchange
+ * makes them reachable (comms-inline.h:766-845). Host-heap objects move with
+ * plain memory copies when the other side is host memory too (the
+ * reference's transport does the same over GASNet), and with hipMemcpy when
+ * it is device memory; everything else below is the device path. Local sides
+ * may be any host or device memory. A put into
  * another GPU's memory goes through hipMemcpy on the peer-mapped pointer (the
  * HIP runtime's P2P copy contract makes the bytes visible to the peer's later
  * kernels; this library's kernels only ever write their own GPU's memory, so
@@ -56,15 +62,32 @@ static void check_pe (const char *fn, int pe)
         shmemi_fatal ("%s: PE %d outside 0..%d", fn, pe, shmemi.npes - 1);
 }
 
-/* Address of symmetric object `sym` (nbytes long) on PE `pe`. */
+/* Address of symmetric object `sym` (nbytes long) on PE `pe`: in the peer's
+ * device heap, or in its host heap segment as mapped here. */
 static void *remote_addr (const char *fn, const void *sym, size_t nbytes, int pe)
 {
     if (pe == shmemi.mype)
         return (void *) sym;
-    if (!shmemi_in_device_heap (sym, nbytes))
-        shmemi_fatal ("%s: remote address %p is not in the device symmetric heap "
-                      "(allocate it with shmemx_malloc_device)", fn, sym);
-    return shmemi_peer_ptr (pe, shmemi_heap_offset (sym));
+    if (shmemi_in_device_heap (sym, nbytes))
+        return shmemi_peer_ptr (pe, shmemi_heap_offset (sym));
+    if (shmemi_in_host_heap (sym, nbytes))
+        return shmemi_host_peer_ptr (pe, sym);
+    shmemi_fatal ("%s: remote address %p is not symmetric (allocate it with shmem_malloc or "
+                  "shmemx_malloc_device)", fn, sym);
+}
+
+static int is_device_ptr (const void *p);
+
+/* p is host memory (no GPU at all: everything is) */
+static int host_side (const void *p)
+{
+    return shmemi.heap == NULL || !is_device_ptr (p);
+}
+
+static void need_gpu (const char *fn)
+{
+    if (shmemi.heap == NULL)
+        shmemi_fatal ("%s: no GPU (SHMEM_BOOTSTRAP_ONLY): only host-memory copies run without one", fn);
 }
 
 static void blocking_copy (void *dst, const void *src, size_t nbytes)
@@ -75,7 +98,6 @@ static void blocking_copy (void *dst, const void *src, size_t nbytes)
     SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
 }
 
-static int is_device_ptr (const void *p);
 static void pull (void **dsts, const void **srcs, size_t *nbytes, int nseg);
 
 static void put_bytes (const char *fn, void *dest, const void *src, size_t nbytes, int pe)
@@ -86,13 +108,20 @@ static void put_bytes (const char *fn, void *dest, const void *src, size_t nbyte
     if (shmemi.heap != NULL)
         shmemi_server_stop ();
     check_pe (fn, pe);
-    if (shmemi.heap == NULL)
-        shmemi_fatal ("%s: no GPU (SHMEM_BOOTSTRAP_ONLY)", fn);
     if (nbytes == 0)
         return;
     void *to = remote_addr (fn, dest, nbytes, pe);
+    const int to_host = shmemi_in_host_heap (dest, nbytes) || (pe == shmemi.mype && host_side (dest));
+    if (to_host && host_side (src)) {
+        /* host memory both sides (a peer's host heap segment is mapped
+         * here): the bytes are in place when memmove returns, and the
+         * barriers' release/acquire make them visible to the peer */
+        memmove (to, src, nbytes);
+        return;
+    }
+    need_gpu (fn);
     const void *from = is_device_ptr (src) ? src : shmemi_host_dev_ptr (src, nbytes);
-    if (from != NULL && from != to && shmemi_pe_same_device (pe)) {
+    if (!to_host && from != NULL && from != to && shmemi_pe_same_device (pe)) {
         /* target memory on this GPU (this PE's own heap, or a PE sharing the
          * GPU) <- device or page-locked host: the streaming copy kernel; the
          * call returns once every store has drained (local completion), and
@@ -119,12 +148,16 @@ static void get_bytes (const char *fn, void *dest, const void *src, size_t nbyte
     if (shmemi.heap != NULL)
         shmemi_server_stop ();
     check_pe (fn, pe);
-    if (shmemi.heap == NULL)
-        shmemi_fatal ("%s: no GPU (SHMEM_BOOTSTRAP_ONLY)", fn);
     if (nbytes == 0)
         return;
     const void *from = remote_addr (fn, src, nbytes, pe);
-    if (is_device_ptr (dest) && dest != from) {
+    const int from_host = shmemi_in_host_heap (src, nbytes) || (pe == shmemi.mype && host_side (src));
+    if (from_host && host_side (dest)) {
+        memmove (dest, from, nbytes);
+        return;
+    }
+    need_gpu (fn);
+    if (!from_host && is_device_ptr (dest) && dest != from) {
         /* device <- (peer) device: the streaming copy kernel pulls over xGMI
          * (2-3x the rate of hipMemcpy's D2D path, profiles/r01/coll_bench) */
         shmemi_order_after_caller (0);
@@ -205,8 +238,6 @@ static struct cset make_set (const char *fn, int PE_start, int logPE_stride, int
     shmemi_init_check (fn);
     if (shmemi.heap != NULL)
         shmemi_server_stop ();
-    if (shmemi.heap == NULL)
-        shmemi_fatal ("%s: no GPU (SHMEM_BOOTSTRAP_ONLY)", fn);
     if (logPE_stride < 0 || logPE_stride > 30 || PE_size < 1 || PE_start < 0 ||
         PE_start + (long) (PE_size - 1) * (1L << logPE_stride) >= shmemi.npes)
         shmemi_fatal ("%s: active set (PE_start %d, logPE_stride %d, PE_size %d) outside the %d PEs", fn,
@@ -223,6 +254,8 @@ static struct cset make_set (const char *fn, int PE_start, int logPE_stride, int
 
 static int is_device_ptr (const void *p)
 {
+    if (shmemi.heap == NULL)
+        return 0;
     if (shmemi_in_device_heap (p, 0))
         return 1;
     hipPointerAttribute_t a;
@@ -230,6 +263,25 @@ static int is_device_ptr (const void *p)
     hipError_t e = hipPointerGetAttributes (&a, p);
     (void) hipGetLastError ();
     return e == hipSuccess && (a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged);
+}
+
+/* Pull nseg byte ranges of peers' symmetric HOST heap segments (mapped here)
+ * into local memory: plain copies into host memory, hipMemcpy into device
+ * memory (the GPU does not read the peers' segments: they are not
+ * registered with this process's HIP). */
+static void pull_host (const char *fn, void **dsts, const void **srcs, size_t *nbytes, int nseg)
+{
+    for (int i = 0; i < nseg; ++i) {
+        if (nbytes[i] == 0)
+            continue;
+        if (host_side (dsts[i])) {
+            memmove (dsts[i], srcs[i], nbytes[i]);
+        } else {
+            need_gpu (fn);
+            SHMEMI_HIP (hipMemcpyAsync (dsts[i], srcs[i], nbytes[i], hipMemcpyDefault, shmemi.stream));
+            SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+        }
+    }
 }
 
 /* Pull nseg byte ranges from peers into local memory: one copy kernel when
@@ -271,12 +323,33 @@ static void pull (void **dsts, const void **srcs, size_t *nbytes, int nseg)
 /* Opening barrier: every source is ready. With device barriers the rest of
  * the collective is queued behind it (dev = 1); else a host barrier after the
  * host has seen the caller's work done. */
+/* 1: source in the symmetric host heap; 0: in the device heap (or nothing to
+ * read); fatal otherwise */
+static int source_kind (const char *fn, const void *source, size_t nbytes)
+{
+    if (nbytes == 0 || shmemi_in_device_heap (source, nbytes))
+        return 0;
+    if (shmemi_in_host_heap (source, nbytes))
+        return 1;
+    shmemi_fatal ("%s: source %p is not symmetric (allocate it with shmem_malloc or shmemx_malloc_device)", fn,
+                  source);
+}
+
+/* PE pe's copy of a symmetric source (device or host heap) */
+static const void *source_on (int pe, const void *source, int host)
+{
+    return host ? shmemi_host_peer_ptr (pe, source) : shmemi_peer_ptr (pe, shmemi_heap_offset (source));
+}
+
 static int collective_entry (const char *fn, const void *source, size_t nbytes, const struct cset *s,
                              int allow_dev)
 {
-    if (nbytes != 0 && !shmemi_in_device_heap (source, nbytes))
-        shmemi_fatal ("%s: source %p is not in the device symmetric heap (allocate it with "
-                      "shmemx_malloc_device)", fn, source);
+    if (source_kind (fn, source, nbytes) != 0 || shmemi.heap == NULL)
+        allow_dev = 0; /* the host heap: host barriers, the copies below run on the host */
+    if (shmemi.heap == NULL) {
+        shmemi_barrier_set (s->start, s->stride, s->size);
+        return 0;
+    }
     if (allow_dev && shmemi_dev_barrier_ok (s->start, s->stride, s->size)) {
         shmemi_order_after_caller (0); /* SHMEM_ENTRY_SYNC */
         shmemi_dev_barrier (s->start, s->stride, s->size, s->me, 0);
@@ -303,7 +376,7 @@ static void collective_exit (const struct cset *s, int dev)
  * write (pageable host memory) pulls into its scratch C and copies out. */
 static int fused_pull_ok (const struct cset *s, size_t total)
 {
-    return s->size >= 2 && shmemi.fused_max != 0 && total <= shmemi.fused_max &&
+    return shmemi.heap != NULL && s->size >= 2 && shmemi.fused_max != 0 && total <= shmemi.fused_max &&
            total <= shmemi.scratch_chunk && shmemi_dev_barrier_ok (s->start, s->stride, s->size);
 }
 
@@ -349,12 +422,10 @@ static void broadcast_bytes (const char *fn, void *target, const void *source, s
     if (PE_root < 0 || PE_root >= PE_size)
         shmemi_fatal ("%s: PE_root %d outside the active set of %d PEs", fn, PE_root, PE_size);
     const int root = PE_start + PE_root * s.stride;
-    if (nbytes != 0 && !shmemi_in_device_heap (source, nbytes))
-        shmemi_fatal ("%s: source %p is not in the device symmetric heap (allocate it with "
-                      "shmemx_malloc_device)", fn, source);
+    const int host = source_kind (fn, source, nbytes);
     if (s.size == 1)
         return; /* the root does not write its own target, and there is nobody to wait for */
-    if (fused_pull_ok (&s, nbytes)) {
+    if (!host && fused_pull_ok (&s, nbytes)) {
         SHMEMI_TRACE (SHMEMI_LOG_BROADCAST, "%s: %zu bytes from PE %d, one fused launch", fn, nbytes, root);
         const void *src = nbytes != 0 ? shmemi_peer_ptr (root, shmemi_heap_offset (source)) : NULL;
         const size_t toff = 0;
@@ -364,8 +435,11 @@ static void broadcast_bytes (const char *fn, void *target, const void *source, s
     const int dev = collective_entry (fn, source, nbytes, &s, 1);
     if (shmemi.mype != root && nbytes != 0) {
         void *d = target;
-        const void *src = shmemi_peer_ptr (root, shmemi_heap_offset (source));
-        pull_impl (&d, &src, &nbytes, 1, !dev);
+        const void *src = source_on (root, source, host);
+        if (host)
+            pull_host (fn, &d, &src, &nbytes, 1);
+        else
+            pull_impl (&d, &src, &nbytes, 1, !dev);
     }
     collective_exit (&s, dev); /* nobody reads the root's source any more */
 }
@@ -385,7 +459,8 @@ void pshmem_broadcast64 (void *target, const void *source, size_t nelems, int PE
 }
 
 /* counts[i] bytes from member i land at the running offset in target */
-static void gather_bytes (void *target, const void *source, const size_t *counts, const struct cset *s, int wait)
+static void gather_bytes (const char *fn, void *target, const void *source, const size_t *counts,
+                          const struct cset *s, int wait, int host)
 {
     void **dsts = (void **) malloc (sizeof (void *) * (size_t) s->size);
     const void **srcs = (const void **) malloc (sizeof (void *) * (size_t) s->size);
@@ -398,13 +473,15 @@ static void gather_bytes (void *target, const void *source, const size_t *counts
         const int pe = s->start + i * s->stride;
         if (counts[i] != 0) {
             dsts[k] = (char *) target + off;
-            srcs[k] = shmemi_peer_ptr (pe, shmemi_heap_offset (source));
+            srcs[k] = source_on (pe, source, host);
             nb[k] = counts[i];
             ++k;
         }
         off += counts[i];
     }
-    if (k > 0)
+    if (k > 0 && host)
+        pull_host (fn, dsts, srcs, nb, k);
+    else if (k > 0)
         pull_impl (dsts, srcs, nb, k, wait);
     free (nb);
     free (srcs);
@@ -415,22 +492,21 @@ static void fcollect_bytes (const char *fn, void *target, const void *source, si
                             int logPE_stride, int PE_size)
 {
     struct cset s = make_set (fn, PE_start, logPE_stride, PE_size);
+    const int host = source_kind (fn, source, nbytes);
     if (s.size == 1) { /* one member: target = source, nobody to wait for */
-        if (nbytes != 0 && !shmemi_in_device_heap (source, nbytes))
-            shmemi_fatal ("%s: source %p is not in the device symmetric heap (allocate it with "
-                          "shmemx_malloc_device)", fn, source);
         if (nbytes != 0 && target != source) {
-            shmemi_order_after_caller (0);
             void *d = target;
             const void *src = source;
-            pull (&d, &src, &nbytes, 1);
+            if (host) {
+                pull_host (fn, &d, &src, &nbytes, 1);
+            } else {
+                shmemi_order_after_caller (0);
+                pull (&d, &src, &nbytes, 1);
+            }
         }
         return;
     }
-    if (s.size <= MI355_PULL_MAX_SEGS && nbytes != 0 && fused_pull_ok (&s, nbytes * (size_t) s.size)) {
-        if (!shmemi_in_device_heap (source, nbytes))
-            shmemi_fatal ("%s: source %p is not in the device symmetric heap (allocate it with "
-                          "shmemx_malloc_device)", fn, source);
+    if (!host && s.size <= MI355_PULL_MAX_SEGS && nbytes != 0 && fused_pull_ok (&s, nbytes * (size_t) s.size)) {
         size_t toff[MI355_PULL_MAX_SEGS], nb[MI355_PULL_MAX_SEGS];
         const void *srcs[MI355_PULL_MAX_SEGS];
         for (int i = 0; i < s.size; ++i) {
@@ -448,7 +524,7 @@ static void fcollect_bytes (const char *fn, void *target, const void *source, si
         shmemi_fatal ("out of host memory");
     for (int i = 0; i < s.size; ++i)
         counts[i] = nbytes;
-    gather_bytes (target, source, counts, &s, !dev);
+    gather_bytes (fn, target, source, counts, &s, !dev, host);
     free (counts);
     collective_exit (&s, dev); /* nobody reads our source any more */
 }
@@ -473,6 +549,7 @@ static void collect_bytes (const char *fn, void *target, const void *source, siz
                            int logPE_stride, int PE_size)
 {
     struct cset s = make_set (fn, PE_start, logPE_stride, PE_size);
+    const int host = source_kind (fn, source, nbytes);
     shmemi_publish_count (nbytes);
     (void) collective_entry (fn, source, nbytes, &s, 0);
     size_t *counts = (size_t *) malloc (sizeof (size_t) * (size_t) s.size);
@@ -480,7 +557,7 @@ static void collect_bytes (const char *fn, void *target, const void *source, siz
         shmemi_fatal ("out of host memory");
     for (int i = 0; i < s.size; ++i)
         counts[i] = shmemi_peer_count (s.start + i * s.stride);
-    gather_bytes (target, source, counts, &s, 1);
+    gather_bytes (fn, target, source, counts, &s, 1, host);
     free (counts);
     shmemi_barrier_set (s.start, s.stride, s.size);
 }

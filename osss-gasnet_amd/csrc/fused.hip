@@ -86,21 +86,8 @@ __device__ unsigned long long g_phase[64][8];
 // staging copy, the server's mailbox) are inlined into every kernel: in the
 // large complex-product instantiations the compiler had left them as calls,
 // whose frames took 1,264 bytes of scratch per lane (round 4;
-// tools/check_residency.py --no-scratch). -DMI355_FUSED_INLINE_HELPERS=0
-// restores the compiler's choice (measurement builds only).
-#ifndef MI355_FUSED_INLINE_HELPERS
-#define MI355_FUSED_INLINE_HELPERS 1
-#endif
-#if MI355_FUSED_INLINE_HELPERS
+// tools/check_residency.py --no-scratch).
 #define FUSED_HELPER __device__ __forceinline__
-#else
-#define FUSED_HELPER __device__
-#endif
-// -DMI355_FUSED_BUFFER_LOADS=0: the folds read with ld16_sys (two 8-byte
-// atomic loads) instead of ld16_sys_at (measurement builds only)
-#ifndef MI355_FUSED_BUFFER_LOADS
-#define MI355_FUSED_BUFFER_LOADS 1
-#endif
 
 __device__ __forceinline__ void st_sys_u64(unsigned long long *p, unsigned long long v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -139,15 +126,14 @@ __device__ __forceinline__ u32x4 ld16_sys(const void *p) {
 // system-coherent loads fold 2 sources in 134 us per 256 MiB against 143 us
 // for ld16_sys's two 8-byte loads (8 sources: 441 vs 459 us); non-temporal
 // loads take 116 / 381 us, so the multi-launch folds keep theirs.
-// The offset must stay below 4 GiB (the fused path is capped at 1 GiB).
+// The offset must stay below 4 GiB: the fused path is capped at 1 GiB, and
+// mi355_fused_allreduce / mi355_fused_server refuse a call whose bytes per
+// member reach kMaxFusedBytes (an out-of-range buffer load returns 0 silently).
+constexpr uint64_t kMaxFusedBytes = 1ull << 32;
 __device__ __forceinline__ u32x4 ld16_sys_at(const char *base, uint32_t off) {
-#if MI355_FUSED_BUFFER_LOADS
     const __amdgpu_buffer_rsrc_t rs =
         __builtin_amdgcn_make_buffer_rsrc(const_cast<char *>(base), 0, (int)0xFFFFFFF0u, 0x00020000);
     return __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 17);  // aux 17: sc0 | sc1
-#else
-    return ld16_sys(base + off);
-#endif
 }
 template <typename T>
 __device__ __forceinline__ T ld_elem_sys(const T *p) {
@@ -1029,6 +1015,9 @@ extern "C" int mi355_fused_allreduce(const MI355FusedArgs *a, void *stream) {
         return MI355_E_INVAL;
     const size_t es = mi355_dtype_size(a->dtype);
     if (a->shard == 0 || (a->shard * es) % 16 != 0) return MI355_E_INVAL;
+    // the folds address a member's buffer with 32-bit buffer offsets (ld16_sys_at)
+    if (a->n * es >= kMaxFusedBytes || (uint64_t)a->shard * es * (uint64_t)a->nmembers >= kMaxFusedBytes)
+        return MI355_E_INVAL;
     for (int i = 0; i < a->nmembers; ++i)
         if (a->src[i] == nullptr || a->dst[i] == nullptr || a->sig[i] == nullptr ||
             (((uintptr_t)a->src[i] | (uintptr_t)a->dst[i]) & 15) != 0 || a->pe[i] < 0 ||
@@ -1098,6 +1087,7 @@ extern "C" int mi355_fused_server(const MI355FusedArgs *a, MI355ServerMailbox *m
     if (a->nmembers < 1 || a->nmembers > MI355_FUSED_MAX_MEMBERS || a->me < 0 || a->me >= a->nmembers)
         return MI355_E_INVAL;
     if (a->host_src != nullptr || a->host_dst != nullptr || a->host_flag == nullptr) return MI355_E_INVAL;
+    if (grid_vecs * 16 >= kMaxFusedBytes) return MI355_E_INVAL;   // 32-bit buffer offsets (ld16_sys_at)
     for (int i = 0; i < a->nmembers; ++i)
         if (a->src[i] == nullptr || a->dst[i] == nullptr || a->sig[i] == nullptr ||
             (((uintptr_t)a->src[i] | (uintptr_t)a->dst[i]) & 15) != 0 || a->pe[i] < 0 ||

@@ -43,16 +43,8 @@
 
 struct shmemi_state shmemi;
 
-struct shmemi_hostblk {
-    void *p;
-    size_t size;
-    int registered;
-    char *dev; /* device-accessible address of p (registered blocks), else NULL */
-    struct shmemi_hostblk *next;
-};
-
 #define SEG_MAGIC 0x4d49333535534d45ull /* "MI355SME" */
-#define SEG_VERSION 5
+#define SEG_VERSION 6
 
 static double now_s (void)
 {
@@ -653,7 +645,7 @@ static void settings_publish (void)
     seg_info (shmemi.mype)->settings =
         (struct shmemi_settings) {shmemi.algorithm, shmemi.order, shmemi.debug != 0, shmemi.srv.enabled,
                                   shmemi.ext_map, 0, shmemi.order_chunk, shmemi.fused_max, shmemi.oneshot_max, shmemi.scratch_chunk,
-                                  shmemi.user_size};
+                                  shmemi.user_size, shmemi.hheap_size};
 }
 
 static void settings_check (void)
@@ -676,6 +668,7 @@ static void settings_check (void)
         S (oneshot_max, "SHMEM_ONESHOT_MAX_BYTES")
         S (scratch_chunk, "SHMEM_DEVICE_SCRATCH_SIZE")
         S (user_size, "SHMEM_DEVICE_HEAP_SIZE")
+        S (hheap_size, "SHMEM_SYMMETRIC_HEAP_SIZE")
 #undef S
     }
 }
@@ -848,7 +841,8 @@ static void coherence_test (size_t mark_off, int *passed, int *stale, int *syslo
  * res[] = 1 where every block of this PE saw every member's new words, in
  * shmemi.prod[] order (F plain, F sysload, F acquire, H plain, H sysload,
  * H acquire). SHMEM_TEST_IPC_FAIL=sysload (PE 1) reports F sysload stale;
- * =producer reports H acquire stale. */
+ * =producer reports H acquire stale; =producer_fused reports F sysload and
+ * F acquire stale (the fused kernel is then turned off job-wide). */
 static void producer_test (size_t off, int *res)
 {
     const int np = shmemi.npes, me = shmemi.mype, nb = 32, W = 32;
@@ -922,6 +916,8 @@ static void producer_test (size_t off, int *res)
         res[MI355_PROD_F_SYS] = 0;
     if (fail != NULL && strcmp (fail, "producer") == 0)
         res[MI355_PROD_H_ACQ] = 0;
+    if (fail != NULL && strcmp (fail, "producer_fused") == 0)
+        res[MI355_PROD_F_SYS] = res[MI355_PROD_F_ACQ] = 0;
     (void) hipFree (dev);
     free (host);
 }
@@ -1176,6 +1172,14 @@ int shmemx_is_device_symmetric (const void *ptr) { return shmemi_in_device_heap 
 /* ---------------------------------------------------------------------- */
 /* host heap (shmem_malloc's default: the reference returns host memory)    */
 /* ---------------------------------------------------------------------- */
+/* SHMEM_SYMMETRIC_HEAP_SIZE (the reference's name, comms-inline.h:675): the
+ * size of each PE's symmetric host heap segment; virtual, pages are committed
+ * per shmem_malloc block. Default 4 GiB (the reference: 32 MiB). */
+static void hheap_setup (void)
+{
+    shmemi_hheap_create (env_size ("SHMEM_SYMMETRIC_HEAP_SIZE", (size_t) 4 << 30));
+}
+
 static int heap_kind_device (void)
 {
     const char *v = getenv ("SHMEM_SYMMETRIC_HEAP_KIND");
@@ -1189,27 +1193,8 @@ void *pshmem_malloc (size_t size)
         shmemi_server_stop (); /* hipHostRegister below */
     if (heap_kind_device ())
         return shmemx_malloc_device (size);
-    void *p = NULL;
-    if (size != 0) {
-        if (posix_memalign (&p, 4096, round_up (size, 4096)) != 0)
-            shmemi_fatal ("shmem_malloc(%zu): out of host memory", size);
-        struct shmemi_hostblk *h = (struct shmemi_hostblk *) calloc (1, sizeof *h);
-        if (h == NULL)
-            shmemi_fatal ("out of host memory");
-        h->p = p;
-        h->size = size;
-        /* page-locked so the staging copies run at full PCIe rate */
-        if (shmemi.device >= 0) {
-            h->registered = hipHostRegister (p, round_up (size, 4096), hipHostRegisterDefault) == hipSuccess;
-            void *d = NULL;
-            if (h->registered && hipHostGetDevicePointer (&d, p, 0) == hipSuccess)
-                h->dev = (char *) d;
-            (void) hipGetLastError ();
-        }
-        h->next = shmemi.host_blocks;
-        shmemi.host_blocks = h;
-    }
-    SHMEMI_TRACE (SHMEMI_LOG_MEMORY, "shmem_malloc(%zu) = %p (host)", size, p);
+    void *p = shmemi_host_malloc (size);
+    SHMEMI_TRACE (SHMEMI_LOG_MEMORY, "shmem_malloc(%zu) = %p (symmetric host heap)", size, p);
     shmem_barrier_all ();
     return p;
 }
@@ -1235,26 +1220,6 @@ int shmemx_pe_same_device (int pe)
     return shmemi_pe_same_device (pe);
 }
 
-/* Device-accessible address of [p, p + nbytes) when it lies inside one
- * page-locked shmem_malloc block (kernels can then read and write it over
- * PCIe directly), else NULL. */
-void *shmemi_host_dev_ptr (const void *p, size_t nbytes)
-{
-    const char *c = (const char *) p;
-    for (const struct shmemi_hostblk *h = shmemi.host_blocks; h != NULL; h = h->next)
-        if (h->dev != NULL && c >= (const char *) h->p && c + nbytes <= (const char *) h->p + h->size)
-            return h->dev + (c - (const char *) h->p);
-    return NULL;
-}
-
-static void host_free_one (struct shmemi_hostblk *h)
-{
-    if (h->registered)
-        (void) hipHostUnregister (h->p);
-    free (h->p);
-    free (h);
-}
-
 void pshmem_free (void *ptr)
 {
     shmemi_init_check ("shmem_free");
@@ -1265,14 +1230,8 @@ void pshmem_free (void *ptr)
         return;
     if (device_free (ptr))
         return;
-    for (struct shmemi_hostblk **pp = &shmemi.host_blocks; *pp != NULL; pp = &(*pp)->next) {
-        if ((*pp)->p == ptr) {
-            struct shmemi_hostblk *h = *pp;
-            *pp = h->next;
-            host_free_one (h);
-            return;
-        }
-    }
+    if (shmemi_host_free (ptr))
+        return;
     shmemi_fatal ("shmem_free(%p): not allocated by shmem_malloc", ptr);
 }
 
@@ -1311,11 +1270,16 @@ void pshmem_init (void)
     static const char *bo_env[] = {"SHMEM_BOOTSTRAP_ONLY", NULL};
     if (env_long (bo_env, 0) != 0) {
         shmemi.device = -1;
-        if (shmemi.npes > 1) {
+        if (shmemi.npes > 1)
             bootstrap_attach ();
+        hheap_setup ();
+        if (shmemi.npes > 1) {
             settings_publish ();
             shmemi_barrier_set (0, 1, shmemi.npes);
             settings_check ();
+            shmemi_hheap_attach ();
+            shmemi_barrier_set (0, 1, shmemi.npes); /* every segment mapped everywhere */
+            shmemi_hheap_unlink ();
             if (shmemi.mype == 0) {
                 shm_unlink (shmemi.seg_name);
                 shmemi.seg_unlinked = 1;
@@ -1355,9 +1319,13 @@ void pshmem_init (void)
         shmemi.fused_max = (size_t) 1 << 30;
     shmemi.oneshot_max = env_size ("SHMEM_ONESHOT_MAX_BYTES", (size_t) 64 << 10);
 
+    if (shmemi.npes == 1)
+        hheap_setup ();
     if (shmemi.npes > 1) {
         bootstrap_attach ();
-        heap_exchange ();
+        hheap_setup ();
+        heap_exchange (); /* settings agreed, every PE's segments created */
+        shmemi_hheap_attach ();
         /* SHMEM_PEER_ACQUIRE=0|1 overrides the choice made from the peers' devices */
         static const char *pa_env[] = {"SHMEM_PEER_ACQUIRE", NULL};
         shmemi.peer_acquire = (int) env_long (pa_env, shmemi.peer_acquire) != 0;
@@ -1366,7 +1334,8 @@ void pshmem_init (void)
         shmemi.local_pes = (int) env_long (gs_env, shmemi.local_pes);
         if (shmemi.local_pes < 1)
             shmemi.local_pes = 1;
-        interconnect_selftest ();
+        interconnect_selftest (); /* its barriers: every PE has mapped every host segment */
+        shmemi_hheap_unlink ();
         if (shmemi.mype == 0 && !shmemi.seg_unlinked) {
             shm_unlink (shmemi.seg_name); /* every PE is attached: drop the name */
             shmemi.seg_unlinked = 1;
@@ -1438,11 +1407,7 @@ void pshmem_finalize (void)
         free (shmemi.blocks);
         shmemi.blocks = n;
     }
-    while (shmemi.host_blocks != NULL) {
-        struct shmemi_hostblk *n = shmemi.host_blocks->next;
-        host_free_one (shmemi.host_blocks);
-        shmemi.host_blocks = n;
-    }
+    shmemi_hheap_finalize (); /* after the barrier above: no peer reads it any more */
     if (shmemi.heap != NULL)
         (void) hipFree (shmemi.heap);
     shmemi.heap = NULL;

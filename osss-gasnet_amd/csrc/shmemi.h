@@ -41,7 +41,7 @@ struct shmemi_dbg_rec {
 /* Settings every PE of a job must share (compared at init). */
 struct shmemi_settings {
     int32_t algorithm, order, debug, persistent, ext_map, pad;
-    uint64_t order_chunk, fused_max, oneshot_max, scratch_chunk, user_size;
+    uint64_t order_chunk, fused_max, oneshot_max, scratch_chunk, user_size, hheap_size;
 };
 
 /* One *_to_all call's device buffers outside the symmetric heap, as this PE
@@ -139,7 +139,12 @@ struct shmemi_state {
     char **peer_heap;           /* [npes]: mapped base of every PE's heap */
     struct shmemi_block *blocks;
 
-    /* host allocations made by shmem_malloc */
+    /* symmetric host heap (hostheap.c): shmem_malloc's blocks */
+    char *hheap;                /* this PE's segment */
+    size_t hheap_size;          /* SHMEM_SYMMETRIC_HEAP_SIZE, page-rounded */
+    int hheap_fd;               /* the shared-memory object (PE_size > 1), else -1 */
+    int hheap_named;            /* its name not yet dropped */
+    char **peer_hheap;          /* [npes]: every PE's segment, mapped here */
     struct shmemi_hostblk *host_blocks;
 
     /* RCCL */
@@ -228,12 +233,22 @@ void shmemi_barrier_arrive (int PE_start, int stride, int PE_size);
 int shmemi_in_device_heap (const void *p, size_t nbytes);
 size_t shmemi_heap_offset (const void *p);
 void *shmemi_peer_ptr (int pe, size_t off);
-void *shmemi_host_dev_ptr (const void *p, size_t nbytes);
 int shmemi_pe_same_device (int pe);
 void shmemi_order_after_caller (int host_wait);
 void shmemi_check_stream_err (const char *fn);
 void shmemi_peer_acquire (hipStream_t st);
 double shmemi_now (void);
+
+/* hostheap.c: shmem_malloc's symmetric heap in host memory, mapped by every PE */
+void shmemi_hheap_create (size_t size);
+void shmemi_hheap_attach (void);
+void shmemi_hheap_unlink (void);
+void shmemi_hheap_finalize (void);
+void *shmemi_host_malloc (size_t size);
+int shmemi_host_free (void *p);
+int shmemi_in_host_heap (const void *p, size_t nbytes);
+void *shmemi_host_peer_ptr (int pe, const void *p);
+void *shmemi_host_dev_ptr (const void *p, size_t nbytes);
 
 /* reduce.c: the persistent fused server; every GPU operation that could wait
  * on it (another spin-waiting grid, a device-wide synchronization, freeing

@@ -58,23 +58,33 @@ def run_datamove(shm, c, me, da, db, ha, hb, results):
         ctypes.memmove(tgt, sentinel.ctypes.data, sentinel.nbytes)
     else:
         shm.put(tgt, sentinel)
+    # "source": "host" -- the symmetric objects in shmem_malloc's host heap
+    # (every PE's segment mapped by every PE, csrc/hostheap.c) instead of the
+    # device heap: the collectives' sources, put targets and get sources
+    sym_host = c.get("source") == "host"
+    sa = ha if sym_host else da
     if len(x):
-        shm.put(da, x)
+        if sym_host:
+            ctypes.memmove(ha, x.ctypes.data, x.nbytes)
+        else:
+            shm.put(da, x)
     psync = shm._psync_ptr
     L = shm.lib
     vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
     if kind == "broadcast":
         f = getattr(L, f"shmem_broadcast{bits}")
         f.argtypes = [vp, vp, sz, i, i, i, i, vp]
-        f(tgt, da, c["n"], c["root"], start, logstride, size, psync)
+        f(tgt, sa, c["n"], c["root"], start, logstride, size, psync)
     elif kind in ("fcollect", "collect"):
         f = getattr(L, f"shmem_{kind}{bits}")
         f.argtypes = [vp, vp, sz, i, i, i, vp]
-        f(tgt, da, len(x), start, logstride, size, psync)
+        f(tgt, sa, len(x), start, logstride, size, psync)
     elif kind == "putget":
         # put my block into the next member's target at my slot, barrier, then
         # get the previous member's block from its source
         nxt, prv = mem[(mem.index(me) + 1) % size], mem[(mem.index(me) - 1) % size]
+        if sym_host:
+            ctypes.memmove(hb, sentinel.ctypes.data, sentinel.nbytes)
         L.shmem_barrier(start, logstride, size, psync)  # every target holds its sentinel
         f = getattr(L, f"shmem_put{bits}")
         f.argtypes = [vp, vp, sz, i]
@@ -87,16 +97,36 @@ def run_datamove(shm, c, me, da, db, ha, hb, results):
         elif c.get("put_from") == "pageable":
             keep = np.ascontiguousarray(x)
             src = keep.ctypes.data
-        f(db + mem.index(me) * c["n"] * es, src, c["n"], nxt)
+        elif c.get("put_from") == "device":
+            src = da
+        # symmetric target of the put: the device heap's db, or (host heap) the
+        # slot array hb; the get's symmetric source is sa, its local target
+        # the other array
+        symt = hb if sym_host else db
+        if sym_host and c.get("put_from") == "device":
+            shm.put(da, x)
+        f(symt + mem.index(me) * c["n"] * es, src, c["n"], nxt)
         L.shmem_barrier(start, logstride, size, psync)
-        g(hb if tgt_host else db + size * c["n"] * es, da, c["n"], prv)
+        if sym_host:   # local side of the get: device memory unless target=host (then plain numpy)
+            keep_get = np.zeros(c["n"], dtype=dt)
+            gdst = keep_get.ctypes.data if c.get("target") == "host" else db
+        else:
+            gdst = hb if tgt_host else db + size * c["n"] * es
+        g(gdst, sa, c["n"], prv)
         L.shmem_barrier(start, logstride, size, psync)
-        if tgt_host:
+        if sym_host and c.get("target") == "host":
+            got2 = keep_get.copy()
+        elif sym_host or not tgt_host:
+            got2 = shm.get(gdst, c["n"], dt)
+        else:
             got2 = np.empty(c["n"], dtype=dt)
             ctypes.memmove(got2.ctypes.data, hb, got2.nbytes)
-        else:
-            got2 = shm.get(db + size * c["n"] * es, c["n"], dt)
         results[str(c["id"]) + "_get"] = got2
+        if sym_host:   # the put slots, read locally from this PE's host heap
+            got = np.empty(cap, dtype=dt)
+            ctypes.memmove(got.ctypes.data, hb, got.nbytes)
+            results[str(c["id"])] = got
+            return
         tgt_host = False
         tgt = db
     if tgt_host:

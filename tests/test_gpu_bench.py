@@ -29,6 +29,9 @@ def free_port():
 
 
 def run(cmd, timeout=240, env=None):
+    # the bench sizes its own device heap (the in-process tests' fixture sets a small one in os.environ)
+    env = {k: v for k, v in (env or os.environ).items()
+           if k not in ("SHMEM_DEVICE_HEAP_SIZE", "SHMEM_DEVICE_SCRATCH_SIZE")}
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]

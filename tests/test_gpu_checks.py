@@ -135,6 +135,38 @@ def test_fused_acquires_follow_the_sysload_check(env, want):
         assert parse(out, "BAD")[0] == ["0", "SCHED", "fused-twoshot"], out
 
 
+FUSED_OFF = ("import oracle\n"
+             "print('THR', *shm.thresholds(), flush=True)\n"
+             "shm.set_fused_max(1 << 20)\n"
+             "print('THR2', *shm.thresholds(), flush=True)\n"
+             "d = shm.malloc_device(40000 * 8); t = shm.malloc_device(40000 * 8)\n"
+             "bad, scheds = 0, set()\n"
+             "for k in range(6):\n"
+             "    n = 40000 if k % 2 else 3000\n"
+             "    xs = [np.random.default_rng(1000 * k + p).random(n) - 0.5 for p in range(npes)]\n"
+             "    shm.put(d, xs[me])\n"
+             "    shm.to_all('sum', 'double', t, d, n, 0, 0, npes)\n"
+             "    scheds.add(shm.last_call_info()['schedule'])\n"
+             "    got = shm.get(t, n, 'double')\n"
+             "    bad += int((got.view(np.uint64) != oracle.reduce_pe('sum', 'double', xs, me).view(np.uint64)).sum())\n"
+             "print('BAD', bad, 'SCHED', *sorted(scheds), flush=True)\n"
+             "shm.finalize()\n")
+
+
+def test_stale_fused_ordering_turns_the_fused_kernel_off():
+    """PE 1 reports a caller's plain stores stale through the
+    fused kernel's flag ordering, with system-coherent loads AND after an
+    acquire (SHMEM_TEST_IPC_FAIL=producer_fused): every PE turns the fused
+    kernel off at init (fused_max 0, the warning on PE 0), the setter cannot
+    turn it back on, and the calls run the multi-launch schedule, bit-exact."""
+    rcs, outs, _ = spawn(3, FUSED_OFF, extra={"SHMEM_TEST_IPC_FAIL": "producer_fused"})
+    for rc, out in zip(rcs, outs):
+        assert rc == 0, out[-2000:]
+        assert parse(out, "THR")[0][0] == "0" and parse(out, "THR2")[0][0] == "0", out
+        assert parse(out, "BAD")[0] == ["0", "SCHED", "p2p"], out
+    assert "the fused kernel is disabled" in outs[0], outs[0]
+
+
 # ---------------------------------------------------------------------------
 # SHMEM_DEBUG=1 collective argument check
 # ---------------------------------------------------------------------------

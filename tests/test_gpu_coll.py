@@ -47,6 +47,32 @@ def check_dm(results, cases):
                     assert (results[pe][str(c["id"]) + "_get"] == srcs[prv]).all(), (c, pe)
 
 
+def test_host_heap_objects_three_pes(tmp_path):
+    """the symmetric objects in shmem_malloc's default host
+    heap (every PE's segment mapped by every PE, csrc/hostheap.c, as the
+    reference's segment exchange makes them reachable, comms-inline.h:766-845):
+    shmem_getmem / putmem (putget.c:249-256) with device, page-locked and
+    pageable local sides, broadcast from every root (broadcast-linear.c:61-82),
+    fcollect (fcollect-linear.c:60-93) and collect into device, host-heap and
+    pageable targets, on 3 PEs; every PE's result against the oracle."""
+    cases = []
+    cid = 0
+    for bits in (32, 64):
+        for root in (0, 1, 2):
+            cases.append(case(cid, "broadcast", bits, 300, [[0, 0, 3]], root=root, source="host")); cid += 1
+        for tk in ("device", "host", "pageable"):
+            cases.append(case(cid, "broadcast", bits, 129, [[0, 0, 3]], root=1, source="host", target=tk)); cid += 1
+            cases.append(case(cid, "fcollect", bits, 200, [[0, 0, 3]], source="host", target=tk)); cid += 1
+            cases.append(case(cid, "collect", bits, 5, [[0, 0, 3]], source="host", target=tk)); cid += 1
+        cases.append(case(cid, "fcollect", bits, 33, [[1, 0, 2]], source="host")); cid += 1
+        cases.append(case(cid, "broadcast", bits, 40, [[2, 0, 1]], root=0, source="host")); cid += 1
+        for pf in ("device", "host", "pageable"):
+            cases.append(case(cid, "putget", bits, 100, [[0, 0, 3]], source="host", put_from=pf)); cid += 1
+        cases.append(case(cid, "putget", bits, 51, [[0, 0, 3]], source="host", target="host")); cid += 1
+    results = run_pes(3, cases, tmp_path)
+    check_dm(results, cases)
+
+
 @pytest.mark.parametrize("fused", ["fused", "barrier_copy_barrier"])
 def test_collectives_four_pes(tmp_path, fused):
     """Small broadcast/fcollect run as one fused pull launch by default;

@@ -109,8 +109,8 @@ SOME = [("sum", "double"), ("sum", "float"), ("xor", "int"), ("and", "longlong")
         ("min", "short"), ("prod", "complexd"), ("sum", "longdouble")]
 
 
-@pytest.mark.parametrize("fused_max,oneshot_max", [("1M", "64K"), ("1M", "0"), ("0", "0")],
-                         ids=["fused-oneshot", "fused-twoshot", "multi-launch"])
+@pytest.mark.parametrize("fused_max,oneshot_max", [("1M", "64K"), ("2M", "0"), ("0", "0")],
+                         ids=["fused-oneshot", "fused-twoshot-2M", "multi-launch"])
 def test_four_pes_all_44_pairs_p2p_and_exact(tmp_path, fused_max, oneshot_max):
     """Every pair on 4 PEs, through the one-launch fused kernel (messages up to
     1 MiB; one-shot fold up to 64 KiB, reduce-scatter + all-gather above) and
@@ -132,8 +132,8 @@ GOLDEN_ROWS = json.load(open(os.path.join(HERE, "golden", "manifest.json")))["ca
 NAN_ROWS = json.load(open(os.path.join(HERE, "golden", "manifest.json")))["nan_cases"]
 
 
-@pytest.mark.parametrize("fused_max,oneshot_max", [("1M", "64K"), ("1M", "0"), ("0", "0")],
-                         ids=["fused-oneshot", "fused-twoshot", "multi-launch"])
+@pytest.mark.parametrize("fused_max,oneshot_max", [("1M", "64K"), ("2M", "0"), ("0", "0")],
+                         ids=["fused-oneshot", "fused-twoshot-2M", "multi-launch"])
 def test_golden_fixtures_on_every_pe(tmp_path, fused_max, oneshot_max):
     """The committed golden vectors (outputs of the reference's own compiled
     operators in each member's fold order, NaN / +-0 / Inf / x87 encodings
@@ -489,7 +489,7 @@ def test_external_device_buffers_fallbacks(tmp_path):
 def test_external_buffer_open_failure_stages_the_call(tmp_path):
     """A member that cannot open a peer's exported buffer (simulated on PE 1,
     SHMEM_TEST_IPC_FAIL=extopen; HIP refuses the handle of an allocation its
-    owner has freed, tools/ipc_reopen_probe.py) does not abort the job: after the
+    owner has freed; profiles/r04/ipc_reopen_probe.json) does not abort the job: after the
     second round of the record exchange every member stages the call, and the
     results stay exact on every PE, fused and multi-launch sizes alike."""
     cases = make_cases(MAPPED_PAIRS, 5000, [[0, 0, 3]], "devother", "p2p", 0)

@@ -46,7 +46,7 @@ def test_levels_file_and_format(tmp_path):
     assert {lvl for _, lvl, _ in lines} == {"MEMORY", "BARRIER"}
     for pe in (0, 1):
         msgs = [m for p, lvl, m in lines if p == pe and lvl == "MEMORY"]
-        assert any(re.match(r"shmem_malloc\(4096\) = 0x[0-9a-f]+ \(host\)", m) for m in msgs), msgs
+        assert any(re.match(r"shmem_malloc\(4096\) = 0x[0-9a-f]+ \(symmetric host heap\)", m) for m in msgs), msgs
         assert sum(1 for p, lvl, m in lines if p == pe and m == "shmem_barrier_all") >= 3
 
 

@@ -21,7 +21,7 @@ import tempfile
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 import check_residency as cr  # noqa: E402
 
-LLVM = "/opt/rocm/lib/llvm/bin"
+from check_residency import LLVM  # noqa: E402  (one LLVM path for both tools)
 
 
 def kind(op):
