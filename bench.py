@@ -514,10 +514,17 @@ def kernel_legs(shm, reps, check):
     for e in ev:
         L.hipEventCreate(ctypes.byref(e))
     res = {}
+    rewritten = 0   # sources a long double / complex leg overwrote (the others read hosts' bytes)
     for name, kname, op, dtype, k, nbytes, orders in KERNEL_LEGS:
         es = np.dtype(shmem_reduce.NP[dtype]).itemsize
         n = nbytes // es
         nout = k if orders else 1
+        if dtype not in ("longdouble", "complexf"):
+            for p in range(rewritten):
+                shm.put(srcs[p], hosts[p])
+            rewritten = 0
+        else:
+            rewritten = max(rewritten, k)
         if dtype == "longdouble":   # realistic x87 operands, not doubles' bytes read as x87
             lds = [hosts[p][:n].astype(np.longdouble) for p in range(k)]
             for p in range(k):

@@ -90,7 +90,7 @@ def run_datamove(shm, c, me, da, db, ha, hb, results):
         f.argtypes = [vp, vp, sz, i]
         g = getattr(L, f"shmem_get{bits}")
         g.argtypes = [vp, vp, sz, i]
-        src = da
+        src = ha if sym_host else da     # the local side holding x by default
         if c.get("put_from") == "host":  # page-locked shmem_malloc source
             ctypes.memmove(ha, x.ctypes.data, x.nbytes)
             src = ha

@@ -16,7 +16,7 @@
 //
 // build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/cold_probe.hip \
 //          -L osss-gasnet_amd/lib -lshmem_reduce -Wl,-rpath,$PWD/osss-gasnet_amd/lib -o tools/cold_probe
-// run:   tools/cold_probe [lib|copy|all]   (one JSON line per measurement)
+// run:   tools/cold_probe [lib|copy|all|copy2|orders]   (one JSON line per measurement)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -102,6 +102,43 @@ __global__ __launch_bounds__(256) void copy_chunk(const u32x4 *s, u32x4 *d, uint
         for (int u = 0; u < U; ++u) {
             const uint64_t i = base + (uint64_t)u * 256;
             if (i < hi) st<ST>(d + i, x[u]);
+        }
+    }
+}
+
+// ---- every-member fold variants (the library's combine_orders_vec for a
+// double sum at 8 sources: member q's chain is src q, then the others in
+// member order; 8 loads and 8 stores per vector)
+template <int U, int LD, int ST>
+__global__ __launch_bounds__(256) void orders8(const u32x4 *s0, const u32x4 *s1, const u32x4 *s2, const u32x4 *s3,
+                                               const u32x4 *s4, const u32x4 *s5, const u32x4 *s6, const u32x4 *s7,
+                                               u32x4 *d0, u32x4 *d1, u32x4 *d2, u32x4 *d3, u32x4 *d4, u32x4 *d5,
+                                               u32x4 *d6, u32x4 *d7, uint64_t nvec) {
+    const u32x4 *s[8] = {s0, s1, s2, s3, s4, s5, s6, s7};
+    u32x4 *d[8] = {d0, d1, d2, d3, d4, d5, d6, d7};
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    const uint64_t step = (uint64_t)gridDim.x * 256 * U;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 * U + threadIdx.x; base < nvec; base += step) {
+        u32x4 x[U][8];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = base + (uint64_t)u * 256;
+            if (i < nvec)
+#pragma unroll
+                for (int k = 0; k < 8; ++k) x[u][k] = ld<LD>(s[k] + i);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = base + (uint64_t)u * 256;
+            if (i >= nvec) continue;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                f64x2 acc = __builtin_bit_cast(f64x2, x[u][q]);
+#pragma unroll
+                for (int k = 0; k < 8; ++k)
+                    if (k != q) acc += __builtin_bit_cast(f64x2, x[u][k]);
+                st<ST>(d[q] + i, __builtin_bit_cast(u32x4, acc));
+            }
         }
     }
 }
@@ -247,6 +284,29 @@ static void lib_orders(const char *name, int op, int dtype, int k, size_t bytes)
     emit(name, v, (size_t)nbuf * bytes, nsets, w, c);
 }
 
+template <typename K>
+static void orders_variant(const char *name, K kern, int bpc, int u, size_t bytes) {
+    const uint64_t nvec = bytes / 16;
+    const int nsets = sets_for(16 * bytes);
+    uint64_t want = (nvec + 256ull * u - 1) / (256ull * u);
+    const unsigned grid = (unsigned)std::min<uint64_t>(want, (uint64_t)g_cus * bpc);
+    auto launch = [&](int st) {
+        const u32x4 *sp[8];
+        u32x4 *dp[8];
+        for (int k = 0; k < 8; ++k) {
+            sp[k] = (const u32x4 *)buf(st, k, 16, bytes);
+            dp[k] = (u32x4 *)buf(st, 8 + k, 16, bytes);
+        }
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(256), 0, 0, sp[0], sp[1], sp[2], sp[3], sp[4], sp[5], sp[6], sp[7],
+                           dp[0], dp[1], dp[2], dp[3], dp[4], dp[5], dp[6], dp[7], nvec);
+    };
+    Stat w = timed(launch, nsets, false, 30);
+    Stat c = timed(launch, nsets, true, std::max(40, 4 * nsets));
+    char v[96];
+    snprintf(v, sizeof v, "%s bpc=%d U=%d", name, bpc, u);
+    emit("orders8<sum,double>", v, 16 * bytes, nsets, w, c);
+}
+
 int main(int argc, char **argv) {
     const std::string what = argc > 1 ? argv[1] : "all";
     CHECK(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -291,6 +351,29 @@ int main(int argc, char **argv) {
         copy_variant("chunk ld=plain st=nt_sc1", copy_chunk<4, LD_PLAIN, ST_NT_SC1>, 1, 4, S, true);
         copy_variant("chunk ld=plain st=nt_sc1", copy_chunk<4, LD_PLAIN, ST_NT_SC1>, 2, 4, S, true);
         copy_variant("chunk ld=nt st=nt_sc1", copy_chunk<4, LD_NT, ST_NT_SC1>, 2, 4, S, true);
+    }
+    if (what == "copy2") {   // round 5: cold copy, more policies
+        copy_variant("pipe ld=nt st=nt_sc1", copy_pipe<4, LD_NT, ST_NT_SC1>, 2, 4, S);
+        copy_variant("pipe ld=nt st=nt_sc1", copy_pipe<2, LD_NT, ST_NT_SC1>, 4, 2, S);
+        copy_variant("pipe ld=nt st=nt_sc1", copy_pipe<8, LD_NT, ST_NT_SC1>, 2, 8, S);
+        copy_variant("pipe ld=nt st=nt_sc1", copy_pipe<4, LD_NT, ST_NT_SC1>, 4, 4, S);
+        copy_variant("pipe ld=nt st=nt", copy_pipe<4, LD_NT, ST_NT>, 2, 4, S);
+        copy_variant("pipe ld=nt st=plain", copy_pipe<4, LD_NT, ST_PLAIN>, 2, 4, S);
+        copy_variant("pipe ld=plain st=nt_sc1", copy_pipe<4, LD_PLAIN, ST_NT_SC1>, 1, 4, S);
+    }
+    if (what == "orders") {   // round 5: the every-member fold, cold
+        const size_t B = 32 * MiB;
+        orders_variant("ld=nt st=sc1", orders8<4, LD_NT, ST_SC1>, 8, 4, B);   // = library (Shape<8>)
+        orders_variant("ld=nt st=sc1", orders8<2, LD_NT, ST_SC1>, 8, 2, B);
+        orders_variant("ld=nt st=sc1", orders8<1, LD_NT, ST_SC1>, 8, 1, B);
+        orders_variant("ld=nt st=sc1", orders8<4, LD_NT, ST_SC1>, 2, 4, B);
+        orders_variant("ld=nt st=sc1", orders8<2, LD_NT, ST_SC1>, 4, 2, B);
+        orders_variant("ld=nt st=nt_sc1", orders8<4, LD_NT, ST_NT_SC1>, 8, 4, B);
+        orders_variant("ld=nt st=nt_sc1", orders8<2, LD_NT, ST_NT_SC1>, 4, 2, B);
+        orders_variant("ld=plain st=nt_sc1", orders8<4, LD_PLAIN, ST_NT_SC1>, 8, 4, B);
+        orders_variant("ld=plain st=sc1", orders8<4, LD_PLAIN, ST_SC1>, 8, 4, B);
+        orders_variant("ld=nt st=nt", orders8<4, LD_NT, ST_NT>, 8, 4, B);
+        orders_variant("ld=nt st=plain", orders8<4, LD_NT, ST_PLAIN>, 8, 4, B);
     }
     CHECK(hipFree(g_pool));
     return 0;
