@@ -18,6 +18,14 @@ export TMPDIR=/tmp
 BENCH=(bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-small --no-ops --no-rotating)
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o run -- python3 "${BENCH[@]}" \
     > "$OUT/bench_trace.log" 2>&1
+# the HBM-only headline (bench.py headline_rotating): its copy_segments<4,1>
+# dispatches come after the headline's 620 (20 warm-up + 3 x 200); the last
+# 200 are its event-stamped pass
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace_rot" -o run -- python3 bench.py \
+    --steps 200 --warmup 20 --no-cpu-baseline --no-small --no-ops --no-kernels --no-host-staged \
+    > "$OUT/bench_trace_rot.log" 2>&1
+python3 tools/trace_split.py "$OUT/trace_rot" "copy_segments<4, 1>" 200 620 > "$DST/rocprof_rotating_split.json"
+grep "^{\"metric\"" "$OUT/bench_trace_rot.log" > "$DST/bench_n1_rotating_under_rocprof.json"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/fetch" -o run -- python3 "${BENCH[@]}" --no-check \
     > "$OUT/bench_fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/write" -o run -- python3 "${BENCH[@]}" --no-check \
