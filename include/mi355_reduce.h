@@ -85,6 +85,13 @@ int mi355_combine_orders (int op, int dtype, void *const *dsts, const void *cons
 int mi355_copy_segments (void *const *dsts, const void *const *srcs,
                          const size_t *nbytes, int nseg, void *stream);
 
+/* The two-member all-gather of a float/double sum or product: dst[i] =
+ * own[i] quieted where own[i] is a NaN, else peer[i] (the other member's shard,
+ * folded in its order: the same bits as this member's order except where
+ * both operands are NaNs, where SSE keeps the first). Pointers 16-byte
+ * aligned; own may alias dst. */
+int mi355_nan_patch_copy (int dtype, void *dst, const void *peer, const void *own, size_t n, void *stream);
+
 /* Attach a pair of HIP events (hipEvent_t, created by the caller with timing
  * enabled) to the NEXT kernel this layer launches from the calling thread:
  * the runtime stamps that kernel's own start and end (hipExtLaunchKernel),

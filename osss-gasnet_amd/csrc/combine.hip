@@ -136,6 +136,69 @@ __global__ __launch_bounds__(kBlock) void copy_segments(SegParams<NS> p) {
     signal_done(p.sig, __syncthreads_or(plain));
 }
 
+// The two-member all-gather of a float/double sum or product (reduce.c,
+// nan_pair): member q copies the other member p's shard, which p folded in
+// ITS order, x86(a_p op a_q), and needs x86(a_q op a_p). The two are the same
+// bits except where both operands are NaNs: SSE returns the first NaN
+// operand, quieted (ops.h x86_result) -- a_q for q. So wherever q's own
+// source a_q is a NaN the result is a_q quieted, elsewhere the copied value:
+//   dst[i] = isnan(own[i]) ? quiet(own[i]) : peer[i]
+// (own may alias dst: element-wise read-then-write). Plain loads and `nt sc1`
+// stores as the copy kernel; one more local read stream than the copy.
+// nvec == 0: every element through the element loop (unaligned pointers).
+struct PatchParams {
+    void *dst;
+    const void *peer;
+    const void *own;
+    uint64_t nvec;   // whole 16-byte vectors
+    uint64_t n;      // elements
+    Signal sig;
+};
+
+template <typename R>
+__device__ __forceinline__ R nan_keep_own(R own, R peer) {
+    using N = X86Nan<R>;
+    using U = typename N::U;
+    return __builtin_isnan(own) ? __builtin_bit_cast(R, __builtin_bit_cast(U, own) | N::quiet) : peer;
+}
+
+template <typename R>
+__global__ __launch_bounds__(kBlock) void nan_patch_copy(PatchParams p) {
+    constexpr int V = 16 / sizeof(R);
+    constexpr int U = 4;
+    const u32x4 *pe = (const u32x4 *)p.peer;
+    const u32x4 *ow = (const u32x4 *)p.own;
+    u32x4 *d = (u32x4 *)p.dst;
+    const uint64_t step = (uint64_t)gridDim.x * kBlock * U;
+    for (uint64_t base = (uint64_t)blockIdx.x * kBlock * U + threadIdx.x; base < p.nvec; base += step) {
+        Pack<R> x[U], o[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = base + (uint64_t)u * kBlock;
+            if (i < p.nvec) {
+                x[u].v = ld16<POL_PLAIN>(pe + i);
+                o[u].v = ld16<POL_PLAIN>(ow + i);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = base + (uint64_t)u * kBlock;
+            if (i < p.nvec) {
+#pragma unroll
+                for (int e = 0; e < V; ++e) x[u].e[e] = nan_keep_own(o[u].e[e], x[u].e[e]);
+                st16(d + i, x[u].v);
+            }
+        }
+    }
+    bool plain = false;
+    for (uint64_t i = p.nvec * V + (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < p.n;
+         i += (uint64_t)gridDim.x * kBlock) {
+        ((R *)p.dst)[i] = nan_keep_own(((const R *)p.own)[i], ((const R *)p.peer)[i]);
+        plain = true;
+    }
+    signal_done(p.sig, __syncthreads_or(plain));
+}
+
 // One block that only carries the completion signal: tells the host when the
 // stream has reached this point (everything queued before it has finished).
 struct EmptyParams {
@@ -315,6 +378,32 @@ static int copy_segments_impl(void *const *dsts, const void *const *srcs, const 
         return launch(copy_segments<U, 1>, dim3(gx, 1), (hipStream_t)stream, p1);
     }
     return launch(copy_segments<U, kMaxSeg>, dim3(gx, used), (hipStream_t)stream, p);
+}
+
+extern "C" int mi355_nan_patch_copy(int dtype, void *dst, const void *peer, const void *own, size_t n,
+                                    void *stream) {
+    const int rc = [&]() -> int {
+        if (dtype != MI355_FLOAT && dtype != MI355_DOUBLE) return MI355_E_UNSUP;
+        if (n == 0) {
+            fire_on_host((hipStream_t)stream);
+            return 0;
+        }
+        if (dst == nullptr || peer == nullptr || own == nullptr) return MI355_E_INVAL;
+        const size_t es = mi355_dtype_size(dtype);
+        // 16-byte vectors when every pointer is aligned (the heap's shards
+        // are), else element by element (a user offset into the arrays)
+        const bool vec = (((uintptr_t)dst | (uintptr_t)peer | (uintptr_t)own) & 15) == 0;
+        PatchParams p{dst, peer, own, vec ? (uint64_t)(n * es / 16) : 0, (uint64_t)n, Signal{}};
+        const unsigned grid = vec ? grid_for((uint64_t)kBlock * 4, p.nvec > 0 ? p.nvec : 1, 1)
+                                  : grid_for((uint64_t)kBlock * 4, p.n, 1);
+        return dtype == MI355_FLOAT ? launch(nan_patch_copy<float>, dim3(grid), (hipStream_t)stream, p)
+                                    : launch(nan_patch_copy<double>, dim3(grid), (hipStream_t)stream, p);
+    }();
+    if (rc != 0) {
+        t_sig = Signal{nullptr, nullptr, 0};
+        t_ev_start = t_ev_stop = nullptr;
+    }
+    return rc;
 }
 
 // System-scope acquire on every XCD of this GPU (`buffer_inv sc0 sc1`): drops

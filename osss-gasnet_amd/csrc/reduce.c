@@ -199,6 +199,20 @@ static int ordered_pair (int op, int dtype, int size)
     return order_sensitive (op, dtype, size) && size <= MI355_ORDERS_MAX_SOURCES;
 }
 
+/* Two members, float or double sum/prod, each member's own order: the
+ * members' results differ only where both operands are NaNs (SSE keeps the
+ * first). The multi-launch schedules then skip the version areas: each owner
+ * folds its shard in ITS order (own source first) and the other member
+ * gathers it NaN-patched from its own source (mi355_nan_patch_copy): one
+ * output per shard, one more local read in the gather. (Complex types keep
+ * the version areas: the imaginary part of gcc's float complex add takes the
+ * incoming operand first, and Annex G's product is not a plain pair.) */
+static int nan_pair (int op, int dtype, const struct aset *s)
+{
+    return shmemi.order == SHMEMX_ORDER_REFERENCE && s->size == 2 && (dtype == MI355_FLOAT || dtype == MI355_DOUBLE) &&
+           (op == MI355_OP_SUM || op == MI355_OP_PROD);
+}
+
 /* Version areas: on every PE, one per signal-region channel, (size - 1)
  * slots of one shard each; slot s of owner i holds member q's version of
  * shard i, s = q < i ? q : q - 1. Each slot starts at the target's offset
@@ -298,7 +312,7 @@ void shmemi_dev_barrier (int PE_start, int stride, int PE_size, int me, int last
  * version area on channel `chan`. Returns the launch's status (0: queued, or
  * nothing to do: empty shard). */
 static int fold_shard (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n, const struct aset *s,
-                       int ordered, int chan, hipStream_t st)
+                       int ordered, int pair, int chan, hipStream_t st)
 {
     const void *sp[MI355_FUSED_MAX_MEMBERS > MI355_ORDERS_MAX_SOURCES ? MI355_FUSED_MAX_MEMBERS
                                                                        : MI355_ORDERS_MAX_SOURCES];
@@ -314,6 +328,11 @@ static int fold_shard (int op, int dtype, size_t es, size_t dst_off, size_t src_
     }
     for (int i = 0; i < s->size; ++i)
         spp[i] = shmemi_peer_ptr (aset_pe (s, i), src_off + lo * es);
+    if (pair && s->me == 1) { /* nan_pair: this owner's order, its own source first */
+        const void *t = spp[0];
+        spp[0] = spp[1];
+        spp[1] = t;
+    }
     void *dst = shmemi_peer_ptr (shmemi.mype, dst_off + lo * es);
     int rc;
     if (!ordered) {
@@ -355,13 +374,27 @@ static int gather_segments (size_t es, size_t dst_off, size_t n, const struct as
     return k;
 }
 
+/* nan_pair's gather: the other member's shard from its target, where this
+ * PE's own source is a NaN that NaN quieted instead. 0: queued, or nothing to
+ * do (an empty shard: fires an armed signal). */
+static int pair_gather (int dtype, size_t es, size_t dst_off, size_t src_off, size_t n, const struct aset *s,
+                        hipStream_t st)
+{
+    const int other = 1 - s->me;
+    size_t l, h;
+    mi355_shard_bounds (n, es, 2, other, &l, &h);
+    return mi355_nan_patch_copy (dtype, shmemi_peer_ptr (shmemi.mype, dst_off + l * es),
+                                 shmemi_peer_ptr (aset_pe (s, other), dst_off + l * es),
+                                 shmemi_peer_ptr (shmemi.mype, src_off + l * es), h > l ? h - l : 0, st);
+}
+
 /* P2P shard schedule, dst and src disjoint or identical, with the three
  * barriers as one-block device-barrier kernels on the library stream: five
  * launches queued back to back, one host wait (the last barrier carries the
  * completion flag). The first barrier also orders the sources: each PE's
  * arrival is stream-ordered after its caller's work. */
 static void p2p_range_dev (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
-                           const struct aset *s, int ordered)
+                           const struct aset *s, int ordered, int pair)
 {
     MI355FusedArgs a;
     member_args (&a, s, SHMEMI_CHAN_HOST);
@@ -372,14 +405,21 @@ static void p2p_range_dev (int op, int dtype, size_t es, size_t dst_off, size_t 
     device_barrier (&a, shmemi.stream); /* every source is ready */
     shmemi_peer_acquire (shmemi.stream);
     shmemi_timed_begin ();
-    int rc = fold_shard (op, dtype, es, dst_off, src_off, n, s, ordered, SHMEMI_CHAN_HOST, shmemi.stream);
+    int rc = fold_shard (op, dtype, es, dst_off, src_off, n, s, ordered, pair, SHMEMI_CHAN_HOST, shmemi.stream);
     shmemi_timed_end ();
     if (rc != 0)
         shmemi_fatal ("combine kernel launch failed (op %d, dtype %d, %d sources, %zu elements): %d", op, dtype,
                       s->size, n, rc);
     device_barrier (&a, shmemi.stream); /* every shard is reduced */
     shmemi_peer_acquire (shmemi.stream);
-    const int k = gather_segments (es, dst_off, n, s, ordered, SHMEMI_CHAN_HOST, dsts, sp, nb);
+    const int k = pair ? 0 : gather_segments (es, dst_off, n, s, ordered, SHMEMI_CHAN_HOST, dsts, sp, nb);
+    if (pair) {
+        shmemi_timed_begin_phase (1);
+        rc = pair_gather (dtype, es, dst_off, src_off, n, s, shmemi.stream);
+        shmemi_timed_end ();
+        if (rc != 0)
+            shmemi_fatal ("gather kernel launch failed: %d", rc);
+    }
     if (k > 0) {
         shmemi_timed_begin_phase (1);
         rc = mi355_copy_segments (dsts, sp, nb, k, shmemi.stream);
@@ -410,7 +450,7 @@ static void host_order (void)
 
 /* P2P shard schedule (host barriers), dst and src disjoint or identical. */
 static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n,
-                       const struct aset *s, int ordered)
+                       const struct aset *s, int ordered, int pair)
 {
     const void **sp = (const void **) malloc (sizeof (void *) * (size_t) s->size);
     void **dsts = (void **) malloc (sizeof (void *) * (size_t) s->size);
@@ -427,7 +467,7 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
         shmemi_peer_acquire (shmemi.stream);
         shmemi_timed_begin ();
         shmemi_arm_signal ();
-        int rc = fold_shard (op, dtype, es, dst_off, src_off, n, s, ordered, SHMEMI_CHAN_HOST, shmemi.stream);
+        int rc = fold_shard (op, dtype, es, dst_off, src_off, n, s, ordered, pair, SHMEMI_CHAN_HOST, shmemi.stream);
         shmemi_timed_end ();
         if (rc != 0)
             shmemi_fatal ("combine kernel launch failed (op %d, dtype %d, %d sources, %zu elements): %d", op,
@@ -438,8 +478,16 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
     shmemi_peer_acquire (shmemi.stream);
 
     /* gather the other members' shards: one launch */
-    const int k = gather_segments (es, dst_off, n, s, ordered, SHMEMI_CHAN_HOST, dsts, sp, nb);
-    copy_wait (dsts, sp, nb, k, 1);
+    if (pair) {
+        shmemi_arm_signal ();
+        const int rc = pair_gather (dtype, es, dst_off, src_off, n, s, shmemi.stream);
+        if (rc != 0)
+            shmemi_fatal ("gather kernel launch failed: %d", rc);
+        shmemi_wait_signal ();
+    } else {
+        const int k = gather_segments (es, dst_off, n, s, ordered, SHMEMI_CHAN_HOST, dsts, sp, nb);
+        copy_wait (dsts, sp, nb, k, 1);
+    }
     shmemi_barrier_set (s->start, s->stride, s->size); /* peers are done reading us */
     free (nb);
     free (dsts);
@@ -450,20 +498,24 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
  * versions outgrow the version area) several, each a complete schedule. */
 static void p2p_any (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n, const struct aset *s)
 {
-    const int ordered = ordered_pair (op, dtype, s->size);
+    const int pair = nan_pair (op, dtype, s);
+    const int ordered = ordered_pair (op, dtype, s->size) && !pair;
     const int dev = device_flags_ok (s);
     const size_t round = ordered ? ordered_round_elems (es, s->size) : n;
     SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: P2P shards, %s barriers, %s (%zu elements, %d members%s)",
-                  dev ? "device" : "host", ordered ? "every member's reference order" : "PE_start order", n, s->size,
-                  ordered && n > round ? ", several rounds" : "");
+                  dev ? "device" : "host",
+                  pair      ? "each member's reference order (own-order fold, NaN-patched gather)"
+                  : ordered ? "every member's reference order"
+                            : "PE_start order",
+                  n, s->size, ordered && n > round ? ", several rounds" : "");
     begin_call (dev ? (n > round ? "p2p-rounds" : "p2p") : (n > round ? "p2p-host-rounds" : "p2p-host"));
     size_t b = 0;
     do {
         const size_t cn = n - b < round ? n - b : round;
         if (dev)
-            p2p_range_dev (op, dtype, es, dst_off + b * es, src_off + b * es, cn, s, ordered);
+            p2p_range_dev (op, dtype, es, dst_off + b * es, src_off + b * es, cn, s, ordered, pair);
         else
-            p2p_range (op, dtype, es, dst_off + b * es, src_off + b * es, cn, s, ordered);
+            p2p_range (op, dtype, es, dst_off + b * es, src_off + b * es, cn, s, ordered, pair);
         b += cn;
     } while (b < n);
 }
@@ -1272,20 +1324,27 @@ static void reduce_on_stream (int op, int dtype, const char *fn, void *target, c
             void *dsts[MI355_FUSED_MAX_MEMBERS];
             const void *sp[MI355_FUSED_MAX_MEMBERS];
             size_t nb[MI355_FUSED_MAX_MEMBERS];
-            const size_t round = ordered ? ordered_round_elems (es, s.size) : n;
+            const int pair = nan_pair (op, dtype, &s);
+            const int ord = ordered && !pair;
+            const size_t round = ord ? ordered_round_elems (es, s.size) : n;
             begin_call (n > round ? "stream-p2p-rounds" : "stream-p2p");
             for (size_t b = 0; b < n; b += round) {
                 const size_t cn = n - b < round ? n - b : round;
                 const size_t d0 = dst_off + b * es, s0 = src_off + b * es;
                 stream_barrier (fn, &s, st); /* every source is ready */
                 shmemi_peer_acquire (st);
-                const int rc = fold_shard (op, dtype, es, d0, s0, cn, &s, ordered, SHMEMI_CHAN_STREAM, st);
+                const int rc = fold_shard (op, dtype, es, d0, s0, cn, &s, ord, pair, SHMEMI_CHAN_STREAM, st);
                 if (rc != 0)
                     shmemi_fatal ("%s: combine kernel launch failed: %d", fn, rc);
                 stream_barrier (fn, &s, st); /* every shard is reduced */
                 shmemi_peer_acquire (st);
-                const int k = gather_segments (es, d0, cn, &s, ordered, SHMEMI_CHAN_STREAM, dsts, sp, nb);
-                stream_copy (fn, dsts, sp, nb, k, st);
+                if (pair) {
+                    if (pair_gather (dtype, es, d0, s0, cn, &s, st) != 0)
+                        shmemi_fatal ("%s: gather kernel launch failed", fn);
+                } else {
+                    const int k = gather_segments (es, d0, cn, &s, ord, SHMEMI_CHAN_STREAM, dsts, sp, nb);
+                    stream_copy (fn, dsts, sp, nb, k, st);
+                }
                 stream_barrier (fn, &s, st); /* peers are done reading this target and version area */
             }
         }

@@ -126,20 +126,21 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
     cb = d["cpu_baseline"]
     assert cb["cores"] == 2 and cb["value"] > 0 and cb["kind"] == "port" and cb["host"]["nproc"] >= 2
     # the roofline kernel is the one the library ran: the trace's schedule
-    # line for the 256 MiB calls says which fold (a 2-member double sum is
-    # order-sensitive: where both operands are NaNs the first one comes out,
-    # so each member's own order -- combine_orders_vec, two outputs)
+    # line for the 256 MiB calls says which fold (a 2-member double sum: each
+    # owner folds its shard in its own order, the plain fold with one output,
+    # and the other member gathers it NaN-patched -- where both operands are
+    # NaNs SSE keeps the first, reduce.c nan_pair)
     S = d["config"]["bytes_per_pe"]
     n = S // 8
     lines = [ln for ln in open(log).read().splitlines() if "schedule:" in ln and f"({n} elements" in ln]
     assert lines, "no schedule trace line for the 256 MiB calls"
-    assert all("P2P shards, device barriers, every member's reference order" in ln for ln in lines), lines[:3]
+    assert all("P2P shards, device barriers, each member's reference order (own-order fold, NaN-patched gather)"
+               in ln for ln in lines), lines[:3]
     r = d["roofline"]
-    assert re.fullmatch(r"void mi355k::combine_orders_vec<0, double, 2, \d, \d, true>\(mi355k::OrdersParams\)",
-                        r["kernel"]), r
+    assert re.fullmatch(r"void mi355k::combine_vec<0, double, 2, \d, \d>\(mi355k::CombineParams\)", r["kernel"]), r
     shard = S // 2
-    assert r["call"]["schedule"] == "p2p" and r["call"]["sources"] == 2 and r["call"]["outputs"] == 2, r
-    assert r["xgmi_view"]["alg_bytes_per_launch"] == shard and r["alg_bytes_per_launch"] == 4 * shard, r
+    assert r["call"]["schedule"] == "p2p" and r["call"]["sources"] == 2 and r["call"]["outputs"] == 1, r
+    assert r["xgmi_view"]["alg_bytes_per_launch"] == shard and r["alg_bytes_per_launch"] == 3 * shard, r
     # both PEs' folds share this GPU's HBM: the device rate counts both PEs' bytes over the call's
     # wall time (a window holding both launches), so it cannot pass the peak
     assert r["pes_on_gpu"] == 2 and 0 < r["frac"] <= 1.0, r

@@ -171,9 +171,14 @@ def test_nan_payload_fixtures_on_every_pe(tmp_path, fused_max, oneshot_max):
     for key, rows in NAN_ROWS.items():
         op, dtype = key.split("_")
         for k, row in enumerate(rows):
-            cases.append({"id": cid, "op": op, "dtype": dtype, "n": row["n"], "sets": [[0, 0, row["npes"]]],
-                          "mode": "dev", "algorithm": "p2p", "seed": 0, "golden": k, "family": "nan_"})
-            cid += 1
+            # two members: also in place, host arrays, unaligned and outside the heap (the two-member
+            # schedule folds each shard in its owner's order and NaN-patches the gather, reduce.c nan_pair)
+            modes = ["dev"] + (["inplace", "host", "unaligned", "devmap_offset", "overlap_up"]
+                               if row["npes"] == 2 else [])
+            for mode in modes:
+                cases.append({"id": cid, "op": op, "dtype": dtype, "n": row["n"], "sets": [[0, 0, row["npes"]]],
+                              "mode": mode, "algorithm": "p2p", "seed": 0, "golden": k, "family": "nan_"})
+                cid += 1
     results = run_pes(9, cases, tmp_path, extra_env={"SHMEM_FUSED_MAX_BYTES": fused_max,
                                                      "SHMEM_ONESHOT_MAX_BYTES": oneshot_max})
     for c in cases:
