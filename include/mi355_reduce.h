@@ -88,9 +88,17 @@ int mi355_copy_segments (void *const *dsts, const void *const *srcs,
 /* The two-member all-gather of a float/double sum or product: dst[i] =
  * own[i] quieted where own[i] is a NaN, else peer[i] (the other member's shard,
  * folded in its order: the same bits as this member's order except where
- * both operands are NaNs, where SSE keeps the first). Pointers 16-byte
- * aligned; own may alias dst. */
-int mi355_nan_patch_copy (int dtype, void *dst, const void *peer, const void *own, size_t n, void *stream);
+ * both operands are NaNs, where SSE keeps the first). own may alias dst.
+ * nan_flag (may be NULL): the other member's word set by its fold when a NaN
+ * came out (mi355_nan_flag_next_launch); while it reads 0 no result is NaN,
+ * so the kernel copies peer[] and does not read own[]. */
+int mi355_nan_patch_copy (int dtype, void *dst, const void *peer, const void *own, size_t n,
+                          const unsigned long long *nan_flag, void *stream);
+
+/* The NEXT fold this layer launches from the calling thread (mi355_combine,
+ * float/double sum or product) stores 1 to *set (system scope) if any of its
+ * results is a NaN, and 0 to *clear first (either may be NULL). */
+void mi355_nan_flag_next_launch (unsigned long long *set, unsigned long long *clear);
 
 /* Attach a pair of HIP events (hipEvent_t, created by the caller with timing
  * enabled) to the NEXT kernel this layer launches from the calling thread:
@@ -151,7 +159,11 @@ int mi355_convert_short (int widen, const void *src, void *dst, size_t n, void *
 #define MI355_SIG_CHANNELS 2
 #define MI355_SIG_SELFTEST (MI355_SIG_CHANNELS * MI355_SIG_CHANNEL_WORDS) /* [PE]: init-time check */
 #define MI355_SIG_SELFTEST2 (MI355_SIG_SELFTEST + 1024) /* [PE]: init-time producer-path check */
-#define MI355_SIG_WORDS (MI355_SIG_SELFTEST2 + 1024)
+/* [channel][parity][partner PE]: "a NaN came out of this PE's two-member fold
+ * of this parity's call with that partner" (mi355_nan_flag_next_launch) */
+#define MI355_SIG_NANFLAG (MI355_SIG_SELFTEST2 + 1024)
+#define MI355_SIG_NANFLAG_AT(chan, parity, pe) (MI355_SIG_NANFLAG + ((chan) * 2 + (parity)) * 1024 + (pe))
+#define MI355_SIG_WORDS (MI355_SIG_NANFLAG + MI355_SIG_CHANNELS * 2 * 1024)
 
 typedef struct MI355FusedArgs {
     int op, dtype;

@@ -150,6 +150,7 @@ struct PatchParams {
     void *dst;
     const void *peer;
     const void *own;
+    const unsigned long long *nan_flag;   // the other member's NaN word, or nullptr (patch)
     uint64_t nvec;   // whole 16-byte vectors
     uint64_t n;      // elements
     Signal sig;
@@ -166,6 +167,11 @@ template <typename R>
 __global__ __launch_bounds__(kBlock) void nan_patch_copy(PatchParams p) {
     constexpr int V = 16 / sizeof(R);
     constexpr int U = 4;
+    // no NaN came out of the other member's fold: no result to patch, a copy
+    // (the word is wave-uniform: one load, then a uniform branch)
+    const bool patch = p.nan_flag == nullptr ||
+                       __hip_atomic_load(const_cast<unsigned long long *>(p.nan_flag), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_SYSTEM) != 0;
     const u32x4 *pe = (const u32x4 *)p.peer;
     const u32x4 *ow = (const u32x4 *)p.own;
     u32x4 *d = (u32x4 *)p.dst;
@@ -177,15 +183,17 @@ __global__ __launch_bounds__(kBlock) void nan_patch_copy(PatchParams p) {
             const uint64_t i = base + (uint64_t)u * kBlock;
             if (i < p.nvec) {
                 x[u].v = ld16<POL_PLAIN>(pe + i);
-                o[u].v = ld16<POL_PLAIN>(ow + i);
+                if (patch) o[u].v = ld16<POL_PLAIN>(ow + i);
             }
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const uint64_t i = base + (uint64_t)u * kBlock;
             if (i < p.nvec) {
+                if (patch) {
 #pragma unroll
-                for (int e = 0; e < V; ++e) x[u].e[e] = nan_keep_own(o[u].e[e], x[u].e[e]);
+                    for (int e = 0; e < V; ++e) x[u].e[e] = nan_keep_own(o[u].e[e], x[u].e[e]);
+                }
                 st16(d + i, x[u].v);
             }
         }
@@ -193,7 +201,8 @@ __global__ __launch_bounds__(kBlock) void nan_patch_copy(PatchParams p) {
     bool plain = false;
     for (uint64_t i = p.nvec * V + (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < p.n;
          i += (uint64_t)gridDim.x * kBlock) {
-        ((R *)p.dst)[i] = nan_keep_own(((const R *)p.own)[i], ((const R *)p.peer)[i]);
+        const R v = ((const R *)p.peer)[i];
+        ((R *)p.dst)[i] = patch ? nan_keep_own(((const R *)p.own)[i], v) : v;
         plain = true;
     }
     signal_done(p.sig, __syncthreads_or(plain));
@@ -245,6 +254,7 @@ static int combine_orders_impl(int op, int dtype, void *const *dsts, const void 
 extern "C" int mi355_combine(int op, int dtype, void *dst, const void *const *srcs, int nsrc,
                              size_t n, void *stream) {
     const int rc = combine_impl(op, dtype, dst, srcs, nsrc, n, stream);
+    t_nan_set = t_nan_clear = nullptr;  // a call that launched no fold consumes them too
     if (rc != 0) {
         t_sig = Signal{nullptr, nullptr, 0};
         t_ev_start = t_ev_stop = nullptr;
@@ -380,8 +390,13 @@ static int copy_segments_impl(void *const *dsts, const void *const *srcs, const 
     return launch(copy_segments<U, kMaxSeg>, dim3(gx, used), (hipStream_t)stream, p);
 }
 
+extern "C" void mi355_nan_flag_next_launch(unsigned long long *set, unsigned long long *clear) {
+    t_nan_set = set;
+    t_nan_clear = clear;
+}
+
 extern "C" int mi355_nan_patch_copy(int dtype, void *dst, const void *peer, const void *own, size_t n,
-                                    void *stream) {
+                                    const unsigned long long *nan_flag, void *stream) {
     const int rc = [&]() -> int {
         if (dtype != MI355_FLOAT && dtype != MI355_DOUBLE) return MI355_E_UNSUP;
         if (n == 0) {
@@ -393,7 +408,7 @@ extern "C" int mi355_nan_patch_copy(int dtype, void *dst, const void *peer, cons
         // 16-byte vectors when every pointer is aligned (the heap's shards
         // are), else element by element (a user offset into the arrays)
         const bool vec = (((uintptr_t)dst | (uintptr_t)peer | (uintptr_t)own) & 15) == 0;
-        PatchParams p{dst, peer, own, vec ? (uint64_t)(n * es / 16) : 0, (uint64_t)n, Signal{}};
+        PatchParams p{dst, peer, own, nan_flag, vec ? (uint64_t)(n * es / 16) : 0, (uint64_t)n, Signal{}};
         const unsigned grid = vec ? grid_for((uint64_t)kBlock * 4, p.nvec > 0 ? p.nvec : 1, 1)
                                   : grid_for((uint64_t)kBlock * 4, p.n, 1);
         return dtype == MI355_FLOAT ? launch(nan_patch_copy<float>, dim3(grid), (hipStream_t)stream, p)

@@ -68,8 +68,16 @@ struct CombineParams {
     uint64_t nvec;   // vector kernel: whole 16-byte vectors; scalar kernel: elements
     uint32_t tail;   // vector kernel: elements after nvec*V (< V)
     uint32_t head;   // vector kernel: elements just BEFORE dst/src (pointers advanced to 16-byte alignment)
+    unsigned long long *nan_set;    // mi355_nan_flag_next_launch: 1 here if a result is NaN
+    unsigned long long *nan_clear;  // ... and 0 here first
     Signal sig;
 };
+
+// The two-member schedule's NaN word (reduce.c nan_pair): written at system
+// scope, read by the other member's gather kernel over the peer mapping.
+__device__ __forceinline__ void nan_flag_store(unsigned long long *w, unsigned long long v) {
+    __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // Cache policy (tools/hbm_sweep.hip, MI355X, 256 MiB per buffer):
 //   stores: write-through to memory at agent scope, which makes the completion
@@ -104,6 +112,7 @@ __device__ __forceinline__ void st16_fold(u32x4 *p, u32x4 v) {
 template <int OP, typename T, int NSRC, int UNROLL, int POL>
 __global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
     constexpr int V = 16 / sizeof(T);
+    if (p.nan_clear != nullptr && blockIdx.x == 0 && threadIdx.x == 0) nan_flag_store(p.nan_clear, 0);
     const u32x4 *s[NSRC];
 #pragma unroll
     for (int k = 0; k < NSRC; ++k) s[k] = (const u32x4 *)p.src[k];
@@ -143,6 +152,7 @@ __global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
 #pragma unroll
                             for (int e = 0; e < V; ++e) acc.e[e] = apply<OP>(acc.e[e], x[u][k].e[e]);
                         }
+                        if (p.nan_set != nullptr) nan_flag_store(p.nan_set, 1);
                     }
                 }
                 st16_fold(d + i, acc.v);
@@ -156,6 +166,7 @@ __global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
 #pragma unroll
         for (int k = 1; k < NSRC; ++k) acc = apply<OP>(acc, ((const T *)p.src[k])[i]);
         ((T *)p.dst)[i] = acc;
+        if (p.nan_set != nullptr && redo_needed<OP>(acc)) nan_flag_store(p.nan_set, 1);
     }
     const bool head_block = V > 1 && p.head != 0 && blockIdx.x == 0;
     if (head_block && threadIdx.x < p.head) {
@@ -164,6 +175,7 @@ __global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
 #pragma unroll
         for (int k = 1; k < NSRC; ++k) acc = apply<OP>(acc, ((const T *)p.src[k])[i]);
         ((T *)p.dst)[i] = acc;
+        if (p.nan_set != nullptr && redo_needed<OP>(acc)) nan_flag_store(p.nan_set, 1);
     }
     signal_done(p.sig, tail_block || head_block);
 }
@@ -172,6 +184,7 @@ __global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
 // arrays). Coalesced element loads, grid-stride.
 template <int OP, typename T, int NSRC>
 __global__ __launch_bounds__(kBlock) void combine_scalar(CombineParams p) {
+    if (p.nan_clear != nullptr && blockIdx.x == 0 && threadIdx.x == 0) nan_flag_store(p.nan_clear, 0);
     const T *s[NSRC];
 #pragma unroll
     for (int k = 0; k < NSRC; ++k) s[k] = (const T *)p.src[k];
@@ -186,6 +199,7 @@ __global__ __launch_bounds__(kBlock) void combine_scalar(CombineParams p) {
 #pragma unroll
         for (int k = 1; k < NSRC; ++k) acc = apply<OP>(acc, v[k]);
         d[i] = acc;
+        if (p.nan_set != nullptr && redo_needed<OP>(acc)) nan_flag_store(p.nan_set, 1);
     }
     signal_done(p.sig, true);
 }
@@ -487,6 +501,8 @@ inline thread_local hipEvent_t t_ev_start = nullptr, t_ev_stop = nullptr;
 inline thread_local Signal t_sig = {nullptr, nullptr, 0};
 // host stub of the kernel this layer launched last (mi355_last_kernel)
 inline thread_local const void *t_last_kernel = nullptr;
+// NaN words for the next fold (mi355_nan_flag_next_launch), consumed by it
+inline thread_local unsigned long long *t_nan_set = nullptr, *t_nan_clear = nullptr;
 
 // A host-visible word the host can also write: an armed signal that no kernel
 // will carry (nothing to launch) is fired right here, in stream order.
@@ -650,6 +666,9 @@ long vector_head(const void *const *ptrs, int np, size_t n) {
 template <int OP, typename T, int NSRC>
 int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, bool final) {
     CombineParams p{};
+    p.nan_set = t_nan_set;
+    p.nan_clear = t_nan_clear;
+    t_nan_set = t_nan_clear = nullptr;
     const void *ptrs[kMaxSrc + 1];
     p.dst = dst;
     ptrs[0] = dst;

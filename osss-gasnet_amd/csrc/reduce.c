@@ -311,9 +311,25 @@ void shmemi_dev_barrier (int PE_start, int stride, int PE_size, int me, int last
  * reference order with the other members' versions going to this PE's
  * version area on channel `chan`. Returns the launch's status (0: queued, or
  * nothing to do: empty shard). */
-static int fold_shard (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n, const struct aset *s,
-                       int ordered, int pair, int chan, hipStream_t st)
+/* nan_pair: this call's number among the two-member calls with the other
+ * member on channel chan -- the same on both members (every member makes the
+ * same collective calls) -- whose parity picks the NaN word the owner's fold
+ * sets (MI355_SIG_NANFLAG_AT; it clears the other parity's, which the previous
+ * call's gather has finished reading) and the other member's gather reads. */
+static long long pair_next (int chan, const struct aset *s)
 {
+    if (shmemi.pair_calls == NULL) {
+        shmemi.pair_calls = (uint64_t *) calloc ((size_t) MI355_SIG_CHANNELS * (size_t) shmemi.npes, sizeof (uint64_t));
+        if (shmemi.pair_calls == NULL)
+            shmemi_fatal ("out of host memory");
+    }
+    return (long long) ++shmemi.pair_calls[(size_t) chan * (size_t) shmemi.npes + (size_t) aset_pe (s, 1 - s->me)];
+}
+
+static int fold_shard (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n, const struct aset *s,
+                       int ordered, long long pair_k, int chan, hipStream_t st)
+{
+    const int pair = pair_k >= 0;
     const void *sp[MI355_FUSED_MAX_MEMBERS > MI355_ORDERS_MAX_SOURCES ? MI355_FUSED_MAX_MEMBERS
                                                                        : MI355_ORDERS_MAX_SOURCES];
     size_t lo, hi;
@@ -335,6 +351,11 @@ static int fold_shard (int op, int dtype, size_t es, size_t dst_off, size_t src_
     }
     void *dst = shmemi_peer_ptr (shmemi.mype, dst_off + lo * es);
     int rc;
+    if (pair) {
+        const int other = aset_pe (s, 1 - s->me);
+        mi355_nan_flag_next_launch (shmemi.sigmem + MI355_SIG_NANFLAG_AT (chan, pair_k & 1, other),
+                                    shmemi.sigmem + MI355_SIG_NANFLAG_AT (chan, (pair_k + 1) & 1, other));
+    }
     if (!ordered) {
         rc = mi355_combine (op, dtype, dst, spp, s->size, hi - lo, st);
     } else {
@@ -378,14 +399,16 @@ static int gather_segments (size_t es, size_t dst_off, size_t n, const struct as
  * PE's own source is a NaN that NaN quieted instead. 0: queued, or nothing to
  * do (an empty shard: fires an armed signal). */
 static int pair_gather (int dtype, size_t es, size_t dst_off, size_t src_off, size_t n, const struct aset *s,
-                        hipStream_t st)
+                        long long pair_k, int chan, hipStream_t st)
 {
-    const int other = 1 - s->me;
+    const int other = 1 - s->me, other_pe = aset_pe (s, other);
     size_t l, h;
     mi355_shard_bounds (n, es, 2, other, &l, &h);
     return mi355_nan_patch_copy (dtype, shmemi_peer_ptr (shmemi.mype, dst_off + l * es),
-                                 shmemi_peer_ptr (aset_pe (s, other), dst_off + l * es),
-                                 shmemi_peer_ptr (shmemi.mype, src_off + l * es), h > l ? h - l : 0, st);
+                                 shmemi_peer_ptr (other_pe, dst_off + l * es),
+                                 shmemi_peer_ptr (shmemi.mype, src_off + l * es), h > l ? h - l : 0,
+                                 shmemi.peer_sig[other_pe] + MI355_SIG_NANFLAG_AT (chan, pair_k & 1, shmemi.mype),
+                                 st);
 }
 
 /* P2P shard schedule, dst and src disjoint or identical, with the three
@@ -402,10 +425,11 @@ static void p2p_range_dev (int op, int dtype, size_t es, size_t dst_off, size_t 
     const void *sp[MI355_FUSED_MAX_MEMBERS];
     size_t nb[MI355_FUSED_MAX_MEMBERS];
 
+    const long long pk = pair ? pair_next (SHMEMI_CHAN_HOST, s) : -1;
     device_barrier (&a, shmemi.stream); /* every source is ready */
     shmemi_peer_acquire (shmemi.stream);
     shmemi_timed_begin ();
-    int rc = fold_shard (op, dtype, es, dst_off, src_off, n, s, ordered, pair, SHMEMI_CHAN_HOST, shmemi.stream);
+    int rc = fold_shard (op, dtype, es, dst_off, src_off, n, s, ordered, pk, SHMEMI_CHAN_HOST, shmemi.stream);
     shmemi_timed_end ();
     if (rc != 0)
         shmemi_fatal ("combine kernel launch failed (op %d, dtype %d, %d sources, %zu elements): %d", op, dtype,
@@ -415,7 +439,7 @@ static void p2p_range_dev (int op, int dtype, size_t es, size_t dst_off, size_t 
     const int k = pair ? 0 : gather_segments (es, dst_off, n, s, ordered, SHMEMI_CHAN_HOST, dsts, sp, nb);
     if (pair) {
         shmemi_timed_begin_phase (1);
-        rc = pair_gather (dtype, es, dst_off, src_off, n, s, shmemi.stream);
+        rc = pair_gather (dtype, es, dst_off, src_off, n, s, pk, SHMEMI_CHAN_HOST, shmemi.stream);
         shmemi_timed_end ();
         if (rc != 0)
             shmemi_fatal ("gather kernel launch failed: %d", rc);
@@ -461,13 +485,14 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
     size_t lo, hi;
     mi355_shard_bounds (n, es, s->size, s->me, &lo, &hi);
 
+    const long long pk = pair ? pair_next (SHMEMI_CHAN_HOST, s) : -1;
     host_order ();
     shmemi_barrier_set (s->start, s->stride, s->size); /* every source is ready */
     if (hi > lo) {
         shmemi_peer_acquire (shmemi.stream);
         shmemi_timed_begin ();
         shmemi_arm_signal ();
-        int rc = fold_shard (op, dtype, es, dst_off, src_off, n, s, ordered, pair, SHMEMI_CHAN_HOST, shmemi.stream);
+        int rc = fold_shard (op, dtype, es, dst_off, src_off, n, s, ordered, pk, SHMEMI_CHAN_HOST, shmemi.stream);
         shmemi_timed_end ();
         if (rc != 0)
             shmemi_fatal ("combine kernel launch failed (op %d, dtype %d, %d sources, %zu elements): %d", op,
@@ -480,7 +505,7 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
     /* gather the other members' shards: one launch */
     if (pair) {
         shmemi_arm_signal ();
-        const int rc = pair_gather (dtype, es, dst_off, src_off, n, s, shmemi.stream);
+        const int rc = pair_gather (dtype, es, dst_off, src_off, n, s, pk, SHMEMI_CHAN_HOST, shmemi.stream);
         if (rc != 0)
             shmemi_fatal ("gather kernel launch failed: %d", rc);
         shmemi_wait_signal ();
@@ -1331,15 +1356,16 @@ static void reduce_on_stream (int op, int dtype, const char *fn, void *target, c
             for (size_t b = 0; b < n; b += round) {
                 const size_t cn = n - b < round ? n - b : round;
                 const size_t d0 = dst_off + b * es, s0 = src_off + b * es;
+                const long long pk = pair ? pair_next (SHMEMI_CHAN_STREAM, &s) : -1;
                 stream_barrier (fn, &s, st); /* every source is ready */
                 shmemi_peer_acquire (st);
-                const int rc = fold_shard (op, dtype, es, d0, s0, cn, &s, ord, pair, SHMEMI_CHAN_STREAM, st);
+                const int rc = fold_shard (op, dtype, es, d0, s0, cn, &s, ord, pk, SHMEMI_CHAN_STREAM, st);
                 if (rc != 0)
                     shmemi_fatal ("%s: combine kernel launch failed: %d", fn, rc);
                 stream_barrier (fn, &s, st); /* every shard is reduced */
                 shmemi_peer_acquire (st);
                 if (pair) {
-                    if (pair_gather (dtype, es, d0, s0, cn, &s, st) != 0)
+                    if (pair_gather (dtype, es, d0, s0, cn, &s, pk, SHMEMI_CHAN_STREAM, st) != 0)
                         shmemi_fatal ("%s: gather kernel launch failed", fn);
                 } else {
                     const int k = gather_segments (es, d0, cn, &s, ord, SHMEMI_CHAN_STREAM, dsts, sp, nb);

@@ -1408,6 +1408,8 @@ void pshmem_finalize (void)
         shmemi.blocks = n;
     }
     shmemi_hheap_finalize (); /* after the barrier above: no peer reads it any more */
+    free (shmemi.pair_calls);
+    shmemi.pair_calls = NULL;
     if (shmemi.heap != NULL)
         (void) hipFree (shmemi.heap);
     shmemi.heap = NULL;

@@ -147,6 +147,10 @@ struct shmemi_state {
     char **peer_hheap;          /* [npes]: every PE's segment, mapped here */
     struct shmemi_hostblk *host_blocks;
 
+    /* [channel * npes + PE]: two-member float/double P2P calls with each PE
+     * (reduce.c nan_pair: the parity picks the NaN word of the call) */
+    uint64_t *pair_calls;
+
     /* RCCL */
     void *rccl_comm;            /* ncclComm_t of the whole world, lazily */
 
