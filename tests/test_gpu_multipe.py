@@ -189,6 +189,39 @@ def test_nan_payload_fixtures_on_every_pe(tmp_path, fused_max, oneshot_max):
                          ctx=f"nan golden {c['op']}/{c['dtype']} case {c['golden']} PE {i}:")
 
 
+@pytest.mark.parametrize("fused_max", ["0", "2M"], ids=["multi-launch", "fused"])
+def test_two_member_calls_alternating_nan_and_finite(tmp_path, fused_max):
+    """The two-member float/double schedule (reduce.c nan_pair): the owner's
+    fold sets a per-call NaN word (parity of the call number with that
+    partner) and the other member patches its gather only when it is set. A
+    sequence on one pair alternating NaN-rich calls (golden_nan rows) and
+    NaN-free ones, in place and not, so each parity's word goes from set to
+    clear and back; every call bit-exact on both PEs."""
+    cases, cid = [], 0
+    for rep in range(2):
+        for op in ("sum", "prod"):
+            for dtype in ("double", "float"):
+                for mode in ("dev", "inplace"):
+                    cases.append({"id": cid, "op": op, "dtype": dtype, "n": NAN_ROWS[f"{op}_{dtype}"][0]["n"],
+                                  "sets": [[0, 0, 2]], "mode": mode, "algorithm": "p2p", "seed": 0, "golden": 0,
+                                  "family": "nan_"})
+                    cid += 1
+                    cases.append({"id": cid, "op": op, "dtype": dtype, "n": 70001 + cid, "sets": [[0, 0, 2]],
+                                  "mode": mode, "algorithm": "p2p", "seed": 900 + cid})
+                    cid += 1
+    results = run_pes(2, cases, tmp_path, extra_env={"SHMEM_FUSED_MAX_BYTES": fused_max})
+    for c in cases:
+        if "golden" in c:
+            g = np.load(os.path.join(HERE, "golden", f"golden_nan_{c['op']}_{c['dtype']}.npz"))
+            outs = g["out_0"]
+        else:
+            xs = [source(c["op"], c["dtype"], c["n"], c["seed"], pe) for pe in range(2)]
+            outs = [oracle.reduce_pe(c["op"], c["dtype"], xs, pe) for pe in range(2)]
+        for i in range(2):
+            assert_match(results[i][str(c["id"])], outs[i], c["op"], c["dtype"], strict=True,
+                         ctx=f"case {c['id']} {c['mode']} {c['op']}/{c['dtype']} PE {i}:")
+
+
 def test_pe_start_order_within_stated_fp_tolerance(tmp_path):
     """SHMEM_REDUCE_ORDER=pe_start gives every PE PE_start's result. For FP
     sum/prod on PE p != PE_start that differs from the reference's own result
