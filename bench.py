@@ -453,7 +453,7 @@ KERNEL_LEGS = [
     # long double (x87 arithmetic in software, x80.h): the sum is VALU-bound, the product HBM-bound
     ("rs_shard_n8_longdouble_sum", "combine_orders_vec<sum,x80,8>", "sum", "longdouble", 8, 32 << 20, True),
     ("rs_shard_n8_longdouble_prod", "combine_orders_vec<prod,x80,8>", "prod", "longdouble", 8, 32 << 20, True),
-    # float complex product (C99 Annex G multiply; one wave vote on its recovery case)
+    # float complex product (C99 Annex G multiply; a lane whose chain met a NaN redoes it exactly)
     ("rs_shard_n8_complexf_prod", "combine_orders_vec<prod,cplxf,8>", "prod", "complexf", 8, 32 << 20, True),
     # what each GPU folds in BASELINE config 4's longlong and at N = 8: 8 shards of 8 MiB (64 MiB / 8);
     # bitwise and is order-free, so the P2P schedule runs the plain fold, one output per shard
@@ -463,6 +463,15 @@ KERNEL_LEGS = [
 # own loop re-reads them) and cold (rotating disjoint buffer sets, >= 2 GiB of
 # footprint, so no byte is still in the 256 MiB Infinity Cache)
 COLD_FOOTPRINT = 2304 << 20
+# Layout of the kernel legs' buffers: consecutive buffers LEG_STAGGER bytes
+# further apart than their size. On the GPU the legs stand in for, a shard's
+# sources are 8 different GPUs' arrays and its outputs this PE's target shard
+# and version slots, which the library spaces by a shard + 256 + VER_STAGGER
+# (4096) bytes (csrc/reduce.c ver_slot_bytes): nothing lines the streams up on
+# the same HBM channels. Buffers exactly a power of two apart would
+# (tools/cold_probe orders_skew2); each leg also reports that layout
+# ("warm_aligned", separate hipMalloc'd buffers) for comparison.
+LEG_STAGGER = 4352
 # the long double legs' VALU floor: their per-element instruction streams in
 # this build priced at the measured issue rates -- computed by the library's
 # build (csrc/Makefile, tools/valu_floor.py --bench-legs) into lib/valu_floor.json;
@@ -503,13 +512,17 @@ def kernel_legs(shm, reps, check):
             raise RuntimeError("hipMalloc failed")
         return p.value
 
+    span = big + LEG_STAGGER
+    pool0 = dmalloc(2 * nbuf * span)
     for p in range(nbuf):
         x = np.random.default_rng(77 + p).random(big // 8) - 0.5
-        d = dmalloc(big)
+        d = pool0 + p * span
         shm.put(d, x)
         srcs.append(d)
         hosts.append(x)
-    outs = [dmalloc(big) for _ in range(nbuf)]
+    outs = [pool0 + (nbuf + p) * span for p in range(nbuf)]
+    al_srcs = [dmalloc(big) for _ in range(nbuf)]   # the power-of-two-aligned layout, for comparison
+    al_outs = [dmalloc(big) for _ in range(nbuf)]
     ev = [vp() for _ in range(2 * reps)]
     for e in ev:
         L.hipEventCreate(ctypes.byref(e))
@@ -534,28 +547,39 @@ def kernel_legs(shm, reps, check):
             for p in range(k):
                 shm.put(srcs[p], lds[p])
 
-        def launch():
+        def launch(so=srcs, oo=outs):
             if orders:
-                return shm.combine_orders(op, dtype, outs[:k], srcs[:k], n)
-            return shm.combine(op, dtype, outs[0], srcs[:k], n)
+                return shm.combine_orders(op, dtype, oo[:k], so[:k], n)
+            return shm.combine(op, dtype, oo[0], so[:k], n)
 
-        for _ in range(3):
-            assert launch() == 0
-        shm.sync()
-        for r in range(reps):
-            L.mi355_time_next_launch(ev[2 * r], ev[2 * r + 1])
-            assert launch() == 0
-        shm.sync()
-        ts = []
-        for r in range(reps):
-            ms = ctypes.c_float()
-            L.hipEventElapsedTime(ctypes.byref(ms), ev[2 * r], ev[2 * r + 1])
-            ts.append(ms.value * 1e-3)
+        def warm(so=srcs, oo=outs):
+            for _ in range(3):
+                assert launch(so, oo) == 0
+            shm.sync()
+            for r in range(reps):
+                L.mi355_time_next_launch(ev[2 * r], ev[2 * r + 1])
+                assert launch(so, oo) == 0
+            shm.sync()
+            ts = []
+            for r in range(reps):
+                ms = ctypes.c_float()
+                L.hipEventElapsedTime(ctypes.byref(ms), ev[2 * r], ev[2 * r + 1])
+                ts.append(ms.value * 1e-3)
+            return ts
+
+        ts = warm()
         t = float(np.mean(ts))
         alg = (k + nout) * nbytes
         gbs = alg / t / 1e9
+        # the same launches on power-of-two-aligned buffers (same source bytes)
+        for q in range(k):
+            if L.hipMemcpy(vp(al_srcs[q]), vp(srcs[q]), ctypes.c_size_t(nbytes), 3) != 0:
+                raise RuntimeError("hipMemcpy failed")
+        ta = float(np.mean(warm(al_srcs, al_outs)))
+        aligned = {"kernel_avg_us": round(ta * 1e6, 2), "frac": round(alg / ta / 1e9 / HBM_PEAK_GBS, 4)}
         # cold: `sets` disjoint copies of the leg's buffers taken in turn
-        set_bytes = (k + nout) * nbytes
+        span_l = nbytes + LEG_STAGGER
+        set_bytes = (k + nout) * span_l
         sets = max(1, -(-COLD_FOOTPRINT // set_bytes))
         cold_bufs = []
         if sets > 1:
@@ -564,15 +588,15 @@ def kernel_legs(shm, reps, check):
             for j in range(sets - 1):
                 base = pool + j * set_bytes
                 for q in range(k):   # the same source bytes as set 0
-                    if L.hipMemcpy(vp(base + q * nbytes), vp(srcs[q]), ctypes.c_size_t(nbytes), 3) != 0:
+                    if L.hipMemcpy(vp(base + q * span_l), vp(srcs[q]), ctypes.c_size_t(nbytes), 3) != 0:
                         raise RuntimeError("hipMemcpy failed")
 
         def launch_set(j):
             if j == 0:
                 return launch()
             base = cold_bufs[0] + (j - 1) * set_bytes
-            cs = [base + q * nbytes for q in range(k)]
-            co = [base + (k + q) * nbytes for q in range(nout)]
+            cs = [base + q * span_l for q in range(k)]
+            co = [base + (k + q) * span_l for q in range(nout)]
             if orders:
                 return shm.combine_orders(op, dtype, co, cs, n)
             return shm.combine(op, dtype, co[0], cs, n)
@@ -620,7 +644,7 @@ def kernel_legs(shm, reps, check):
                      "alg_bytes_per_launch": alg, "kernel_avg_us": round(t * 1e6, 2),
                      "kernel_median_us": round(float(np.median(ts)) * 1e6, 2), "launches": reps,
                      "achieved_GB_s": round(gbs, 1), "frac": round(gbs / HBM_PEAK_GBS, 4), "check": ck,
-                     "cold": cold}
+                     "cold": cold, "warm_aligned": aligned}
         if dtype == "longdouble":
             try:
                 fl = json.load(open(VALU_FLOOR))[name]
@@ -637,12 +661,15 @@ def kernel_legs(shm, reps, check):
                 res[name]["valu_floor_error"] = f"{type(e).__name__}: {e}"
     for e in ev:
         L.hipEventDestroy(e)
-    for d in srcs + outs:
+    for d in [pool0] + al_srcs + al_outs:
         L.hipFree(vp(d))
     res["note"] = ("fold kernels timed alone (HIP event pair per launch on its stream), algorithmic bytes = "
                    "(sources + outputs) x bytes; frac against the 8 TB/s HBM peak; warm = the same buffers every "
                    "launch (a set under ~256 MiB stays in the Infinity Cache), cold = disjoint copies taken in "
-                   "turn over >= 2 GiB: every byte from HBM")
+                   "turn over >= 2 GiB: every byte from HBM; buffers %d bytes further apart than their size (a "
+                   "shard's sources live on different GPUs, its outputs in version slots the library staggers); "
+                   "warm_aligned = the same launches on separately hipMalloc'd buffers, which line the streams up "
+                   "on the same HBM channels" % LEG_STAGGER)
     return res
 
 

@@ -216,11 +216,17 @@ static int nan_pair (int op, int dtype, const struct aset *s)
 /* Version areas: on every PE, one per signal-region channel, (size - 1)
  * slots of one shard each; slot s of owner i holds member q's version of
  * shard i, s = q < i ? q : q - 1. Each slot starts at the target's offset
- * within 256 bytes, so the gather copies run as aligned vectors. */
+ * within 256 bytes, so the gather copies run as aligned vectors.
+ * Consecutive slots are VER_STAGGER bytes further apart than a shard needs:
+ * the every-member fold writes all its outputs at the same element offset,
+ * and outputs a power-of-two shard size apart land in the same HBM channels
+ * (tools/cold_probe orders_skew2, 8 x 32 MiB double sum: 0.62 of peak from
+ * HBM with 256-byte gaps, 0.68-0.70 with 4 KiB-granular ones). */
+#define VER_STAGGER 4096
 static size_t ver_slot_bytes (size_t n, size_t es, int size)
 {
     const size_t b = shard_chunk (n, es, size) * es;
-    return (b + 255) / 256 * 256 + 256;
+    return (b + 255) / 256 * 256 + 256 + VER_STAGGER;
 }
 
 static size_t ver_off (int chan, int owner, int q, size_t slot_bytes, size_t dst_off)
@@ -235,10 +241,10 @@ static size_t ordered_round_elems (size_t es, int size)
 {
     const size_t align = es >= 256 ? 1 : 256 / es;
     const size_t per_slot = shmemi.order_chunk / (size_t) (size - 1);
-    if (per_slot < 512 + align * es)
+    if (per_slot < 512 + VER_STAGGER + align * es)
         shmemi_fatal ("SHMEM_DEVICE_ORDER_SIZE (%zu bytes per channel) is too small for %d PEs", shmemi.order_chunk,
                       size);
-    return (per_slot - 512) / es / align * align * (size_t) size;
+    return (per_slot - 512 - VER_STAGGER) / es / align * align * (size_t) size;
 }
 
 /* ---------------------------------------------------------------------- */

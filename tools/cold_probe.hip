@@ -195,6 +195,8 @@ static Stat timed_lib(const std::function<void(int)> &launch, int nsets, bool ro
 
 static char *g_pool;
 static size_t g_pool_bytes;
+static size_t g_skew;      // extra bytes between consecutive buffers (orders_skew)
+static int g_skew_from;    // ... from buffer index g_skew_from on
 
 static void emit(const char *kernel, const char *variant, size_t alg, int nsets, Stat w, Stat c) {
     printf("{\"kernel\": \"%s\", \"variant\": \"%s\", \"alg_bytes\": %zu, \"sets\": %d, \"footprint_MiB\": %zu, "
@@ -214,7 +216,9 @@ static int sets_for(size_t set_bytes) {
     return n;
 }
 static char *buf(int set, int k, int nbuf, size_t bytes) {
-    return g_pool + ((size_t)set * nbuf + k) * bytes;
+    const size_t j = (size_t)set * nbuf + k;
+    const size_t sk = k >= g_skew_from ? (size_t)(k - g_skew_from + 1) * g_skew : 0;
+    return g_pool + j * (bytes + (size_t)nbuf * g_skew) + sk;
 }
 
 template <typename K>
@@ -235,7 +239,7 @@ static void copy_variant(const char *name, K kern, int bpc, int u, size_t bytes,
     emit("copy", v, 2 * bytes, nsets, w, c);
 }
 
-static void lib_copy(size_t bytes) {
+static void lib_copy(size_t bytes, const char *name = "copy_segments<4,1>") {
     const int nsets = sets_for(2 * bytes);
     auto launch = [&](int s) {
         void *d[1] = {buf(s, 1, 2, bytes)};
@@ -245,7 +249,7 @@ static void lib_copy(size_t bytes) {
     };
     Stat w = timed_lib(launch, nsets, false, 30);
     Stat c = timed_lib(launch, nsets, true, 4 * nsets);
-    emit("copy_segments<4,1>", "library", 2 * bytes, nsets, w, c);
+    emit(name, "library", 2 * bytes, nsets, w, c);
 }
 
 static void lib_fold(const char *name, int op, int dtype, int k, size_t bytes) {
@@ -374,6 +378,77 @@ int main(int argc, char **argv) {
         orders_variant("ld=plain st=sc1", orders8<4, LD_PLAIN, ST_SC1>, 8, 4, B);
         orders_variant("ld=nt st=nt", orders8<4, LD_NT, ST_NT>, 8, 4, B);
         orders_variant("ld=nt st=plain", orders8<4, LD_NT, ST_PLAIN>, 8, 4, B);
+    }
+    if (what == "orders_skew") {   // round 5: do same-offset buffers (power-of-two stride) collide in DRAM?
+        for (size_t sk : {(size_t)0, (size_t)256, (size_t)4096, (size_t)65536 + 256, (size_t)MiB + 4096,
+                          (size_t)2 * MiB + 768}) {
+            g_skew = sk;
+            char nm[96];
+            snprintf(nm, sizeof nm, "combine_orders_vec<sum,double,8> skew=%zu", sk);
+            lib_orders(nm, MI355_OP_SUM, MI355_DOUBLE, 8, 32 * MiB);
+            snprintf(nm, sizeof nm, "copy_segments<4,1> skew=%zu", sk);
+            lib_copy(S, nm);
+        }
+        g_skew = 0;
+    }
+    if (what == "orders_skew2") {   // finer: which stride, and outputs only
+        for (int from : {0, 8})
+            for (size_t sk : {(size_t)1024, (size_t)2048, (size_t)4096, (size_t)8192, (size_t)12288, (size_t)16384,
+                              (size_t)32768, (size_t)4096 + 256, (size_t)3 * 4096 + 512}) {
+                g_skew = sk;
+                g_skew_from = from;
+                char nm[96];
+                snprintf(nm, sizeof nm, "combine_orders_vec<sum,double,8> skew=%zu from=%d", sk, from);
+                lib_orders(nm, MI355_OP_SUM, MI355_DOUBLE, 8, 32 * MiB);
+            }
+        for (size_t sk : {(size_t)0, (size_t)4096}) {
+            g_skew = sk;
+            g_skew_from = 0;
+            char nm[96];
+            snprintf(nm, sizeof nm, "combine_orders_vec<max,float,8> 8 MiB skew=%zu", sk);
+            lib_orders(nm, MI355_OP_MAX, MI355_FLOAT, 8, 8 * MiB);
+            snprintf(nm, sizeof nm, "combine_vec<sum,double,8> 32 MiB skew=%zu", sk);
+            lib_fold(nm, MI355_OP_SUM, MI355_DOUBLE, 8, 32 * MiB);
+            snprintf(nm, sizeof nm, "combine_vec<and,longlong,8> 8 MiB skew=%zu", sk);
+            lib_fold(nm, MI355_OP_AND, MI355_LONGLONG, 8, 8 * MiB);
+            snprintf(nm, sizeof nm, "combine_vec<sum,double,2> 256 MiB skew=%zu", sk);
+            lib_fold(nm, MI355_OP_SUM, MI355_DOUBLE, 2, S);
+        }
+        g_skew = 0;
+        g_skew_from = 0;
+    }
+    if (what == "segs") {   // round 5: the all-gather's shape (7 shards into one target at N = 8)
+        const size_t B = 32 * MiB;
+        for (int mode = 0; mode < 3; ++mode) {
+            // 0: one 224 MiB segment; 1: 7 x 32 MiB, target contiguous (the gather's layout), sources
+            // staggered 4352 B apart; 2: both sides staggered (what a decorrelated target would give)
+            const size_t stag = 4352;
+            const size_t set = 16 * (B + stag);
+            const int nsets = sets_for(set);
+            auto launch = [&](int st) {
+                char *base = g_pool + (size_t)st * set;
+                void *d[7];
+                const void *sr[7];
+                size_t nb[7];
+                if (mode == 0) {
+                    d[0] = base;
+                    sr[0] = base + 8 * (B + stag);
+                    nb[0] = 7 * B;
+                    if (mi355_copy_segments(d, sr, nb, 1, nullptr) != 0) exit(2);
+                    return;
+                }
+                for (int i = 0; i < 7; ++i) {
+                    d[i] = mode == 1 ? base + (size_t)(i + 1) * B : base + (size_t)(i + 1) * (B + stag);
+                    sr[i] = base + (size_t)(8 + i) * (B + stag);
+                    nb[i] = B;
+                }
+                if (mi355_copy_segments(d, sr, nb, 7, nullptr) != 0) exit(2);
+            };
+            Stat w = timed_lib(launch, nsets, false, 30);
+            Stat c = timed_lib(launch, nsets, true, std::max(40, 4 * nsets));
+            static const char *nm[3] = {"1 x 224 MiB", "7 x 32 MiB, target contiguous", "7 x 32 MiB, both staggered"};
+            emit("copy_segments", nm[mode], 14 * B, nsets, w, c);
+        }
     }
     CHECK(hipFree(g_pool));
     return 0;
