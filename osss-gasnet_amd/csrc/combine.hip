@@ -49,6 +49,21 @@ struct SegParams {
     Signal sig;
 };
 
+// Where a segment's vector part starts: `head` bytes peeled so the target is
+// 16-byte aligned (to a 128-byte line when source and target share their
+// offset within one), then the source's phase against it (0: both aligned;
+// otherwise copy_segments_shift).
+struct SegPlan {
+    uint64_t head;
+    unsigned delta;
+};
+__host__ __device__ inline SegPlan seg_plan(const void *dst, const void *src, uint64_t nb) {
+    const unsigned dmis128 = (unsigned)((uintptr_t)dst & 127);
+    uint64_t head = dmis128 == (unsigned)((uintptr_t)src & 127) ? (128u - dmis128) & 127u : (16u - (dmis128 & 15u)) & 15u;
+    if (head > nb) head = nb;
+    return {head, (unsigned)(((uintptr_t)src + head) & 15)};
+}
+
 template <int UNROLL, int NS>
 __global__ __launch_bounds__(kBlock) void copy_segments(SegParams<NS> p) {
     const int sg = blockIdx.y;
@@ -132,6 +147,61 @@ __global__ __launch_bounds__(kBlock) void copy_segments(SegParams<NS> p) {
             dst[i] = src[i];
             plain = true;
         }
+    }
+    signal_done(p.sig, __syncthreads_or(plain));
+}
+
+// A launch with a segment whose source is at another 16-byte phase than its
+// target (a byte offset into one of the buffers): the target peeled to 16
+// bytes, then copy_segments' pipelined loop with unaligned source loads
+// (combine_kernels.h ld16_src; 0.77 of peak against 0.24 in 8-byte words). Only such launches take this kernel, so
+// copy_segments' code stays as measured.
+template <int UNROLL, int NS>
+__global__ __launch_bounds__(kBlock) void copy_segments_shift(SegParams<NS> p) {
+    const int sg = blockIdx.y;
+    const uint64_t nb = p.nbytes[sg];
+    const char *src = (const char *)p.src[sg];
+    char *dst = (char *)p.dst[sg];
+    const uint64_t head = seg_plan(dst, src, nb).head;
+    const u32x4 *s = (const u32x4 *)(src + head);   // not 16-byte aligned: read with ld16_src<.., true>
+    u32x4 *d = (u32x4 *)(dst + head);
+    const uint64_t nvec = (nb - head) / 16;
+    // copy_segments' pipelined loop, two blocks per CU (cold_probe
+    // misaligned, 256 MiB: 87 us = 0.77 of peak; one vector per lane per pass:
+    // 119 us)
+    const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
+    uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
+    u32x4 x[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+        const uint64_t i = base + (uint64_t)u * kBlock;
+        if (i < nvec) x[u] = ld16_src<POL_PLAIN, true>(s, i);
+    }
+    while (base < nvec) {
+        const uint64_t next = base + step;
+        u32x4 y[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = next + (uint64_t)u * kBlock;
+            if (i < nvec) y[u] = ld16_src<POL_PLAIN, true>(s, i);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = base + (uint64_t)u * kBlock;
+            if (i < nvec) st16(d + i, x[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) x[u] = y[u];
+        base = next;
+    }
+    // the bytes outside the vector part: [0, head) and [head + 16 nvec, nb)
+    const uint64_t vec_end = head + nvec * 16;
+    const uint64_t nrest = head + (nb - vec_end);
+    bool plain = false;
+    for (uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x; r < nrest; r += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t i = r < head ? r : vec_end + (r - head);
+        dst[i] = src[i];
+        plain = true;
     }
     signal_done(p.sig, __syncthreads_or(plain));
 }
@@ -374,20 +444,25 @@ static int copy_segments_impl(void *const *dsts, const void *const *srcs, const 
     }
     // pipelined UNROLL 4, one block per CU (tools/copy_variants.hip,
     // profiles/r01/copy_variants.txt: 78.2-78.5 us for 256 MiB, the best of
-    // grid-stride / per-block partition / 1-4 blocks per CU / UNROLL 4-16)
+    // grid-stride / per-block partition / 1-4 blocks per CU / UNROLL 4-16);
+    // a segment whose source is at another phase than its target: the
+    // unaligned-load kernel, two blocks per CU
     constexpr int U = 4;
-    unsigned gx = grid_for((uint64_t)kBlock * U, maxv, 1);
+    bool shifted = false;
+    for (int k = 0; k < used; ++k) shifted = shifted || seg_plan(p.dst[k], p.src[k], p.nbytes[k]).delta != 0;
+    unsigned gx = grid_for((uint64_t)kBlock * U, maxv, shifted ? 2 : 1);
     // keep total blocks ~ cap when many segments share the chip
-    unsigned cap = (unsigned)device_cus();
+    unsigned cap = (unsigned)device_cus() * (shifted ? 2 : 1);
     if ((uint64_t)gx * used > cap) gx = cap / used > 0 ? cap / used : 1;
     if (used == 1) {
         SegParams<1> p1{};
         p1.dst[0] = p.dst[0];
         p1.src[0] = p.src[0];
         p1.nbytes[0] = p.nbytes[0];
-        return launch(copy_segments<U, 1>, dim3(gx, 1), (hipStream_t)stream, p1);
+        return launch(shifted ? copy_segments_shift<U, 1> : copy_segments<U, 1>, dim3(gx, 1), (hipStream_t)stream, p1);
     }
-    return launch(copy_segments<U, kMaxSeg>, dim3(gx, used), (hipStream_t)stream, p);
+    return launch(shifted ? copy_segments_shift<U, kMaxSeg> : copy_segments<U, kMaxSeg>, dim3(gx, used),
+                  (hipStream_t)stream, p);
 }
 
 extern "C" void mi355_nan_flag_next_launch(unsigned long long *set, unsigned long long *clear) {

@@ -106,18 +106,37 @@ __device__ __forceinline__ void st16_fold(u32x4 *p, u32x4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 
-// Vector path: every pointer 16-byte aligned. Each lane owns UNROLL vectors
-// spaced one block apart (so a wave touches contiguous 1 KiB per source per
-// step) and issues all NSRC*UNROLL loads before combining.
-template <int OP, typename T, int NSRC, int UNROLL, int POL>
-__global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
+// Sources at another 16-byte phase than the outputs (a user offset into one
+// of the arrays, e.g. target = &t[1], source = &s[0]): the outputs are still
+// written as aligned vectors and each source vector is read with one 16-byte
+// load from its unaligned address. gfx950 runs in unaligned access mode (the
+// loads stay global_load_dwordx4; the type below only tells the compiler the
+// alignment it may assume). Measured (tools/cold_probe unal / shift / dpp,
+// 256 MiB double sum of two sources, target aligned, sources 8 bytes off):
+// 0.84 of peak warm / 0.76 cold -- against 0.59 element-wise, 0.73 / 0.70
+// assembling each vector from two aligned loads (v_alignbyte), 0.77 / 0.71
+// with the neighbour's vector through a DPP wave shift, 0.42 through
+// ds_bpermute; the copy 0.86 / 0.72 against 0.24 in 8-byte words. Every byte
+// offset 1-15 reads the right bytes (cold_probe unal's check).
+typedef unsigned u32x4_any __attribute__((ext_vector_type(4), aligned(1)));
+template <int POL, bool SHIFT>
+__device__ __forceinline__ u32x4 ld16_src(const u32x4 *s, uint64_t i) {
+    if constexpr (!SHIFT) return ld16<POL>(s + i);
+    const u32x4_any *p = (const u32x4_any *)s + i;
+    if constexpr ((POL & POL_NT_LOAD) != 0) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+// The vector loop of combine_vec (SHIFT: sources at another phase than the
+// target, read unaligned).
+template <int OP, typename T, int NSRC, int UNROLL, int POL, bool SHIFT>
+__device__ __forceinline__ void fold_vectors(const CombineParams &p) {
     constexpr int V = 16 / sizeof(T);
-    if (p.nan_clear != nullptr && blockIdx.x == 0 && threadIdx.x == 0) nan_flag_store(p.nan_clear, 0);
+    const uint64_t nvec = p.nvec;
     const u32x4 *s[NSRC];
 #pragma unroll
     for (int k = 0; k < NSRC; ++k) s[k] = (const u32x4 *)p.src[k];
     u32x4 *d = (u32x4 *)p.dst;
-    const uint64_t nvec = p.nvec;
     const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
     for (uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x; base < nvec;
          base += step) {
@@ -127,9 +146,13 @@ __global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
             const uint64_t i = base + (uint64_t)u * kBlock;
             if (i < nvec) {
 #pragma unroll
-                for (int k = 0; k < NSRC; ++k) x[u][k].v = ld16<POL>(s[k] + i);
+                for (int k = 0; k < NSRC; ++k) x[u][k].v = ld16_src<POL, SHIFT>(s[k], i);
             }
         }
+        // every load issued before the first use: left alone, the scheduler
+        // placed a register copy of one load's data (and its wait) before
+        // the next load (float sum, two sources: 174 vs 125 us per 256 MiB)
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
             const uint64_t i = base + (uint64_t)u * kBlock;
@@ -159,6 +182,18 @@ __global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
             }
         }
     }
+}
+
+// Vector path: every output 16-byte aligned, the sources too or (SHIFT) all
+// at one other phase. Each lane owns UNROLL vectors
+// spaced one block apart (so a wave touches contiguous 1 KiB per source per
+// step) and issues all NSRC*UNROLL loads before combining.
+template <int OP, typename T, int NSRC, int UNROLL, int POL, bool SHIFT = false>
+__global__ __launch_bounds__(kBlock) void combine_vec(CombineParams p) {
+    constexpr int V = 16 / sizeof(T);
+    if (p.nan_clear != nullptr && blockIdx.x == 0 && threadIdx.x == 0) nan_flag_store(p.nan_clear, 0);
+    fold_vectors<OP, T, NSRC, UNROLL, POL, SHIFT>(p);
+    const uint64_t nvec = p.nvec;
     const bool tail_block = V > 1 && p.tail != 0 && blockIdx.x == 0;
     if (tail_block && threadIdx.x < p.tail) {
         const uint64_t i = nvec * V + threadIdx.x;
@@ -383,22 +418,15 @@ __device__ __forceinline__ Pack<T> member_chain(const Pack<T> (&x)[NSRC], int q)
     return acc;
 }
 
-template <int OP, typename T, int NSRC, int UNROLL, int POL, bool ALL>
-__global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
+// The vector loop of combine_orders_vec (SHIFT: as fold_vectors).
+template <int OP, typename T, int NSRC, int UNROLL, int POL, bool ALL, bool SHIFT>
+__device__ __forceinline__ void orders_vectors(const OrdersParams &p) {
     constexpr int V = 16 / sizeof(T);
     const uint64_t nvec = p.nvec;
     const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
-    if constexpr (std::is_same<T, x80>::value && (OP == MI355_OP_SUM || OP == MI355_OP_PROD)) {
-        const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-        uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-        for (; i < nvec; i += stride) {
-            x80 v[NSRC];
-            x80_load<NSRC>(p, i, v);
-            x80_orders_vector<OP, NSRC, ALL>(p, i, v);
-        }
-        signal_done(p.sig, false);
-        return;
-    }
+    const u32x4 *sb[NSRC];
+#pragma unroll
+    for (int k = 0; k < NSRC; ++k) sb[k] = (const u32x4 *)p.src[k];
     for (uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x; base < nvec;
          base += step) {
         Pack<T> x[UNROLL][NSRC];
@@ -407,9 +435,10 @@ __global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
             const uint64_t i = base + (uint64_t)u * kBlock;
             if (i < nvec) {
 #pragma unroll
-                for (int k = 0; k < NSRC; ++k) x[u][k].v = ld16<POL>((const u32x4 *)p.src[k] + i);
+                for (int k = 0; k < NSRC; ++k) x[u][k].v = ld16_src<POL, SHIFT>(sb[k], i);
             }
         }
+        __builtin_amdgcn_sched_barrier(0);   // loads first (fold_vectors)
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
             const uint64_t i = base + (uint64_t)u * kBlock;
@@ -476,6 +505,26 @@ __global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
             }
         }
     }
+}
+
+template <int OP, typename T, int NSRC, int UNROLL, int POL, bool ALL, bool SHIFT = false>
+__global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
+    constexpr int V = 16 / sizeof(T);
+    const uint64_t nvec = p.nvec;
+    const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
+    static_assert(!SHIFT || !std::is_same<T, x80>::value, "long double runs aligned or element-wise");
+    if constexpr (std::is_same<T, x80>::value && (OP == MI355_OP_SUM || OP == MI355_OP_PROD)) {
+        const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+        uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+        for (; i < nvec; i += stride) {
+            x80 v[NSRC];
+            x80_load<NSRC>(p, i, v);
+            x80_orders_vector<OP, NSRC, ALL>(p, i, v);
+        }
+        signal_done(p.sig, false);
+        return;
+    }
+    orders_vectors<OP, T, NSRC, UNROLL, POL, ALL, SHIFT>(p);
     const bool tail_block = V > 1 && p.tail != 0 && blockIdx.x == 0;
     if (tail_block && threadIdx.x < p.tail) orders_element<OP, T, NSRC>(p, (int64_t)(nvec * V + threadIdx.x));
     const bool head_block = V > 1 && p.head != 0 && blockIdx.x == 0;
@@ -663,6 +712,29 @@ long vector_head(const void *const *ptrs, int np, size_t n) {
     return same && n > head ? (long)head : -1;
 }
 
+// Outputs 16-byte aligned after peeling whole elements and every source at
+// one other phase: the vector kernels with unaligned source loads (SHIFT).
+// Returns the elements to peel, or -1 (sources at mixed phases, an output
+// not element-aligned, no whole vector, long double). The aligned launch
+// shapes (cold_probe unal: the same rates at 2 or 4 blocks per CU).
+template <typename T>
+long shift_head(const void *const *outs, int nout, const void *const *srcs, int nsrc, size_t n) {
+    if constexpr (std::is_same<T, x80>::value) {
+        return -1;
+    } else {
+        constexpr size_t es = sizeof(T);
+        constexpr size_t V = 16 / es;
+        const uintptr_t pd = (uintptr_t)outs[0] & 15, ps = (uintptr_t)srcs[0] & 15;
+        for (int k = 1; k < nout; ++k)
+            if (((uintptr_t)outs[k] & 15) != pd) return -1;
+        for (int k = 1; k < nsrc; ++k)
+            if (((uintptr_t)srcs[k] & 15) != ps) return -1;
+        if (pd % es != 0) return -1;
+        const size_t head = ((16 - pd) & 15) / es;
+        if (((ps + head * es) & 15) == 0 || n < head + V) return -1;
+        return (long)head;
+    }
+}
 template <int OP, typename T, int NSRC>
 int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, bool final) {
     CombineParams p{};
@@ -691,6 +763,21 @@ int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, b
                             : resident_blocks((const void *)k);
         const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, bpc);
         return launch(k, dim3(grid), st, p, final);
+    }
+    const long sh = shift_head<T>(&ptrs[0], 1, &ptrs[1], NSRC, n);
+    if constexpr (!std::is_same<T, x80>::value) {
+        if (sh >= 0) {
+            p.head = (uint32_t)sh;
+            p.dst = (char *)dst + sh * sizeof(T);
+            for (int k = 0; k < NSRC; ++k) p.src[k] = (const char *)srcs[k] + sh * sizeof(T);
+            n -= (size_t)sh;
+            using S = Shape<NSRC, T>;
+            p.nvec = n / V;
+            p.tail = (uint32_t)(n % V);
+            auto k = combine_vec<OP, T, NSRC, S::unroll, S::policy, true>;
+            const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, S::blocks_per_cu);
+            return launch(k, dim3(grid), st, p, final);
+        }
     }
     p.nvec = n;
     p.tail = 0;
@@ -739,6 +826,29 @@ int launch_orders_fixed(void *const *dsts, const void *const *srcs, size_t n, hi
             bpc = 1 << 20;
         const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, bpc);
         return launch(k, dim3(grid), st, p);
+    }
+    const void *outs[kMaxSrc];
+    int nout = 0;
+    for (int k = 0; k < NSRC; ++k)
+        if (dsts[k] != nullptr) outs[nout++] = dsts[k];
+    const long sh = nout > 0 ? shift_head<T>(outs, nout, srcs, NSRC, n) : -1;
+    if constexpr (!std::is_same<T, x80>::value) {
+        if (sh >= 0) {
+            p.head = (uint32_t)sh;
+            for (int k = 0; k < NSRC; ++k) {
+                p.src[k] = (const char *)srcs[k] + sh * sizeof(T);
+                if (dsts[k] != nullptr) p.dst[k] = (char *)dsts[k] + sh * sizeof(T);
+            }
+            n -= (size_t)sh;
+            using S = OrdersShape<OP, NSRC, T>;
+            p.nvec = n / V;
+            p.tail = (uint32_t)(n % V);
+            const bool all = nout == NSRC;
+            auto k = all ? combine_orders_vec<OP, T, NSRC, S::unroll, S::policy, true, true>
+                         : combine_orders_vec<OP, T, NSRC, S::unroll, S::policy, false, true>;
+            const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, S::blocks_per_cu);
+            return launch(k, dim3(grid), st, p);
+        }
     }
     p.nvec = n;
     p.tail = 0;

@@ -137,7 +137,7 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
     assert all("P2P shards, device barriers, each member's reference order (own-order fold, NaN-patched gather)"
                in ln for ln in lines), lines[:3]
     r = d["roofline"]
-    assert re.fullmatch(r"void mi355k::combine_vec<0, double, 2, \d, \d>\(mi355k::CombineParams\)", r["kernel"]), r
+    assert re.fullmatch(r"void mi355k::combine_vec<0, double, 2, \d, \d, false>\(mi355k::CombineParams\)", r["kernel"]), r
     shard = S // 2
     assert r["call"]["schedule"] == "p2p" and r["call"]["sources"] == 2 and r["call"]["outputs"] == 1, r
     assert r["xgmi_view"]["alg_bytes_per_launch"] == shard and r["alg_bytes_per_launch"] == 3 * shard, r

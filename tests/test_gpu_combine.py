@@ -457,8 +457,10 @@ def test_copy_segments_sizes_offsets_and_many_segments(shm, dev):
     sizes = [1, 15, 16, 17, 255, 4096, 8000, 16383, 16384, 16400, 65536 + 48, 1 << 20, (1 << 22) + 16]
     for nb in sizes:
         # (target offset, source offset): aligned, equally misaligned (head
-        # peeled, then vectors), differently misaligned (byte copy)
-        for doff, soff in ((0, 0), (16, 16), (3, 3), (8, 8), (3, 5)):
+        # peeled, then vectors), differently misaligned (shifted loads:
+        # funnel16, every source phase 1-15 against an aligned target)
+        for doff, soff in ((0, 0), (16, 16), (3, 3), (8, 8), (3, 5), (0, 8), (8, 0), (0, 4), (4, 12), (0, 1),
+                           (1, 0), (15, 2), (7, 0), (0, 15), (5, 30)):
             x = rng.integers(0, 256, nb + soff, dtype=np.uint8)
             s = dev.upload(x)
             d = dev.empty(nb + doff)
@@ -470,8 +472,9 @@ def test_copy_segments_sizes_offsets_and_many_segments(shm, dev):
             got = shm.get(d + doff, nb, np.uint8)
             assert (got == x[soff:]).all(), (nb, doff, soff, int(np.argmax(got != x[soff:])))
     for k, seg in ((7, 33333), (64, 4112)):
+        # segments at mixed phases: aligned, shifted by 8, by 3
         xs = [rng.integers(0, 256, seg, dtype=np.uint8) for _ in range(k)]
-        sp = [dev.upload(x) for x in xs]
+        sp = [_upload_at(dev, x, (0, 8, 3)[i % 3]) for i, x in enumerate(xs)]
         dp = [dev.empty(seg) for _ in range(k)]
         dsts = (ctypes.c_void_p * k)(*dp)
         srcs = (ctypes.c_void_p * k)(*sp)
@@ -482,19 +485,83 @@ def test_copy_segments_sizes_offsets_and_many_segments(shm, dev):
             assert (shm.get(dp[i], seg, np.uint8) == xs[i]).all(), (k, i)
 
 
+def _upload_at(dev, arr, off):
+    """arr on the device at byte offset `off` from a fresh (256-byte aligned) buffer."""
+    return dev.upload(np.concatenate([np.zeros(off, np.uint8), np.ascontiguousarray(arr).view(np.uint8)])) + off
+
+
 def test_combine_target_and_sources_misaligned_differently(shm, dev):
-    """Target one element off, sources three off: no common alignment, so the
-    element-wise kernel runs; results as the oracle's."""
-    import ctypes
+    """Target one element off, sources three off: the sources share a phase
+    the target lacks, so the fold runs as vectors with shifted loads
+    (funnel16); sources at different phases from each other run element-wise.
+    Results as the oracle's."""
     import gen_golden
     n, es = 3001, 8
     rng = np.random.default_rng(77)
     srcs = [gen_golden.values(rng, "sum", "double", n) for _ in range(3)]
-    ptrs = [dev.upload(np.concatenate([np.zeros(3), s])) + 3 * es for s in srcs]
-    out = dev.empty((n + 1) * es) + es
-    assert shm.combine("sum", "double", out, ptrs, n) == 0
-    shm.sync()
-    assert_match(shm.get(out, n, "double"), oracle.reduce_pe("sum", "double", srcs, 0), "sum", "double")
+    for soffs in ((3 * es,) * 3, (3 * es, 0, 3 * es)):
+        ptrs = [_upload_at(dev, s, o) for s, o in zip(srcs, soffs)]
+        out = dev.empty((n + 1) * es) + es
+        assert shm.combine("sum", "double", out, ptrs, n) == 0
+        shm.sync()
+        assert_match(shm.get(out, n, "double"), oracle.reduce_pe("sum", "double", srcs, 0), "sum", "double",
+                     ctx=str(soffs))
+
+
+# (target byte offset, source byte offset) pairs whose 16-byte phases differ:
+# the shifted-load vector kernels (combine_kernels.h shift_head / funnel16)
+SHIFT_PAIRS = {2: [(0, 2), (2, 0), (0, 6), (6, 14), (10, 4)], 4: [(0, 4), (4, 0), (0, 8), (12, 4), (8, 12)],
+               8: [(0, 8), (8, 0), (24, 16)], 16: [(0, 8)]}
+SHIFT_TYPES = [("sum", "short"), ("xor", "int"), ("prod", "int"), ("and", "long"), ("sum", "longlong"),
+               ("sum", "float"), ("max", "float"), ("prod", "float"), ("sum", "double"), ("min", "double"),
+               ("prod", "double"), ("sum", "complexf"), ("prod", "complexf"), ("sum", "complexd"),
+               ("prod", "complexd")]
+
+
+@pytest.mark.parametrize("op,dtype", SHIFT_TYPES)
+@pytest.mark.parametrize("nsrc", [1, 2, 3, 8])
+def test_combine_shifted_sources(shm, dev, op, dtype, nsrc):
+    """Target and sources at different 16-byte phases (every source at the
+    same one): every value as the oracle's, NaN payloads included, for sizes
+    around the vector boundaries (head peeled off the target, element tail)."""
+    import gen_golden
+    es = np.dtype(oracle.NP[dtype]).itemsize
+    rng = np.random.default_rng(400 + nsrc)
+    for doff, soff in SHIFT_PAIRS[es]:
+        for n in (1, 7, 1000, 65537):
+            srcs = [gen_golden.values(rng, op, dtype, n) for _ in range(nsrc)]
+            ptrs = [_upload_at(dev, x, soff) for x in srcs]
+            out = dev.empty(n * es + 32) + doff
+            assert shm.combine(op, dtype, out, ptrs, n) == 0
+            shm.sync()
+            assert_match(shm.get(out, n, dtype), oracle.reduce_pe(op, dtype, srcs, 0), op, dtype,
+                         ctx=f"target +{doff}, sources +{soff}, n={n}")
+            dev.free()
+
+
+@pytest.mark.parametrize("op,dtype", SHIFT_TYPES)
+@pytest.mark.parametrize("nsrc", [2, 3, 8])
+def test_combine_orders_shifted_sources(shm, dev, op, dtype, nsrc):
+    """The every-member fold with its outputs at another 16-byte phase than
+    its sources (the P2P schedule with target = &t[1], source = &s[0]): every
+    member's reference result, one output skipped, one in place (same phase as
+    the sources: element-wise)."""
+    import gen_golden
+    es = np.dtype(oracle.NP[dtype]).itemsize
+    rng = np.random.default_rng(500 + nsrc)
+    for doff, soff in SHIFT_PAIRS[es]:
+        for n, skip in ((7, ()), (4097, (1,)), (65537, ())):
+            srcs = [gen_golden.values(rng, op, dtype, n) for _ in range(nsrc)]
+            sp = [_upload_at(dev, x, soff) for x in srcs]
+            dp = [None if q in skip else dev.empty(n * es + 32) + doff for q in range(nsrc)]
+            assert shm.combine_orders(op, dtype, dp, sp, n) == 0
+            shm.sync()
+            for q in range(nsrc):
+                if dp[q] is None:
+                    continue
+                assert_match(shm.get(dp[q], n, dtype), oracle.reduce_pe(op, dtype, srcs, q), op, dtype,
+                             ctx=f"member {q}, target +{doff}, sources +{soff}, n={n}")
+            dev.free()
 
 
 # ---------------------------------------------------------------------------

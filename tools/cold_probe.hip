@@ -143,6 +143,164 @@ __global__ __launch_bounds__(256) void orders8(const u32x4 *s0, const u32x4 *s1,
     }
 }
 
+
+// ---- realigning copy / fold prototypes (target 16-byte aligned, sources at
+// another phase delta): output vector i = bytes [delta, delta + 16) of the
+// source's aligned vectors A_i : A_(i+1). MODE 0: each lane loads both;
+// MODE 1: A_(i+1) from the next lane (__shfl_down), lane 63 loads its own.
+__device__ __forceinline__ u32x4 funnel(u32x4 a, u32x4 b, unsigned q, unsigned r) {
+    unsigned w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    u32x4 o;
+    // q uniform: selects, no register-array indexing
+    unsigned lo0 = q == 0 ? w[0] : q == 1 ? w[1] : q == 2 ? w[2] : w[3];
+    unsigned lo1 = q == 0 ? w[1] : q == 1 ? w[2] : q == 2 ? w[3] : w[4];
+    unsigned lo2 = q == 0 ? w[2] : q == 1 ? w[3] : q == 2 ? w[4] : w[5];
+    unsigned lo3 = q == 0 ? w[3] : q == 1 ? w[4] : q == 2 ? w[5] : w[6];
+    unsigned lo4 = q == 0 ? w[4] : q == 1 ? w[5] : q == 2 ? w[6] : w[7];
+    o.x = __builtin_amdgcn_alignbyte(lo1, lo0, r);
+    o.y = __builtin_amdgcn_alignbyte(lo2, lo1, r);
+    o.z = __builtin_amdgcn_alignbyte(lo3, lo2, r);
+    o.w = __builtin_amdgcn_alignbyte(lo4, lo3, r);
+    return o;
+}
+__device__ __forceinline__ u32x4 shfl_next(u32x4 v) {
+    u32x4 o;
+    o.x = __shfl_down((int)v.x, 1);
+    o.y = __shfl_down((int)v.y, 1);
+    o.z = __shfl_down((int)v.z, 1);
+    o.w = __shfl_down((int)v.w, 1);
+    return o;
+}
+// A_(i+1) from the next lane with a DPP wave shift (wave_shl:1: lane l reads
+// lane l + 1; lane 63 keeps `old`, here its own load of A_(i+1))
+__device__ __forceinline__ u32x4 dpp_next(u32x4 v, u32x4 old) {
+    u32x4 o;
+    o.x = (unsigned)__builtin_amdgcn_update_dpp((int)old.x, (int)v.x, 0x130, 0xF, 0xF, false);
+    o.y = (unsigned)__builtin_amdgcn_update_dpp((int)old.y, (int)v.y, 0x130, 0xF, 0xF, false);
+    o.z = (unsigned)__builtin_amdgcn_update_dpp((int)old.z, (int)v.z, 0x130, 0xF, 0xF, false);
+    o.w = (unsigned)__builtin_amdgcn_update_dpp((int)old.w, (int)v.w, 0x130, 0xF, 0xF, false);
+    return o;
+}
+template <int LD>
+__global__ __launch_bounds__(256) void fold2_dpp(const u32x4 *sa0, const u32x4 *sa1, u32x4 *d, uint64_t nvec,
+                                                 unsigned delta) {
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    const unsigned q = delta >> 2, r = delta & 3;
+    const bool last = (threadIdx.x & 63) == 63;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i - (threadIdx.x & 63) < nvec;
+         i += (uint64_t)gridDim.x * 256) {
+        const uint64_t ic = i < nvec ? i : nvec - 1;
+        u32x4 a0 = ld<LD>(sa0 + ic), a1 = ld<LD>(sa1 + ic), o0 = {0, 0, 0, 0}, o1 = {0, 0, 0, 0};
+        if (last) {
+            o0 = ld<LD>(sa0 + ic + 1);
+            o1 = ld<LD>(sa1 + ic + 1);
+        }
+        const u32x4 b0 = dpp_next(a0, o0), b1 = dpp_next(a1, o1);
+        if (i < nvec) {
+            f64x2 x = __builtin_bit_cast(f64x2, funnel(a0, b0, q, r)) + __builtin_bit_cast(f64x2, funnel(a1, b1, q, r));
+            st<ST_SC1>(d + i, __builtin_bit_cast(u32x4, x));
+        }
+    }
+}
+template <int LD>
+__global__ __launch_bounds__(256) void copy_dpp(const u32x4 *sa, u32x4 *d, uint64_t nvec, unsigned delta) {
+    const unsigned q = delta >> 2, r = delta & 3;
+    const bool last = (threadIdx.x & 63) == 63;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i - (threadIdx.x & 63) < nvec;
+         i += (uint64_t)gridDim.x * 256) {
+        const uint64_t ic = i < nvec ? i : nvec - 1;
+        u32x4 a = ld<LD>(sa + ic), o = {0, 0, 0, 0};
+        if (last) o = ld<LD>(sa + ic + 1);
+        const u32x4 b = dpp_next(a, o);
+        if (i < nvec) st<ST_NT_SC1>(d + i, funnel(a, b, q, r));
+    }
+}
+// misaligned dwordx4: loads straight from a 4-byte-aligned (not 16) address,
+// relying on the hardware's unaligned access mode
+__global__ __launch_bounds__(256) void fold2_unal(const char *s0, const char *s1, u32x4 *d, uint64_t nvec) {
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (uint64_t)gridDim.x * 256) {
+        const u32x4 a = __builtin_nontemporal_load((const u32x4 *)(s0 + 16 * i));
+        const u32x4 b = __builtin_nontemporal_load((const u32x4 *)(s1 + 16 * i));
+        f64x2 x = __builtin_bit_cast(f64x2, a) + __builtin_bit_cast(f64x2, b);
+        st<ST_SC1>(d + i, __builtin_bit_cast(u32x4, x));
+    }
+}
+__global__ __launch_bounds__(256) void copy_unal(const char *s, u32x4 *d, uint64_t nvec) {
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (uint64_t)gridDim.x * 256)
+        st<ST_NT_SC1>(d + i, *(const u32x4 *)(s + 16 * i));
+}
+// sa: the source's aligned base (source - delta); nvec output vectors; every
+// lane of a wave active for the shuffle (lanes past the end load a clamped index)
+template <int U, int MODE, int LD, int ST>
+__global__ __launch_bounds__(256) void copy_shift(const u32x4 *sa, u32x4 *d, uint64_t nvec, unsigned delta) {
+    const unsigned q = delta >> 2, r = delta & 3;
+    const uint64_t step = (uint64_t)gridDim.x * 256 * U;
+    const bool last = (threadIdx.x & 63) == 63;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 * U + threadIdx.x; base - (threadIdx.x & 63) < nvec; base += step) {
+        u32x4 a[U], b[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = base + (uint64_t)u * 256;
+            const uint64_t ic = i < nvec ? i : nvec - 1;
+            a[u] = ld<LD>(sa + ic);
+            if (MODE == 0) b[u] = ld<LD>(sa + ic + 1);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (MODE == 1) {
+                b[u] = shfl_next(a[u]);
+                const uint64_t i = base + (uint64_t)u * 256;
+                if (last && i < nvec) b[u] = ld<LD>(sa + i + 1);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = base + (uint64_t)u * 256;
+            if (i < nvec) st<ST>(d + i, funnel(a[u], b[u], q, r));
+        }
+    }
+}
+template <int MODE, int LDA = LD_NT, int LDB = LD_NT, int U = 1>
+__global__ __launch_bounds__(256) void fold2_shift(const u32x4 *sa0, const u32x4 *sa1, u32x4 *d, uint64_t nvec,
+                                                   unsigned delta) {
+    typedef double f64x2 __attribute__((ext_vector_type(2)));
+    const unsigned q = delta >> 2, r = delta & 3;
+    const bool last = (threadIdx.x & 63) == 63;
+    const uint64_t step = (uint64_t)gridDim.x * 256 * U;
+    for (uint64_t base = (uint64_t)blockIdx.x * 256 * U + threadIdx.x; base - (threadIdx.x & 63) < nvec; base += step) {
+        u32x4 a0[U], a1[U], b0[U], b1[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = base + (uint64_t)u * 256;
+            const uint64_t ic = i < nvec ? i : nvec - 1;
+            a0[u] = ld<LDA>(sa0 + ic);
+            a1[u] = ld<LDA>(sa1 + ic);
+            if (MODE == 0) {
+                b0[u] = ld<LDB>(sa0 + ic + 1);
+                b1[u] = ld<LDB>(sa1 + ic + 1);
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = base + (uint64_t)u * 256;
+            if (MODE == 1) {
+                b0[u] = shfl_next(a0[u]);
+                b1[u] = shfl_next(a1[u]);
+                if (last && i < nvec) {
+                    b0[u] = ld<LDB>(sa0 + i + 1);
+                    b1[u] = ld<LDB>(sa1 + i + 1);
+                }
+            }
+            if (i < nvec) {
+                f64x2 x = __builtin_bit_cast(f64x2, funnel(a0[u], b0[u], q, r)) +
+                          __builtin_bit_cast(f64x2, funnel(a1[u], b1[u], q, r));
+                st<ST_SC1>(d + i, __builtin_bit_cast(u32x4, x));
+            }
+        }
+    }
+}
+
 // ---- timing
 static hipEvent_t g_a, g_b;
 static int g_cus = 256;
@@ -197,6 +355,7 @@ static char *g_pool;
 static size_t g_pool_bytes;
 static size_t g_skew;      // extra bytes between consecutive buffers (orders_skew)
 static int g_skew_from;    // ... from buffer index g_skew_from on
+static size_t g_dst_mis;   // bytes added to every output pointer (misaligned-target probe)
 
 static void emit(const char *kernel, const char *variant, size_t alg, int nsets, Stat w, Stat c) {
     printf("{\"kernel\": \"%s\", \"variant\": \"%s\", \"alg_bytes\": %zu, \"sets\": %d, \"footprint_MiB\": %zu, "
@@ -242,9 +401,9 @@ static void copy_variant(const char *name, K kern, int bpc, int u, size_t bytes,
 static void lib_copy(size_t bytes, const char *name = "copy_segments<4,1>") {
     const int nsets = sets_for(2 * bytes);
     auto launch = [&](int s) {
-        void *d[1] = {buf(s, 1, 2, bytes)};
+        void *d[1] = {buf(s, 1, 2, bytes) + g_dst_mis};
         const void *sr[1] = {buf(s, 0, 2, bytes)};
-        size_t nb[1] = {bytes};
+        size_t nb[1] = {bytes - (g_dst_mis ? 16 : 0)};
         if (mi355_copy_segments(d, sr, nb, 1, nullptr) != 0) exit(2);
     };
     Stat w = timed_lib(launch, nsets, false, 30);
@@ -259,7 +418,7 @@ static void lib_fold(const char *name, int op, int dtype, int k, size_t bytes) {
     auto launch = [&](int s) {
         const void *sr[8];
         for (int j = 0; j < k; ++j) sr[j] = buf(s, j, nbuf, bytes);
-        if (mi355_combine(op, dtype, buf(s, k, nbuf, bytes), sr, k, n, nullptr) != 0) exit(2);
+        if (mi355_combine(op, dtype, buf(s, k, nbuf, bytes) + g_dst_mis, sr, k, n - (g_dst_mis ? 1 : 0), nullptr) != 0) exit(2);
     };
     Stat w = timed_lib(launch, nsets, false, 30);
     Stat c = timed_lib(launch, nsets, true, std::max(40, 2 * nsets));
@@ -277,9 +436,9 @@ static void lib_orders(const char *name, int op, int dtype, int k, size_t bytes)
         void *ds[8];
         for (int j = 0; j < k; ++j) {
             sr[j] = buf(s, j, nbuf, bytes);
-            ds[j] = buf(s, k + j, nbuf, bytes);
+            ds[j] = buf(s, k + j, nbuf, bytes) + g_dst_mis;
         }
-        if (mi355_combine_orders(op, dtype, ds, sr, k, n, nullptr) != 0) exit(2);
+        if (mi355_combine_orders(op, dtype, ds, sr, k, n - (g_dst_mis ? 1 : 0), nullptr) != 0) exit(2);
     };
     Stat w = timed_lib(launch, nsets, false, 30);
     Stat c = timed_lib(launch, nsets, true, std::max(40, 2 * nsets));
@@ -449,6 +608,163 @@ int main(int argc, char **argv) {
             static const char *nm[3] = {"1 x 224 MiB", "7 x 32 MiB, target contiguous", "7 x 32 MiB, both staggered"};
             emit("copy_segments", nm[mode], 14 * B, nsets, w, c);
         }
+    }
+    if (what == "misaligned") {   // target 8 bytes off the sources' 16-byte phase
+        g_skew = 4352;
+        for (size_t mis : {(size_t)0, (size_t)8, (size_t)4}) {
+            g_dst_mis = mis;
+            char nm[96];
+            snprintf(nm, sizeof nm, "copy_segments dst+%zu", mis);
+            lib_copy(S, nm);
+            snprintf(nm, sizeof nm, "combine_vec<sum,double,2> dst+%zu", mis);
+            if (mis % 8 == 0) lib_fold(nm, MI355_OP_SUM, MI355_DOUBLE, 2, S);
+            snprintf(nm, sizeof nm, "combine_vec<sum,float,2> dst+%zu", mis);
+            lib_fold(nm, MI355_OP_SUM, MI355_FLOAT, 2, S);
+            snprintf(nm, sizeof nm, "combine_orders_vec<sum,double,8> dst+%zu", mis);
+            if (mis % 8 == 0) lib_orders(nm, MI355_OP_SUM, MI355_DOUBLE, 8, 32 * MiB);
+        }
+        g_dst_mis = 0;
+        g_skew = 0;
+    }
+    if (what == "unal") {   // misaligned 16-byte loads: correct? fast?
+        const size_t B = S - 4096;
+        const uint64_t nvec = B / 16;
+        g_skew = 4352;
+        {
+            const char *a = buf(0, 0, 4, S), *b = buf(0, 1, 4, S);
+            u32x4 *o1 = (u32x4 *)buf(0, 2, 4, S), *o2 = (u32x4 *)buf(0, 3, 4, S);
+            const size_t cmpn = 4 * MiB;
+            std::vector<char> h1(cmpn), h2(cmpn);
+            int bad = 0;
+            for (unsigned dl : {8u, 4u, 12u, 1u, 2u, 3u, 6u, 15u}) {
+                hipLaunchKernelGGL((fold2_shift<0>), dim3(g_cus * 2), dim3(256), 0, 0, (const u32x4 *)a, (const u32x4 *)b, o1, nvec, dl);
+                hipLaunchKernelGGL(fold2_unal, dim3(g_cus * 2), dim3(256), 0, 0, a + dl, b + dl, o2, nvec);
+                CHECK(hipDeviceSynchronize());
+                for (size_t off : {(size_t)0, B - cmpn}) {
+                    CHECK(hipMemcpy(h1.data(), (char *)o1 + off, cmpn, hipMemcpyDeviceToHost));
+                    CHECK(hipMemcpy(h2.data(), (char *)o2 + off, cmpn, hipMemcpyDeviceToHost));
+                    if (memcmp(h1.data(), h2.data(), cmpn) != 0) { ++bad; printf("{\"fold_mismatch_delta\": %u, \"off\": %zu}\n", dl, off); }
+                }
+                hipLaunchKernelGGL(copy_unal, dim3(g_cus * 2), dim3(256), 0, 0, a + dl, o2, nvec);
+                CHECK(hipDeviceSynchronize());
+                std::vector<char> hs(cmpn + 16);
+                CHECK(hipMemcpy(hs.data(), a, cmpn + 16, hipMemcpyDeviceToHost));
+                CHECK(hipMemcpy(h2.data(), (char *)o2, cmpn, hipMemcpyDeviceToHost));
+                if (memcmp(hs.data() + dl, h2.data(), cmpn) != 0) { ++bad; printf("{\"copy_mismatch_delta\": %u}\n", dl); }
+            }
+            printf("{\"unal_check_mismatches\": %d}\n", bad);
+            fflush(stdout);
+        }
+        for (int v = 0; v < 8; ++v) {
+            const int nbuf = v % 4 < 2 ? 2 : 3;
+            const int nsets = sets_for(nbuf * (S + g_skew));
+            const unsigned grid = (unsigned)g_cus * (v % 2 ? 4 : 2);
+            const size_t mis = v < 4 ? 8 : 3;
+            auto launch = [&](int st) {
+                const char *a = buf(st, 0, nbuf, S) + mis, *b = buf(st, 1, nbuf, S) + mis;
+                u32x4 *dd = (u32x4 *)buf(st, nbuf - 1, nbuf, S);
+                if (v % 4 < 2) hipLaunchKernelGGL(copy_unal, dim3(grid), dim3(256), 0, 0, a, dd, nvec);
+                else hipLaunchKernelGGL(fold2_unal, dim3(grid), dim3(256), 0, 0, a, b, dd, nvec);
+            };
+            Stat w = timed(launch, nsets, false, 30);
+            Stat c = timed(launch, nsets, true, std::max(40, 4 * nsets));
+            static const char *nm[8] = {"copy unal+8 bpc=2", "copy unal+8 bpc=4", "fold2 unal+8 bpc=2", "fold2 unal+8 bpc=4",
+                                        "copy unal+3 bpc=2", "copy unal+3 bpc=4", "fold2 unal+3 bpc=2", "fold2 unal+3 bpc=4"};
+            emit("shift", nm[v], (size_t)nbuf * B, nsets, w, c);
+        }
+        g_skew = 0;
+    }
+    if (what == "dpp") {   // DPP neighbour exchange: correctness against the two-load form, then rates
+        const size_t B = S - 4096;
+        const uint64_t nvec = B / 16;
+        g_skew = 4352;
+        {   // correctness: 3 buffers of set 0 (a, b, out) + a reference out
+            const u32x4 *a = (const u32x4 *)buf(0, 0, 4, S), *b = (const u32x4 *)buf(0, 1, 4, S);
+            u32x4 *o1 = (u32x4 *)buf(0, 2, 4, S), *o2 = (u32x4 *)buf(0, 3, 4, S);
+            const size_t cmpn = 4 * MiB;
+            std::vector<char> h1(cmpn), h2(cmpn);
+            int bad = 0;
+            for (unsigned dl : {4u, 8u, 12u, 2u, 6u, 1u, 15u}) {
+                hipLaunchKernelGGL((fold2_shift<0>), dim3(g_cus * 2), dim3(256), 0, 0, a, b, o1, nvec, dl);
+                hipLaunchKernelGGL((fold2_dpp<LD_NT>), dim3(g_cus * 2), dim3(256), 0, 0, a, b, o2, nvec, dl);
+                CHECK(hipDeviceSynchronize());
+                for (size_t off : {(size_t)0, B - cmpn}) {
+                    CHECK(hipMemcpy(h1.data(), (char *)o1 + off, cmpn, hipMemcpyDeviceToHost));
+                    CHECK(hipMemcpy(h2.data(), (char *)o2 + off, cmpn, hipMemcpyDeviceToHost));
+                    bad += memcmp(h1.data(), h2.data(), cmpn) != 0;
+                }
+                hipLaunchKernelGGL((copy_shift<4, 0, LD_PLAIN, ST_NT_SC1>), dim3(g_cus * 2), dim3(256), 0, 0, a, o1, nvec, dl);
+                hipLaunchKernelGGL((copy_dpp<LD_PLAIN>), dim3(g_cus * 2), dim3(256), 0, 0, a, o2, nvec, dl);
+                CHECK(hipDeviceSynchronize());
+                for (size_t off : {(size_t)0, B - cmpn}) {
+                    CHECK(hipMemcpy(h1.data(), (char *)o1 + off, cmpn, hipMemcpyDeviceToHost));
+                    CHECK(hipMemcpy(h2.data(), (char *)o2 + off, cmpn, hipMemcpyDeviceToHost));
+                    bad += memcmp(h1.data(), h2.data(), cmpn) != 0;
+                }
+                // the copy against the host: out[j] = src bytes [dl + 16 j, ...)
+                std::vector<char> hs(cmpn + 16);
+                CHECK(hipMemcpy(hs.data(), (const char *)a, cmpn + 16, hipMemcpyDeviceToHost));
+                CHECK(hipMemcpy(h2.data(), (char *)o2, cmpn, hipMemcpyDeviceToHost));
+                bad += memcmp(hs.data() + dl, h2.data(), cmpn) != 0;
+            }
+            printf("{\"dpp_check_mismatches\": %d}\n", bad);
+            if (bad) return 3;
+        }
+        for (int v = 0; v < 4; ++v) {
+            const int nbuf = v < 2 ? 2 : 3;
+            const int nsets = sets_for(nbuf * (S + g_skew));
+            const unsigned grid = (unsigned)g_cus * 2;
+            auto launch = [&](int st) {
+                const u32x4 *a = (const u32x4 *)buf(st, 0, nbuf, S);
+                u32x4 *dd = (u32x4 *)buf(st, nbuf - 1, nbuf, S);
+                const u32x4 *b = (const u32x4 *)buf(st, 1, nbuf, S);
+                if (v == 0) hipLaunchKernelGGL(copy_dpp<LD_PLAIN>, dim3(grid), dim3(256), 0, 0, a, dd, nvec, 8u);
+                if (v == 1) hipLaunchKernelGGL(copy_dpp<LD_NT>, dim3(grid), dim3(256), 0, 0, a, dd, nvec, 8u);
+                if (v == 2) hipLaunchKernelGGL(fold2_dpp<LD_NT>, dim3(grid), dim3(256), 0, 0, a, b, dd, nvec, 8u);
+                if (v == 3) hipLaunchKernelGGL(fold2_dpp<LD_PLAIN>, dim3(grid), dim3(256), 0, 0, a, b, dd, nvec, 8u);
+            };
+            Stat w = timed(launch, nsets, false, 30);
+            Stat c = timed(launch, nsets, true, std::max(40, 4 * nsets));
+            static const char *nm[4] = {"copy dpp plain bpc=2", "copy dpp nt bpc=2", "fold2 dpp nt bpc=2", "fold2 dpp plain bpc=2"};
+            emit("shift", nm[v], (size_t)nbuf * B, nsets, w, c);
+        }
+        g_skew = 0;
+    }
+    if (what == "shift") {   // realigning copy / k = 2 fold, target aligned, sources 8 bytes off
+        const size_t B = S - 4096;
+        const uint64_t nvec = B / 16;
+        g_skew = 4352;
+        for (int v = 0; v < 12; ++v) {
+            const int nbuf = v < 4 ? 2 : 3;
+            const int nsets = sets_for(nbuf * (S + g_skew));
+            const unsigned grid = v < 4 ? (unsigned)g_cus * (v % 2 ? 2 : 1) : v >= 10 ? (unsigned)g_cus * 4 : (unsigned)g_cus * 2;
+            auto launch = [&](int st) {
+                const u32x4 *a = (const u32x4 *)buf(st, 0, nbuf, S);
+                u32x4 *dd = (u32x4 *)buf(st, nbuf - 1, nbuf, S);
+                if (v == 0) hipLaunchKernelGGL((copy_shift<4, 0, LD_PLAIN, ST_NT_SC1>), dim3(grid), dim3(256), 0, 0, a, dd, nvec, 8u);
+                if (v == 1) hipLaunchKernelGGL((copy_shift<4, 0, LD_PLAIN, ST_NT_SC1>), dim3(grid), dim3(256), 0, 0, a, dd, nvec, 8u);
+                if (v == 2) hipLaunchKernelGGL((copy_shift<4, 1, LD_PLAIN, ST_NT_SC1>), dim3(grid), dim3(256), 0, 0, a, dd, nvec, 8u);
+                if (v == 3) hipLaunchKernelGGL((copy_shift<4, 1, LD_PLAIN, ST_NT_SC1>), dim3(grid), dim3(256), 0, 0, a, dd, nvec, 8u);
+                const u32x4 *b = (const u32x4 *)buf(st, 1, nbuf, S);
+                if (v == 4) hipLaunchKernelGGL(fold2_shift<0>, dim3(grid), dim3(256), 0, 0, a, b, dd, nvec, 8u);
+                if (v == 5) hipLaunchKernelGGL(fold2_shift<1>, dim3(grid), dim3(256), 0, 0, a, b, dd, nvec, 8u);
+                if (v == 6) hipLaunchKernelGGL((fold2_shift<0, LD_PLAIN, LD_PLAIN>), dim3(grid), dim3(256), 0, 0, a, b, dd, nvec, 8u);
+                if (v == 7) hipLaunchKernelGGL((fold2_shift<0, LD_NT, LD_PLAIN>), dim3(grid), dim3(256), 0, 0, a, b, dd, nvec, 8u);
+                if (v == 8) hipLaunchKernelGGL((fold2_shift<0, LD_PLAIN, LD_NT>), dim3(grid), dim3(256), 0, 0, a, b, dd, nvec, 8u);
+                if (v == 9) hipLaunchKernelGGL((fold2_shift<0, LD_NT, LD_NT, 2>), dim3(grid), dim3(256), 0, 0, a, b, dd, nvec, 8u);
+                if (v == 10) hipLaunchKernelGGL((fold2_shift<0, LD_NT, LD_NT>), dim3(grid), dim3(256), 0, 0, a, b, dd, nvec, 8u);
+                if (v == 11) hipLaunchKernelGGL((fold2_shift<0, LD_PLAIN, LD_PLAIN>), dim3(grid), dim3(256), 0, 0, a, b, dd, nvec, 8u);
+            };
+            Stat w = timed(launch, nsets, false, 30);
+            Stat c = timed(launch, nsets, true, std::max(40, 4 * nsets));
+            static const char *nm[12] = {"copy two-load bpc=1", "copy two-load bpc=2", "copy shfl bpc=1", "copy shfl bpc=2",
+                                        "fold2 double two-load bpc=2", "fold2 double shfl bpc=2",
+                                        "fold2 two-load plain/plain bpc=2", "fold2 two-load nt/plain bpc=2",
+                                        "fold2 two-load plain/nt bpc=2", "fold2 two-load nt/nt U=2 bpc=2",
+                                        "fold2 two-load nt/nt bpc=4", "fold2 two-load plain/plain bpc=4"};
+            emit("shift", nm[v], (size_t)nbuf * B, nsets, w, c);
+        }
+        g_skew = 0;
     }
     CHECK(hipFree(g_pool));
     return 0;

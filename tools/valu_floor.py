@@ -76,8 +76,8 @@ def floor(obj, sub, rates_path, elements, stores=1):
 # bench.py's kernel legs on the long double every-member fold: 8 sources x
 # 32 MiB (2 Mi x87 elements), 8 outputs, each stored when its chain ends
 BENCH_LEGS = {
-    "rs_shard_n8_longdouble_sum": ("combine_orders_vec<0, x80, 8, 1, 1, true>", 2097152, 8),
-    "rs_shard_n8_longdouble_prod": ("combine_orders_vec<1, x80, 8, 1, 1, true>", 2097152, 8),
+    "rs_shard_n8_longdouble_sum": ("combine_orders_vec<0, x80, 8, 1, 1, true, false>", 2097152, 8),
+    "rs_shard_n8_longdouble_prod": ("combine_orders_vec<1, x80, 8, 1, 1, true, false>", 2097152, 8),
 }
 
 
