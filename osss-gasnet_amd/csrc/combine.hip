@@ -215,14 +215,18 @@ __global__ __launch_bounds__(kBlock) void copy_segments_shift(SegParams<NS> p) {
 //   dst[i] = isnan(own[i]) ? quiet(own[i]) : peer[i]
 // (own may alias dst: element-wise read-then-write). Plain loads and `nt sc1`
 // stores as the copy kernel; one more local read stream than the copy.
-// nvec == 0: every element through the element loop (unaligned pointers).
+// dst and peer share their 16-byte phase (one symmetric offset): the host
+// peels `head` elements so both are aligned; own, at another phase when the
+// target is offset against the source, is read unaligned (SHIFT, ld16_src).
+// nvec == 0: every element through the element loop.
 struct PatchParams {
     void *dst;
     const void *peer;
     const void *own;
     const unsigned long long *nan_flag;   // the other member's NaN word, or nullptr (patch)
     uint64_t nvec;   // whole 16-byte vectors
-    uint64_t n;      // elements
+    uint64_t n;      // elements from dst (after the head)
+    uint32_t head;   // elements just before dst / peer / own (peeled)
     Signal sig;
 };
 
@@ -233,7 +237,7 @@ __device__ __forceinline__ R nan_keep_own(R own, R peer) {
     return __builtin_isnan(own) ? __builtin_bit_cast(R, __builtin_bit_cast(U, own) | N::quiet) : peer;
 }
 
-template <typename R>
+template <typename R, bool SHIFT>
 __global__ __launch_bounds__(kBlock) void nan_patch_copy(PatchParams p) {
     constexpr int V = 16 / sizeof(R);
     constexpr int U = 4;
@@ -253,7 +257,7 @@ __global__ __launch_bounds__(kBlock) void nan_patch_copy(PatchParams p) {
             const uint64_t i = base + (uint64_t)u * kBlock;
             if (i < p.nvec) {
                 x[u].v = ld16<POL_PLAIN>(pe + i);
-                if (patch) o[u].v = ld16<POL_PLAIN>(ow + i);
+                if (patch) o[u].v = ld16_src<POL_PLAIN, SHIFT>(ow, i);
             }
         }
 #pragma unroll
@@ -268,9 +272,11 @@ __global__ __launch_bounds__(kBlock) void nan_patch_copy(PatchParams p) {
             }
         }
     }
+    // the elements outside the vectors: [-head, 0) and [V nvec, n)
     bool plain = false;
-    for (uint64_t i = p.nvec * V + (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < p.n;
-         i += (uint64_t)gridDim.x * kBlock) {
+    const uint64_t rest = p.head + (p.n - p.nvec * V);
+    for (uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x; r < rest; r += (uint64_t)gridDim.x * kBlock) {
+        const int64_t i = r < p.head ? (int64_t)r - (int64_t)p.head : (int64_t)(p.nvec * V + (r - p.head));
         const R v = ((const R *)p.peer)[i];
         ((R *)p.dst)[i] = patch ? nan_keep_own(((const R *)p.own)[i], v) : v;
         plain = true;
@@ -480,14 +486,34 @@ extern "C" int mi355_nan_patch_copy(int dtype, void *dst, const void *peer, cons
         }
         if (dst == nullptr || peer == nullptr || own == nullptr) return MI355_E_INVAL;
         const size_t es = mi355_dtype_size(dtype);
-        // 16-byte vectors when every pointer is aligned (the heap's shards
-        // are), else element by element (a user offset into the arrays)
-        const bool vec = (((uintptr_t)dst | (uintptr_t)peer | (uintptr_t)own) & 15) == 0;
-        PatchParams p{dst, peer, own, nan_flag, vec ? (uint64_t)(n * es / 16) : 0, (uint64_t)n, Signal{}};
-        const unsigned grid = vec ? grid_for((uint64_t)kBlock * 4, p.nvec > 0 ? p.nvec : 1, 1)
-                                  : grid_for((uint64_t)kBlock * 4, p.n, 1);
-        return dtype == MI355_FLOAT ? launch(nan_patch_copy<float>, dim3(grid), (hipStream_t)stream, p)
-                                    : launch(nan_patch_copy<double>, dim3(grid), (hipStream_t)stream, p);
+        // 16-byte vectors from the element where dst (and peer, at the same
+        // phase) is aligned; own read unaligned if its phase differs. Element
+        // by element when dst and peer differ in phase or dst is not
+        // element-aligned.
+        const uintptr_t pd = (uintptr_t)dst & 15;
+        const bool vec = pd == ((uintptr_t)peer & 15) && pd % es == 0;
+        const size_t head = vec ? ((16 - pd) & 15) / es : 0;
+        const bool use_vec = vec && n >= head;
+        PatchParams p{};
+        p.nan_flag = nan_flag;
+        if (use_vec) {
+            p.dst = (char *)dst + head * es;
+            p.peer = (const char *)peer + head * es;
+            p.own = (const char *)own + head * es;
+            p.n = n - head;
+            p.head = (uint32_t)head;
+            p.nvec = p.n * es / 16;
+        } else {
+            p.dst = dst;
+            p.peer = peer;
+            p.own = own;
+            p.n = n;
+        }
+        const bool shift = use_vec && ((uintptr_t)p.own & 15) != 0;
+        const unsigned grid = grid_for((uint64_t)kBlock * 4, p.nvec > 0 ? p.nvec : p.n + p.head, 1);
+        auto k = dtype == MI355_FLOAT ? (shift ? nan_patch_copy<float, true> : nan_patch_copy<float, false>)
+                                      : (shift ? nan_patch_copy<double, true> : nan_patch_copy<double, false>);
+        return launch(k, dim3(grid), (hipStream_t)stream, p);
     }();
     if (rc != 0) {
         t_sig = Signal{nullptr, nullptr, 0};

@@ -44,7 +44,7 @@
 struct shmemi_state shmemi;
 
 #define SEG_MAGIC 0x4d49333535534d45ull /* "MI355SME" */
-#define SEG_VERSION 6
+#define SEG_VERSION 7
 
 static double now_s (void)
 {
@@ -487,6 +487,16 @@ void *shmemi_peer_ptr (int pe, size_t off)
     return shmemi.peer_heap[pe] + off;
 }
 
+/* Where PE `pe`'s heap starts in its hipMalloc'd arena. PEs that share a
+ * GPU (the test layout) would otherwise have their symmetric objects at
+ * offsets a large power of two apart in one HBM, so a fold reading the
+ * members' sources at one element offset sends every stream to the same
+ * channels (the version slots are staggered the same
+ * way in reduce.c). 4,352 B = 17 x 256: the heap base stays 256-aligned. */
+#define HEAP_STAGGER 4352
+#define HEAP_STAGGER_SPAN (16 * HEAP_STAGGER)
+static size_t heap_skew (int pe) { return (size_t) (pe % 16) * HEAP_STAGGER; }
+
 static void heap_init (void)
 {
     shmemi.user_size = round_up (env_size ("SHMEM_DEVICE_HEAP_SIZE", (size_t) 2 << 30), SHMEMI_ALIGN);
@@ -505,12 +515,13 @@ static void heap_init (void)
     shmemi.order_chunk = order / 2 / SHMEMI_ALIGN * SHMEMI_ALIGN;
     shmemi.heap_size = shmemi.user_size + scratch + order;
     void *p = NULL;
-    hipError_t e = hipMalloc (&p, shmemi.heap_size);
+    hipError_t e = hipMalloc (&p, shmemi.heap_size + HEAP_STAGGER_SPAN);
     if (e != hipSuccess)
         shmemi_fatal ("hipMalloc of the %zu-byte device symmetric heap failed: %s "
                       "(set SHMEM_DEVICE_HEAP_SIZE / SHMEM_DEVICE_SCRATCH_SIZE)",
                       shmemi.heap_size, hipGetErrorString (e));
-    shmemi.heap = (char *) p;
+    shmemi.heap_arena = (char *) p;
+    shmemi.heap = shmemi.heap_arena + heap_skew (shmemi.mype);
     struct shmemi_block *b = (struct shmemi_block *) calloc (1, sizeof *b);
     if (b == NULL)
         shmemi_fatal ("out of host memory");
@@ -681,7 +692,7 @@ static void heap_exchange (void)
     me->device = shmemi.device;
     if (hipDeviceGetPCIBusId (me->pci_bus_id, (int) sizeof me->pci_bus_id, shmemi.device) != hipSuccess)
         me->pci_bus_id[0] = '\0';
-    SHMEMI_HIP (hipIpcGetMemHandle (&me->heap_handle, shmemi.heap));
+    SHMEMI_HIP (hipIpcGetMemHandle (&me->heap_handle, shmemi.heap_arena));
     SHMEMI_HIP (hipIpcGetMemHandle (&me->sig_handle, shmemi.sigmem));
     me->heap_size = shmemi.heap_size;
     settings_publish ();
@@ -733,7 +744,7 @@ static void heap_exchange (void)
             (void) hipGetLastError ();
             p = NULL;
         }
-        shmemi.peer_heap[pe] = (char *) p;
+        shmemi.peer_heap[pe] = p != NULL ? (char *) p + heap_skew (pe) : NULL;
         p = NULL;
         e = fail != NULL && strcmp (fail, "sig") == 0
                 ? hipErrorInvalidValue
@@ -1393,7 +1404,7 @@ void pshmem_finalize (void)
     if (shmemi.peer_heap != NULL) {
         for (int pe = 0; pe < shmemi.npes; ++pe) {
             if (pe != shmemi.mype && shmemi.peer_heap[pe] != NULL)
-                (void) hipIpcCloseMemHandle (shmemi.peer_heap[pe]);
+                (void) hipIpcCloseMemHandle (shmemi.peer_heap[pe] - heap_skew (pe));
             if (pe != shmemi.mype && shmemi.peer_sig != NULL && shmemi.peer_sig[pe] != NULL)
                 (void) hipIpcCloseMemHandle (shmemi.peer_sig[pe]);
         }
@@ -1410,9 +1421,9 @@ void pshmem_finalize (void)
     shmemi_hheap_finalize (); /* after the barrier above: no peer reads it any more */
     free (shmemi.pair_calls);
     shmemi.pair_calls = NULL;
-    if (shmemi.heap != NULL)
-        (void) hipFree (shmemi.heap);
-    shmemi.heap = NULL;
+    if (shmemi.heap_arena != NULL)
+        (void) hipFree (shmemi.heap_arena);
+    shmemi.heap = shmemi.heap_arena = NULL;
     if (shmemi.sigmem != NULL)
         (void) hipFree (shmemi.sigmem);
     shmemi.sigmem = NULL;

@@ -130,6 +130,7 @@ struct shmemi_state {
 
     /* device symmetric heap: [user | scratch] */
     char *heap;                 /* this PE's base */
+    char *heap_arena;           /* its hipMalloc'd arena (the heap starts heap_skew(mype) bytes in) */
     size_t heap_size;           /* total */
     size_t user_size;           /* user part */
     size_t scratch_off;         /* = user_size */

@@ -544,8 +544,7 @@ def test_combine_shifted_sources(shm, dev, op, dtype, nsrc):
 def test_combine_orders_shifted_sources(shm, dev, op, dtype, nsrc):
     """The every-member fold with its outputs at another 16-byte phase than
     its sources (the P2P schedule with target = &t[1], source = &s[0]): every
-    member's reference result, one output skipped, one in place (same phase as
-    the sources: element-wise)."""
+    member's reference result, with and without a skipped output."""
     import gen_golden
     es = np.dtype(oracle.NP[dtype]).itemsize
     rng = np.random.default_rng(500 + nsrc)
@@ -611,3 +610,41 @@ def test_nan_payloads_sparse_in_large_arrays(shm, dev, op, dtype):
     got = gpu_orders(shm, dev, op, dtype, srcs)
     for q in range(k):
         assert_match(got[q], oracle.reduce_pe(op, dtype, srcs, q), op, dtype, strict=True, ctx=f"member {q}")
+
+
+@pytest.mark.parametrize("dtype", ["float", "double"])
+def test_nan_patch_copy_phases_and_flag(shm, dev, dtype):
+    """mi355_nan_patch_copy (the two-member gather of reduce.c nan_pair):
+    dst[i] = isnan(own[i]) ? quiet(own[i]) : peer[i] when the owner's NaN
+    word is set (or absent), a plain copy of peer when it is clear; dst and
+    peer at one 16-byte phase (a symmetric offset), own at the same or another
+    one (the target offset against the source: own read unaligned)."""
+    import ctypes
+    import gen_golden
+    from shmem_reduce import DTYPES
+    L = shm.lib
+    vp = ctypes.c_void_p
+    L.mi355_nan_patch_copy.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_size_t, vp, vp]
+    L.mi355_nan_patch_copy.restype = ctypes.c_int
+    es = np.dtype(oracle.NP[dtype]).itemsize
+    ut = np.uint32 if es == 4 else np.uint64
+    quiet = ut(1 << 22) if es == 4 else ut(1 << 51)
+    rng = np.random.default_rng(91)
+    words = {v: _upload_at(dev, np.array([v], np.uint64), 0) for v in (0, 1)}
+    for doff, ooff in ((0, 0), (es, 0), (0, 8), (8, es), (12 if es == 4 else 8, 4 if es == 4 else 0)):
+        for n in (1, 5, 1000, 70001):
+            peer = gen_golden.values(rng, "sum", dtype, n)
+            own = gen_golden.values(rng, "sum", dtype, n)
+            pp, po = _upload_at(dev, peer, doff), _upload_at(dev, own, ooff)
+            for flag in (None, 0, 1):
+                d = dev.empty(n * es + 32) + doff
+                rc = L.mi355_nan_patch_copy(DTYPES.index(dtype), d, pp, po, n, None if flag is None else words[flag],
+                                            None)
+                assert rc == 0, rc
+                shm.sync()
+                got = shm.get(d, n, dtype).view(ut)
+                pb, ob = peer.view(ut), own.view(ut)
+                want = pb if flag == 0 else np.where(np.isnan(own), ob | quiet, pb)
+                assert (got == want).all(), (doff, ooff, n, flag, int(np.argmax(got != want)))
+            dev.free()
+            words = {v: _upload_at(dev, np.array([v], np.uint64), 0) for v in (0, 1)}
