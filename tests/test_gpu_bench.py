@@ -83,6 +83,10 @@ def test_bench_one_gpu_line():
     hr = d["headline_rotating"]
     assert hr["check"].startswith("bit-exact") and hr["footprint_MiB"] >= 2048 and hr["kernel"] == r["kernel"], hr
     assert 0 < hr["frac"] <= 1.0 and r["hbm_only"]["frac"] == hr["frac"] and "Infinity Cache" in r["attribution"]
+    # a target one element off the source's 16-byte phase: unaligned-load copy, not 8-byte words
+    ot = d["headline_offset_target"]
+    assert ot["check"].startswith("bit-exact") and ot["kernel"].startswith("void mi355k::copy_segments_shift"), ot
+    assert 0.4 < ot["frac"] <= 1.0 and ot["target_offset_bytes"] == 8, ot
     assert d["coherence_selftest"] is None
     # north_star's host-memory rate: page-locked host arrays, staged over PCIe in each call
     hs = d["host_staged"]
@@ -95,6 +99,7 @@ def test_bench_one_gpu_line():
         assert k[name]["check"].startswith("bit-exact"), (name, k[name])
         assert 0 < k[name]["frac"] <= 1.0 and k[name]["kernel_avg_us"] > 0, (name, k[name])
         assert 0 < k[name]["cold"]["frac"] <= 1.0 and k[name]["cold"]["footprint_MiB"] >= 2048, (name, k[name])
+        assert 0 < k[name]["warm_aligned"]["frac"] <= 1.0, (name, k[name])
     # the x87 sum's own roofline: VALU issue, from this build's instruction stream
     ls = k["rs_shard_n8_longdouble_sum"]
     assert ls["bound"] == "valu" and 0.3 < ls["valu_frac"] < 1.05 and ls["valu_per_element_wave"] > 1000, ls
