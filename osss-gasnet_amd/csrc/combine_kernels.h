@@ -657,7 +657,7 @@ template <int NSRC, typename T> struct Shape {
     static constexpr int unroll =
         alu_heavy ? 1 : NSRC == 2 ? 1 : NSRC == 3 ? 2 : NSRC == 4 ? 1 : NSRC < 8 ? 2 : 4;
     static constexpr int blocks_per_cu =
-        alu_heavy ? 8 : NSRC == 2 ? 2 : NSRC == 3 ? 1 : NSRC == 4 ? 1 : NSRC < 8 ? 4 : 8;
+        alu_heavy ? 8 : NSRC == 2 ? (std::is_same<T, float>::value ? 4 : 2) : NSRC == 3 ? 1 : NSRC == 4 ? 1 : NSRC < 8 ? 4 : 8;
     static constexpr int policy = POL_NT_LOAD;
 };
 

@@ -609,6 +609,21 @@ int main(int argc, char **argv) {
             emit("copy_segments", nm[mode], 14 * B, nsets, w, c);
         }
     }
+    if (what == "k2types") {   // the two-source fold per element type (Shape<2, T> tuning)
+        g_skew = 4352;
+        lib_fold("combine_vec<sum,short,2>", MI355_OP_SUM, MI355_SHORT, 2, S);
+        lib_fold("combine_vec<sum,int,2>", MI355_OP_SUM, MI355_INT, 2, S);
+        lib_fold("combine_vec<xor,long,2>", MI355_OP_XOR, MI355_LONG, 2, S);
+        lib_fold("combine_vec<sum,float,2>", MI355_OP_SUM, MI355_FLOAT, 2, S);
+        lib_fold("combine_vec<max,float,2>", MI355_OP_MAX, MI355_FLOAT, 2, S);
+        lib_fold("combine_vec<sum,double,2>", MI355_OP_SUM, MI355_DOUBLE, 2, S);
+        lib_fold("combine_vec<prod,double,2>", MI355_OP_PROD, MI355_DOUBLE, 2, S);
+        lib_fold("combine_vec<sum,complexf,2>", MI355_OP_SUM, MI355_COMPLEXF, 2, S);
+        lib_fold("combine_vec<prod,complexf,2>", MI355_OP_PROD, MI355_COMPLEXF, 2, S);
+        lib_fold("combine_vec<sum,complexd,2>", MI355_OP_SUM, MI355_COMPLEXD, 2, S);
+        lib_fold("combine_vec<prod,complexd,2>", MI355_OP_PROD, MI355_COMPLEXD, 2, S);
+        g_skew = 0;
+    }
     if (what == "misaligned") {   // target 8 bytes off the sources' 16-byte phase
         g_skew = 4352;
         for (size_t mis : {(size_t)0, (size_t)8, (size_t)4}) {
