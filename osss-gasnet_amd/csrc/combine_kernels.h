@@ -651,7 +651,11 @@ inline unsigned grid_for(uint64_t units_per_block_pass, uint64_t units, int bloc
 //        depth at half the blocks)
 // Box-to-box spread is +-3 %, so neighbours within that band are ties.
 // Long double is VALU-bound (x87 arithmetic in software): it wants many
-// waves to hide ALU latency, not deep per-lane load queues.
+// waves to hide ALU latency, not deep per-lane load queues. Round 5
+// (tools/cold_probe k2types, 256 MiB): the float two-source fold at 4 blocks
+// per CU, 115 vs 122 us (its NaN checks cover four lanes per vector); the
+// float complex product's at 8 (ShapeOp), 131 vs 162 us -- its sum is faster
+// at 2 (120 vs 123 us), so that one is per operator.
 template <int NSRC, typename T> struct Shape {
     static constexpr bool alu_heavy = std::is_same<T, x80>::value;
     static constexpr int unroll =
@@ -659,6 +663,11 @@ template <int NSRC, typename T> struct Shape {
     static constexpr int blocks_per_cu =
         alu_heavy ? 8 : NSRC == 2 ? (std::is_same<T, float>::value ? 4 : 2) : NSRC == 3 ? 1 : NSRC == 4 ? 1 : NSRC < 8 ? 4 : 8;
     static constexpr int policy = POL_NT_LOAD;
+};
+
+template <int OP, int NSRC, typename T> struct ShapeOp : Shape<NSRC, T> {
+    static constexpr int blocks_per_cu =
+        NSRC == 2 && std::is_same<T, cplxf>::value && OP == MI355_OP_PROD ? 8 : Shape<NSRC, T>::blocks_per_cu;
 };
 
 // mi355_combine_orders: NSRC loads and up to NSRC stores per vector (every
@@ -754,7 +763,7 @@ int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, b
             for (int k = 0; k < NSRC; ++k) p.src[k] = (const char *)srcs[k] + head * sizeof(T);
             n -= (size_t)head;
         }
-        using S = Shape<NSRC, T>;
+        using S = ShapeOp<OP, NSRC, T>;
         p.nvec = n / V;
         p.tail = (uint32_t)(n % V);
         auto k = combine_vec<OP, T, NSRC, S::unroll, S::policy>;
@@ -771,7 +780,7 @@ int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, b
             p.dst = (char *)dst + sh * sizeof(T);
             for (int k = 0; k < NSRC; ++k) p.src[k] = (const char *)srcs[k] + sh * sizeof(T);
             n -= (size_t)sh;
-            using S = Shape<NSRC, T>;
+            using S = ShapeOp<OP, NSRC, T>;
             p.nvec = n / V;
             p.tail = (uint32_t)(n % V);
             auto k = combine_vec<OP, T, NSRC, S::unroll, S::policy, true>;
