@@ -14,7 +14,7 @@
 // the copy, variants of its loop compiled here (load / store policy, blocks
 // per CU, vectors per lane).
 //
-// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/cold_probe.hip \
+// build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -I include -I osss-gasnet_amd/csrc tools/cold_probe.hip \
 //          -L osss-gasnet_amd/lib -lshmem_reduce -Wl,-rpath,$PWD/osss-gasnet_amd/lib -o tools/cold_probe
 // run:   tools/cold_probe [lib|copy|all|copy2|orders]   (one JSON line per measurement)
 #include <hip/hip_runtime.h>
@@ -29,6 +29,7 @@
 #include <vector>
 
 #include "mi355_reduce.h"
+#include "combine_kernels.h"   // the library's fold kernels, instantiated here at other launch shapes
 
 #define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
     fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e)); exit(1); } } while (0)
@@ -470,6 +471,36 @@ static void orders_variant(const char *name, K kern, int bpc, int u, size_t byte
     emit("orders8<sum,double>", v, 16 * bytes, nsets, w, c);
 }
 
+// ---- the library's combine_vec at a chosen shape (k8shapes)
+template <int OP, typename T, int U>
+static void fold_shape(const char *name, size_t bytes, int bpc) {
+    constexpr int NS = 8;
+    const int nbuf = NS + 1;
+    const int nsets = sets_for(nbuf * (bytes + g_skew));
+    const uint64_t nvec = bytes / 16;
+    const unsigned grid = (unsigned)std::min<uint64_t>((nvec + 256ull * U - 1) / (256ull * U), (uint64_t)g_cus * bpc);
+    auto launch = [&](int st) {
+        mi355k::CombineParams p{};
+        p.dst = buf(st, NS, nbuf, bytes);
+        for (int k = 0; k < NS; ++k) p.src[k] = buf(st, k, nbuf, bytes);
+        p.nvec = nvec;
+        hipLaunchKernelGGL((mi355k::combine_vec<OP, T, NS, U, mi355k::POL_NT_LOAD, false>), dim3(grid), dim3(256), 0, 0, p);
+    };
+    Stat w = timed(launch, nsets, false, 30);
+    Stat c = timed(launch, nsets, true, std::max(40, 2 * nsets));
+    char v[96];
+    snprintf(v, sizeof v, "8 x %zu MiB U=%d bpc=%d", bytes / MiB, U, bpc);
+    emit(name, v, (size_t)nbuf * bytes, nsets, w, c);
+}
+template <int OP, typename T>
+static void fold_shapes(const char *name, size_t bytes) {
+    for (int bpc : {2, 4, 8}) {
+        fold_shape<OP, T, 1>(name, bytes, bpc);
+        fold_shape<OP, T, 2>(name, bytes, bpc);
+        fold_shape<OP, T, 4>(name, bytes, bpc);
+    }
+}
+
 int main(int argc, char **argv) {
     const std::string what = argc > 1 ? argv[1] : "all";
     CHECK(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -608,6 +639,14 @@ int main(int argc, char **argv) {
             static const char *nm[3] = {"1 x 224 MiB", "7 x 32 MiB, target contiguous", "7 x 32 MiB, both staggered"};
             emit("copy_segments", nm[mode], 14 * B, nsets, w, c);
         }
+    }
+    if (what == "k8shapes") {   // the eight-source fold's launch shape per type (library: U=4, 8 blocks/CU)
+        g_skew = 4352;
+        fold_shapes<MI355_OP_SUM, double>("combine_vec<sum,double,8>", 64 * MiB);
+        fold_shapes<MI355_OP_MAX, float>("combine_vec<max,float,8>", 64 * MiB);
+        fold_shapes<MI355_OP_AND, long long>("combine_vec<and,longlong,8>", 64 * MiB);
+        fold_shapes<MI355_OP_SUM, double>("combine_vec<sum,double,8>", 8 * MiB);
+        g_skew = 0;
     }
     if (what == "k2types") {   // the two-source fold per element type (Shape<2, T> tuning)
         g_skew = 4352;
