@@ -439,7 +439,7 @@ def rotating_leg(shm, S, me, npes, src, dst, k, check):
                     "the 256 MiB Infinity Cache serves" % (ROT_PAIRS, ROT_PAIRS * 2 * S >> 20)}
 
 
-def offset_target_leg(shm, S, me, npes, src, dst, k, check):
+def offset_target_leg(shm, S, me, npes, src, k, check):
     """N = 1: the headline call with the target one element off the source's
     16-byte phase (target = &t[1], source = &s[0], nreduce - 1 elements), a
     caller's offset into an array: the target is peeled to 16 bytes and the
@@ -447,31 +447,34 @@ def offset_target_leg(shm, S, me, npes, src, dst, k, check):
     round 5 an 8-byte-word copy at 0.24 of peak). Timed like the headline."""
     n = S // 8 - 1
     loop = shmem_reduce.bench_loop()
-    tgt = dst + 8
-    loop(tgt, src, n, 0, 0, npes, None, shm._psync_ptr, 3)
-    shm.barrier_all()
-    shm.sync()
-    t0 = time.perf_counter()
-    loop(tgt, src, n, 0, 0, npes, None, shm._psync_ptr, k)
-    shm.sync()
-    t = (time.perf_counter() - t0) / k
-    shm.kernel_timing(True)
-    loop(tgt, src, n, 0, 0, npes, None, shm._psync_ptr, k)
-    shm.sync()
-    nk, _, k_avg_ms = shm.kernel_timing_stats()
-    shm.kernel_timing(False)
-    info = shm.last_call_info()
-    ck = "skipped"
-    if check:
-        import oracle
-        idx = np.unique(np.random.default_rng(600 + me).integers(0, n, 1 << 14)).astype(np.uint64)
-        want = oracle.reduce_pe("sum", "double", [synth(p, idx) for p in range(npes)], me)
-        got = shm.get(tgt, n, "double")[idx.astype(np.int64)]
-        bad = int((got.view(np.uint64) != want.view(np.uint64)).sum())
-        ck = f"bit-exact vs the reference, {len(idx)} samples" if bad == 0 else f"MISMATCH in {bad} samples"
-    # the headline's target as the headline left it (its check reads it later)
-    loop(dst, src, n + 1, 0, 0, npes, None, shm._psync_ptr, 1)
-    shm.sync()
+    own = shm.malloc_device(S)   # its own target: the headline's stays as the headline left it
+    if not own:
+        raise RuntimeError("the device heap has no room for a %d-byte target" % S)
+    tgt = own + 8
+    try:
+        loop(tgt, src, n, 0, 0, npes, None, shm._psync_ptr, 3)
+        shm.barrier_all()
+        shm.sync()
+        t0 = time.perf_counter()
+        loop(tgt, src, n, 0, 0, npes, None, shm._psync_ptr, k)
+        shm.sync()
+        t = (time.perf_counter() - t0) / k
+        shm.kernel_timing(True)
+        loop(tgt, src, n, 0, 0, npes, None, shm._psync_ptr, k)
+        shm.sync()
+        nk, _, k_avg_ms = shm.kernel_timing_stats()
+        shm.kernel_timing(False)
+        info = shm.last_call_info()
+        ck = "skipped"
+        if check:
+            import oracle
+            idx = np.unique(np.random.default_rng(600 + me).integers(0, n, 1 << 14)).astype(np.uint64)
+            want = oracle.reduce_pe("sum", "double", [synth(p, idx) for p in range(npes)], me)
+            got = shm.get(tgt, n, "double")[idx.astype(np.int64)]
+            bad = int((got.view(np.uint64) != want.view(np.uint64)).sum())
+            ck = f"bit-exact vs the reference, {len(idx)} samples" if bad == 0 else f"MISMATCH in {bad} samples"
+    finally:
+        shm.free_device(own)
     alg = info["alg_bytes"] // max(1, info["launches"])
     kt = k_avg_ms * 1e-3
     achieved = alg / kt / 1e9 if kt > 0 else 0.0
@@ -915,17 +918,18 @@ def main():
     t_calls = call_times(dst, src, n, 0, 0, npes, shm._psync_ptr, args.steps)
     legs_s["headline"] = round(time.perf_counter() - t_head0, 2)
 
+    # N = 1: the same call into a target one element off (offset_target_leg);
+    # before the rotating leg, whose launches rocprof's split counts last
+    offset_target = None
+    if npes == 1 and not args.host:
+        with timed_leg("headline_offset_target"):
+            offset_target = offset_target_leg(shm, S, me, npes, src, args.steps, not args.no_check)
+
     # N = 1: the same call with every byte from HBM (rotating_leg)
     rotating = None
     if npes == 1 and not args.host and not args.no_rotating:
         with timed_leg("headline_rotating"):
             rotating = rotating_leg(shm, S, me, npes, src, dst, args.steps, not args.no_check)
-
-    # N = 1: the same call into a target one element off (offset_target_leg)
-    offset_target = None
-    if npes == 1 and not args.host:
-        with timed_leg("headline_offset_target"):
-            offset_target = offset_target_leg(shm, S, me, npes, src, dst, args.steps, not args.no_check)
 
     # the many-small-bucket regime (BASELINE config 5 shape: 64 KiB per call)
     small_n, small_calls = 8192, 0 if args.no_small else 4096   # BASELINE config 5: 4096 x 64 KiB
