@@ -161,13 +161,14 @@ def fused_same_gpu(npes, calls, persistent=False):
     procs = [subprocess.Popen([sys.executable, script, str(calls)], env=dict(env, SHMEM_PE=str(pe)),
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for pe in range(npes)]
     outs = []
-    try:
-        for p in procs:
-            outs.append(p.communicate(timeout=180))
-    except subprocess.TimeoutExpired:
-        for p in procs:
-            p.kill()
-        return {"error": "timed out"}
+    for p in procs:
+        r = wait_child(p, "fused_same_gpu")
+        if r is None:
+            for q in procs:
+                q.kill()
+                q.communicate()
+            return {"error": "timed out after 150 s"}
+        outs.append(r)
     if any(p.returncode != 0 for p in procs):
         return {"error": "; ".join(f"PE {i} rc {p.returncode}: {o[1][-300:]}" for i, (p, o) in enumerate(zip(procs, outs))
                                    if p.returncode != 0)}
@@ -209,6 +210,25 @@ def traffic_for(rec, key, host):
     return f"PMC passes of this library's kernels (gfx950 code objects {want})"
 
 
+def wait_child(p, name, limit=150):
+    """communicate() with a child job, printing a heartbeat to stderr every
+    30 s (a silent wait reads as a hang to a watchdog) and giving up after
+    `limit` s. Returns (out, err) or None on the time limit (child killed)."""
+    import subprocess
+    t0 = time.perf_counter()
+    while True:
+        try:
+            return p.communicate(timeout=30)
+        except subprocess.TimeoutExpired:
+            waited = time.perf_counter() - t0
+            if waited >= limit:
+                p.kill()
+                p.communicate()
+                return None
+            print(f"[bench rank {os.environ.get('RANK', '0')}] {name}: child job running, {waited:.0f} s",
+                  file=sys.stderr, flush=True)
+
+
 def persistent_child(rank, world, calls):
     """N > 1: BASELINE config 5's 64 KiB calls with the opt-in persistent
     server (SHMEM_PERSISTENT=1), run by one child PE process per rank on the
@@ -228,12 +248,10 @@ def persistent_child(rank, world, calls):
     script = os.path.join(ROOT, "tools", "fused_bench.py")
     p = subprocess.Popen([sys.executable, script, str(calls), str(64 << 10)], env=env, stdout=subprocess.PIPE,
                          stderr=subprocess.PIPE, text=True)
-    try:
-        out, err = p.communicate(timeout=240)
-    except subprocess.TimeoutExpired:
-        p.kill()
-        p.communicate()
-        return {"error": "timed out after 240 s"}
+    r = wait_child(p, "small_call_persistent")
+    if r is None:
+        return {"error": "timed out after 150 s"}
+    out, err = r
     if p.returncode != 0:
         return {"error": f"PE {rank} rc {p.returncode}: {err[-400:]}"}
     lines = [ln for ln in out.splitlines() if ln.startswith("{")]
@@ -275,12 +293,10 @@ def extra_legs_child(rank, world, mib, steps, algorithm, flags):
 
     def failed(msg):
         return {k: {"error": msg} for k in names}
-    try:
-        out, err = p.communicate(timeout=240)
-    except subprocess.TimeoutExpired:
-        p.kill()
-        p.communicate()
-        return failed("child job timed out after 240 s")
+    r = wait_child(p, "extra_legs_child")
+    if r is None:
+        return failed("child job timed out after 150 s")
+    out, err = r
     if p.returncode != 0:
         return failed(f"child job: PE {rank} rc {p.returncode}: {err[-400:]}")
     if rank != 0:
@@ -773,6 +789,9 @@ def main():
     @contextlib.contextmanager
     def timed_leg(name, optional=True):
         t0 = time.perf_counter()
+        # progress on stderr (the JSON line is stdout's only content): a run
+        # that stops shows which leg it stopped in
+        print(f"[bench rank {os.environ.get('RANK', '0')}] {name} ...", file=sys.stderr, flush=True)
         try:
             yield
         except Exception as e:  # noqa: BLE001 -- reported in the line
@@ -835,6 +854,7 @@ def main():
     shm = shmem_reduce.Shmem()
     shm.init()
     legs_s["init"] = round(time.perf_counter() - t_init0, 2)
+    print(f"[bench rank {rank}] headline ...", file=sys.stderr, flush=True)
     t_head0 = time.perf_counter()
     # the init self-test found peer heap reads broken: the library runs the
     # RCCL pairs through RCCL whatever is selected
@@ -851,7 +871,9 @@ def main():
         ran, passed, stale = shm.coherence_selftest()
         sysload, no_acq = shm.coherence_sysload()
         prod_ran, prod = shm.coherence_producer()
+        slow_waits, barrier_us = shm.device_wait_report()
         coherence = {"ran": ran, "passed": passed, "stale_without_acquire": stale,
+                     "device_barrier_us": round(barrier_us, 1), "device_waits_timesliced": slow_waits,
                      "sysload_fresh": sysload, "fused_acquires_skipped": no_acq,
                      "producer_path": dict(prod, ran=prod_ran,
                                            note="32 words written with plain stores by a kernel on the null stream "

@@ -211,6 +211,12 @@ void shmemx_coherence_sysload (int *sysload_fresh, int *acquires_skipped);
  * sysload_fresh) hold; it is not used when neither fresh[1] nor fresh[2];
  * the job runs RCCL when fresh[5] fails. ran = 0 above 64 PEs. */
 void shmemx_coherence_producer (int *ran, int *fresh);
+/* The init timing of device-side waits (PE_size > 1 jobs with signal regions):
+ * us = the job's slowest PE's time per device barrier over all PEs; slow = 1
+ * when that passed 1 ms (the hardware time-slices the PEs' queues: more PEs
+ * on one GPU than it schedules together), and then the job runs host barriers
+ * and no fused kernel. */
+void shmemx_device_wait_report (int *slow, double *us);
 
 /* Bring up the RCCL communicator of the whole job (what SHMEM_REDUCE_ALGORITHM=rccl uses) without
  * aborting when RCCL cannot come up within timeout_s seconds: 0 = ready on this PE, -1 = not. Every PE

@@ -272,7 +272,7 @@ static void member_args (MI355FusedArgs *a, const struct aset *s, int chan)
 static int device_flags_ok (const struct aset *s)
 {
     return s->size <= MI355_FUSED_MAX_MEMBERS && shmemi.npes <= MI355_SIG_RSDONE && shmemi.sigmem != NULL &&
-           !shmemi.sig_broken;
+           !shmemi.sig_broken && !shmemi.dev_wait_slow;
 }
 
 static void device_barrier (const MI355FusedArgs *a, hipStream_t st)
@@ -726,6 +726,7 @@ static void server_start (int op, int dtype, size_t es, size_t n, int oneshot, c
     /* the grid of this call's launch (mi355_fused_allreduce) */
     const unsigned long long vecs = oneshot || s->size == 1 ? (n * es + 15) / 16
                                                             : shard_chunk (n, es, s->size) * es / 16 * (s->size - 1);
+    shmemi_lazy_stream (&shmemi.srv.st, hipStreamNonBlocking);
     const int rc = mi355_fused_server (&a, mb, shmemi.srv.seq, (unsigned long long) (shmemi.srv.idle_s * 1e8), vecs,
                                        shmemi.srv.st);
     if (rc != 0) {
@@ -972,6 +973,8 @@ static void staged (int op, int dtype, const char *fn, void *target, const void 
                     const struct aset *s, int ks, int kt, int use_rccl)
 {
     const size_t es = mi355_dtype_size (dtype);
+    shmemi_lazy_stream (&shmemi.stream_in, hipStreamDefault);
+    shmemi_lazy_stream (&shmemi.stream_out, hipStreamDefault);
     const size_t half = shmemi.scratch_chunk / 2 / SHMEMI_ALIGN * SHMEMI_ALIGN;
     const size_t per = half / es;
     const size_t nchunks = (n + per - 1) / per;

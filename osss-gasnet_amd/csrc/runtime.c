@@ -44,7 +44,7 @@
 struct shmemi_state shmemi;
 
 #define SEG_MAGIC 0x4d49333535534d45ull /* "MI355SME" */
-#define SEG_VERSION 7
+#define SEG_VERSION 8
 
 static double now_s (void)
 {
@@ -552,6 +552,20 @@ static void signal_init (void)
     shmemi.sig_epoch = 0;
 }
 
+/* A stream the library needs only on some paths, created on first use. Every
+ * stream takes one of the process's hardware queues (HIP's
+ * GPU_MAX_HW_QUEUES, 4 by default), and the device-side waits of the fused
+ * kernel and the device barriers need every member's queue scheduled at
+ * once: with 6 PEs sharing one GPU and 4 queues each, the hardware
+ * time-sliced the queues and a 64 KiB fused call took 22 ms instead of
+ * 40 us (2 queues each). A PE that never stages host buffers or runs the
+ * persistent server keeps two: the null stream and the library's stream. */
+void shmemi_lazy_stream (hipStream_t *st, unsigned flags)
+{
+    if (*st == NULL)
+        SHMEMI_HIP (hipStreamCreateWithFlags (st, flags));
+}
+
 /* The persistent server's mailbox (host-coherent, same address on both
  * sides) and stream; SHMEM_PERSISTENT=1 turns it on (reduce.c). */
 static void server_init (void)
@@ -564,7 +578,7 @@ static void server_init (void)
     memset (h, 0, sizeof (MI355ServerMailbox));
     shmemi.srv.mb = (MI355ServerMailbox *) h;
     shmemi.srv.seq = 1;
-    SHMEMI_HIP (hipStreamCreateWithFlags (&shmemi.srv.st, hipStreamNonBlocking));
+    shmemi.srv.st = NULL; /* created by the first server start (shmemi_lazy_stream) */
     static const char *pe_env[] = {"SHMEM_PERSISTENT", NULL};
     static const char *idle_env[] = {"SHMEM_PERSISTENT_IDLE_US", NULL};
     shmemi.srv.enabled = env_long (pe_env, 0) != 0;
@@ -933,6 +947,75 @@ static void producer_test (size_t off, int *res)
     free (host);
 }
 
+
+/* Device-side waits across PEs need every member's hardware queue scheduled
+ * at once. With more queues on one GPU than the hardware maps together
+ * (PEs sharing a GPU, 4 queues each by default: 6 PEs = 24), the queues are
+ * time-sliced and every spin-wait lasts until its peers' turn: a 64 KiB
+ * fused call took 22 ms instead of 40 us (bench.py fused_same_gpu at 6 PEs,
+ * 40 us with GPU_MAX_HW_QUEUES=2). So init times 8 device barriers over the
+ * whole job and counts the queues on this GPU; if any PE finds either too
+ * high, every PE runs host barriers and no fused kernel (kernels that never
+ * wait on each other run fine time-sliced).
+ * The stream-ordered collectives have only device barriers: they stay, slow.
+ * SHMEM_TEST_IPC_FAIL=slowwait makes PE 1 report slow waits (tests). */
+static void device_wait_test (int np, int me)
+{
+    MI355FusedArgs a;
+    shmemi_member_args (&a, 0, 1, np, me);
+    /* one untimed barrier (first launch of the kernel), then every PE starts
+     * the timed ones together: a late PE would otherwise count as slow waits */
+    if (mi355_device_barrier (&a, shmemi.stream) != 0)
+        shmemi_fatal ("self-test device barrier launch failed");
+    SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    shmemi_barrier_set (0, 1, np);
+    const int k = 8;
+    const double t0 = shmemi_now ();
+    for (int i = 0; i < k; ++i)
+        if (mi355_device_barrier (&a, shmemi.stream) != 0)
+            shmemi_fatal ("self-test device barrier launch failed");
+    SHMEMI_HIP (hipStreamSynchronize (shmemi.stream));
+    const double us = (shmemi_now () - t0) / k * 1e6;
+    int slow = us > 1000.0;
+    /* At init each PE has touched only the null stream's and the library
+     * stream's queues, so the timing above passes even where the steady
+     * state (HIP allocates up to GPU_MAX_HW_QUEUES per process as it runs)
+     * is time-sliced: 6 PEs x 4 queues timed 8 barriers fine and still ran
+     * fused calls at 22 ms. PEs x queues on this GPU above 16 (4 PEs x 4 ran
+     * at full speed) counts as slow too. */
+    static const char *hwq_env[] = {"GPU_MAX_HW_QUEUES", NULL};
+    const long hwq = env_long (hwq_env, 4);
+    slow |= (long) shmemi.local_pes * (hwq > 0 ? hwq : 4) > 16;
+    const char *fail = me == 1 ? getenv ("SHMEM_TEST_IPC_FAIL") : NULL;
+    slow |= fail != NULL && strcmp (fail, "slowwait") == 0;
+    /* SHMEM_DEVICE_WAITS=1 keeps the device-side waits whatever the above says,
+     * =0 turns them off (a job-wide setting, like the others) */
+    static const char *dw_env[] = {"SHMEM_DEVICE_WAITS", NULL};
+    const long force = env_long (dw_env, -1);
+    if (force == 0 || force == 1)
+        slow = force == 0;
+    /* the timing in ns, this PE's vote in bit 63 */
+    __atomic_store_n (&seg_info (me)->barrier_ns, (uint64_t) (us * 1e3) | ((uint64_t) slow << 63), __ATOMIC_RELEASE);
+    shmemi_barrier_set (0, 1, np);
+    double worst = 0;
+    int any_slow = 0;
+    for (int q = 0; q < np; ++q) {
+        const uint64_t r = __atomic_load_n (&seg_info (q)->barrier_ns, __ATOMIC_ACQUIRE);
+        const double u = (double) (r & ~(1ull << 63)) * 1e-3;
+        worst = u > worst ? u : worst;
+        any_slow |= (int) (r >> 63);
+    }
+    shmemi.dev_barrier_us = worst;
+    if (any_slow) {
+        if (me == 0)
+            fprintf (stderr, "[shmem] warning: device-side waits across PEs would be time-sliced (%d PE(s) on this "
+                             "GPU x %ld hardware queues; init barriers %.0f us each; GPU_MAX_HW_QUEUES=2 lowers a PE's "
+                             "share): host barriers, no fused kernel\n", shmemi.local_pes, hwq, worst);
+        shmemi.dev_wait_slow = 1;
+        shmemi.fused_max = 0, shmemi.fused_off = 1;
+    }
+}
+
 /* Interconnect check at init (PE_size > 1): every PE stores a value into
  * every peer's signal region over the peer mapping (what the fused kernel's
  * flags do) and reads a marker from every peer's heap (what the reduce-scatter
@@ -1078,6 +1161,8 @@ static void interconnect_selftest (void)
                              "the fused small-message kernel is disabled\n");
         shmemi.fused_max = 0, shmemi.fused_off = 1;
         shmemi.sig_broken = 1;
+    } else {
+        device_wait_test (np, me);
     }
     if (!all_heap) {
         if (me == 0)
@@ -1312,8 +1397,8 @@ void pshmem_init (void)
     SHMEMI_HIP (hipSetDevice (shmemi.device));
     /* blocking: ordered after the null stream, see shmemi_order_after_caller */
     SHMEMI_HIP (hipStreamCreateWithFlags (&shmemi.stream, hipStreamDefault));
-    SHMEMI_HIP (hipStreamCreateWithFlags (&shmemi.stream_in, hipStreamDefault));
-    SHMEMI_HIP (hipStreamCreateWithFlags (&shmemi.stream_out, hipStreamDefault));
+    /* stream_in / stream_out (host staging) and the server's stream come with
+     * their first use (shmemi_lazy_stream) */
     for (int i = 0; i < 2; ++i) {
         SHMEMI_HIP (hipEventCreateWithFlags (&shmemi.ev_in[i], hipEventDisableTiming));
         SHMEMI_HIP (hipEventCreateWithFlags (&shmemi.ev_out[i], hipEventDisableTiming));
@@ -1456,8 +1541,11 @@ void pshmem_finalize (void)
             (void) hipEventDestroy (shmemi.ev_in[i]);
             (void) hipEventDestroy (shmemi.ev_out[i]);
         }
-        (void) hipStreamDestroy (shmemi.stream_in);
-        (void) hipStreamDestroy (shmemi.stream_out);
+        if (shmemi.stream_in != NULL)
+            (void) hipStreamDestroy (shmemi.stream_in);
+        if (shmemi.stream_out != NULL)
+            (void) hipStreamDestroy (shmemi.stream_out);
+        shmemi.stream_in = shmemi.stream_out = NULL;
         (void) hipStreamDestroy (shmemi.stream);
     }
     shmemi.stream = NULL;
@@ -1623,6 +1711,14 @@ void shmemx_coherence_producer (int *ran, int *fresh)
     if (fresh != NULL)
         for (int i = 0; i < 6; ++i)
             fresh[i] = shmemi.prod[i];
+}
+
+void shmemx_device_wait_report (int *slow, double *us)
+{
+    if (slow != NULL)
+        *slow = shmemi.dev_wait_slow;
+    if (us != NULL)
+        *us = shmemi.dev_barrier_us;
 }
 
 int shmemx_get_reduce_order (void) { return shmemi.order; }

@@ -72,6 +72,7 @@ struct shmemi_pe_info {
                                    shmemi.prod[] order: fused ordering plain / sysload / acquire, then the
                                    host-wait ordering plain / sysload / acquire */
     uint64_t collect_bytes;     /* this PE's contribution to the current shmem_collect */
+    uint64_t barrier_ns;        /* init: this PE's time per device barrier over the job (device_wait_test) */
     struct shmemi_settings settings;
     struct shmemi_dbg_rec dbg;
     struct shmemi_ext_rec ext;
@@ -162,6 +163,8 @@ struct shmemi_state {
     size_t oneshot_max;         /* SHMEM_ONESHOT_MAX_BYTES: largest fused message folded one-shot */
     int fused_off;              /* a failed self-test disabled the fused path: the setters keep it off */
     int sig_broken;             /* peers' signal-region stores failed the init self-test */
+    int dev_wait_slow;          /* device-side waits across PEs time-sliced (init timing): host barriers, no fused kernel */
+    double dev_barrier_us;      /* that timing: the job's slowest PE, microseconds per device barrier */
 
     /* completion signal: host-coherent word the last block of a kernel writes */
     unsigned *sig_flag;         /* hipHostMalloc coherent+mapped, same address on both sides */
@@ -258,6 +261,7 @@ void *shmemi_host_dev_ptr (const void *p, size_t nbytes);
 /* reduce.c: the persistent fused server; every GPU operation that could wait
  * on it (another spin-waiting grid, a device-wide synchronization, freeing
  * memory) stops it first */
+void shmemi_lazy_stream (hipStream_t *st, unsigned flags);
 void shmemi_server_stop (void);
 
 /* reduce.c: device-flag barrier on the library stream (host channel) */

@@ -133,6 +133,7 @@ void shmemi_trace_show_info (void)
         {"SHMEM_PERSISTENT", "1: back-to-back fused calls served by a resident fused kernel (opt-in; shmemx.h)"},
         {"SHMEM_PERSISTENT_IDLE_US", "the persistent server leaves after this long without a call (default 1000)"},
         {"SHMEM_FUSED_MAX_BYTES", "largest message for the one-launch fused reduction (default 2M)"},
+        {"SHMEM_DEVICE_WAITS", "1: keep device-side waits (fused kernel, device barriers) even where init finds them time-sliced; 0: host barriers"},
         {"SHMEM_ONESHOT_MAX_BYTES", "largest fused message folded one-shot, not reduce-scatter + all-gather (default 64K)"},
         {"SHMEM_BARRIER_TIMEOUT", "seconds before a barrier wait aborts the job (default 600)"},
         {"SHMEM_BOOTSTRAP_TIMEOUT", "seconds a PE waits at init for PE 0 to create the job's segment (default: "

@@ -344,6 +344,13 @@ class Shmem:
         self.lib.shmemx_coherence_producer(ctypes.byref(ran), fresh)
         return bool(ran.value), {k: bool(fresh[i]) for i, k in enumerate(self.PRODUCER_FIELDS)}
 
+    def device_wait_report(self):
+        """(slow, us): the init timing of device barriers over the job (shmemx.h
+        shmemx_device_wait_report); slow = host barriers and no fused kernel"""
+        slow, us = _i(), ctypes.c_double()
+        self.lib.shmemx_device_wait_report(ctypes.byref(slow), ctypes.byref(us))
+        return bool(slow.value), us.value
+
     def kernel_timing(self, enable):
         self.lib.shmemx_kernel_timing(1 if enable else 0)
 

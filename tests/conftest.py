@@ -28,6 +28,13 @@ def pytest_collection_modifyitems(session, config, items):
 
 _SHM = None
 
+# Up to 12 PE processes share the test GPU. With HIP's default of 4 hardware
+# queues each, more than 4 of them exceed what the GPU schedules together and
+# the library (runtime.c device_wait_test) would run host barriers instead of
+# the device-side waits these tests are meant to cover; 2 queues each keeps up
+# to 8 PEs on the device path (the spawned PE processes inherit this).
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "2")
+
 
 @pytest.fixture(scope="session")
 def shm():

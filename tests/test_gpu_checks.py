@@ -167,6 +167,31 @@ def test_stale_fused_ordering_turns_the_fused_kernel_off():
     assert "the fused kernel is disabled" in outs[0], outs[0]
 
 
+def test_timesliced_device_waits_use_host_barriers():
+    """PE 1 votes its device-side waits slow (SHMEM_TEST_IPC_FAIL=slowwait, as
+    when more PEs share a GPU than it schedules together): every PE records
+    the slow waits, turns the fused kernel off (the setter cannot re-enable
+    it) and runs host barriers; the results stay bit-exact. Without the fault
+    the init timing is recorded and nothing is turned off."""
+    code = FUSED_OFF.replace("shm.finalize()\n", "print('DW', *shm.device_wait_report(), flush=True)\nshm.finalize()\n")
+    rcs, outs, _ = spawn(3, code, extra={"SHMEM_TEST_IPC_FAIL": "slowwait"})
+    for rc, out in zip(rcs, outs):
+        assert rc == 0, out[-2000:]
+        assert parse(out, "THR")[0][0] == "0" and parse(out, "THR2")[0][0] == "0", out
+        bad = parse(out, "BAD")[0]
+        assert bad[0] == "0" and not any("fused" in x for x in bad[2:]), out
+        slow, us = parse(out, "DW")[0]
+        assert slow == "True" and float(us) > 0.0, out
+    assert "host barriers, no fused kernel" in outs[0], outs[0]
+    # without the fault: the timing is recorded, nothing turned off
+    rcs, outs, _ = spawn(3, code)
+    for rc, out in zip(rcs, outs):
+        assert rc == 0, out[-2000:]
+        slow, us = parse(out, "DW")[0]
+        assert slow == "False" and 0.0 < float(us) < 1000.0, out
+        assert parse(out, "BAD")[0][0] == "0", out
+
+
 # ---------------------------------------------------------------------------
 # SHMEM_DEBUG=1 collective argument check
 # ---------------------------------------------------------------------------
