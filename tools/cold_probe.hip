@@ -231,6 +231,52 @@ __global__ __launch_bounds__(256) void copy_unal(const char *s, u32x4 *d, uint64
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < nvec; i += (uint64_t)gridDim.x * 256)
         st<ST_NT_SC1>(d + i, *(const u32x4 *)(s + 16 * i));
 }
+// copy_segments_shift's loop (pipelined, U vectors per lane) on unaligned sources
+template <int U, bool PIPE>
+__global__ __launch_bounds__(256) void copy_unal_u(const char *src, u32x4 *d, uint64_t nvec) {
+    const mi355k::u32x4_any *s = (const mi355k::u32x4_any *)src;
+    const uint64_t step = (uint64_t)gridDim.x * 256 * U;
+    uint64_t base = (uint64_t)blockIdx.x * 256 * U + threadIdx.x;
+    if constexpr (PIPE) {
+        u32x4 x[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = base + (uint64_t)u * 256;
+            if (i < nvec) x[u] = s[i];
+        }
+        while (base < nvec) {
+            const uint64_t next = base + step;
+            u32x4 y[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t i = next + (uint64_t)u * 256;
+                if (i < nvec) y[u] = s[i];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t i = base + (uint64_t)u * 256;
+                if (i < nvec) st<ST_NT_SC1>(d + i, x[u]);
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) x[u] = y[u];
+            base = next;
+        }
+    } else {
+        for (; base < nvec; base += step) {
+            u32x4 x[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t i = base + (uint64_t)u * 256;
+                if (i < nvec) x[u] = s[i];
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t i = base + (uint64_t)u * 256;
+                if (i < nvec) st<ST_NT_SC1>(d + i, x[u]);
+            }
+        }
+    }
+}
 // sa: the source's aligned base (source - delta); nvec output vectors; every
 // lane of a wave active for the shuffle (lanes past the end load a clamped index)
 template <int U, int MODE, int LD, int ST>
@@ -678,6 +724,29 @@ int main(int argc, char **argv) {
             if (mis % 8 == 0) lib_orders(nm, MI355_OP_SUM, MI355_DOUBLE, 8, 32 * MiB);
         }
         g_dst_mis = 0;
+        g_skew = 0;
+    }
+    if (what == "unalcopy") {   // the shifted copy's loop shape
+        const size_t B = S - 4096;
+        const uint64_t nvec = B / 16;
+        g_skew = 4352;
+        const int nsets = sets_for(2 * (S + g_skew));
+        struct V { const char *name; void (*k)(const char *, u32x4 *, uint64_t); int U; int bpc; };
+        const V vs[] = {{"pipe U=4 bpc=1", copy_unal_u<4, true>, 4, 1}, {"pipe U=4 bpc=2", copy_unal_u<4, true>, 4, 2},
+                        {"pipe U=2 bpc=2", copy_unal_u<2, true>, 2, 2}, {"pipe U=2 bpc=4", copy_unal_u<2, true>, 2, 4},
+                        {"flat U=1 bpc=2", copy_unal_u<1, false>, 1, 2}, {"flat U=1 bpc=4", copy_unal_u<1, false>, 1, 4},
+                        {"flat U=2 bpc=2", copy_unal_u<2, false>, 2, 2}, {"flat U=4 bpc=1", copy_unal_u<4, false>, 4, 1},
+                        {"flat U=4 bpc=2", copy_unal_u<4, false>, 4, 2}};
+        for (const V &v : vs) {
+            const unsigned grid = (unsigned)std::min<uint64_t>((nvec + 256ull * v.U - 1) / (256ull * v.U), (uint64_t)g_cus * v.bpc);
+            auto launch = [&](int st) {
+                hipLaunchKernelGGL(v.k, dim3(grid), dim3(256), 0, 0, (const char *)buf(st, 0, 2, S) + 8,
+                                   (u32x4 *)buf(st, 1, 2, S), nvec);
+            };
+            Stat w = timed(launch, nsets, false, 30);
+            Stat c = timed(launch, nsets, true, std::max(40, 4 * nsets));
+            emit("copy_unal", v.name, 2 * B, nsets, w, c);
+        }
         g_skew = 0;
     }
     if (what == "unal") {   // misaligned 16-byte loads: correct? fast?
