@@ -49,17 +49,17 @@ struct SegParams {
     Signal sig;
 };
 
-// Where a segment's vector part starts: `head` bytes peeled so the target is
-// 16-byte aligned (to a 128-byte line when source and target share their
-// offset within one), then the source's phase against it (0: both aligned;
-// otherwise copy_segments_shift).
+// Where a segment's vector part starts: `head` bytes peeled so the target
+// starts on a 128-byte line (whole-line stores: a target 16 bytes off its
+// line cost the copy 96 us against 77 per 256 MiB, profiles/r05/cold/
+// linepeel_*.jsonl), then the source's phase against it (0: 16-byte aligned
+// too; otherwise copy_segments_shift).
 struct SegPlan {
     uint64_t head;
     unsigned delta;
 };
 __host__ __device__ inline SegPlan seg_plan(const void *dst, const void *src, uint64_t nb) {
-    const unsigned dmis128 = (unsigned)((uintptr_t)dst & 127);
-    uint64_t head = dmis128 == (unsigned)((uintptr_t)src & 127) ? (128u - dmis128) & 127u : (16u - (dmis128 & 15u)) & 15u;
+    uint64_t head = (128u - (unsigned)((uintptr_t)dst & 127)) & 127u;
     if (head > nb) head = nb;
     return {head, (unsigned)(((uintptr_t)src + head) & 15)};
 }
@@ -71,15 +71,14 @@ __global__ __launch_bounds__(kBlock) void copy_segments(SegParams<NS> p) {
     const char *src = (const char *)p.src[sg];
     char *dst = (char *)p.dst[sg];
     // 16-byte vectors where both ends are aligned: pointers with the same
-    // misalignment (a user offset into two arrays) peel a head so that both
-    // start on a 128-byte line (or at least on 16 bytes); different
-    // misalignments take the narrow path below
+    // misalignment within 16 bytes (a user offset into two arrays) peel a
+    // head so that the target starts on a 128-byte line (seg_plan); different
+    // misalignments take the narrow path below (the launcher sends them to
+    // copy_segments_shift)
     const unsigned mis128 = (unsigned)((uintptr_t)dst & 127);
     const unsigned mis = mis128 & 15u;
     const bool coaligned = mis == (unsigned)((uintptr_t)src & 15);
-    uint64_t head = !coaligned ? nb
-                    : mis128 == (unsigned)((uintptr_t)src & 127) ? (128u - mis128) & 127u
-                                                                  : (16u - mis) & 15u;
+    uint64_t head = !coaligned ? nb : (128u - mis128) & 127u;
     if (head > nb) head = nb;
     uint64_t vec_end = head;  // bytes [head, vec_end) go as vectors
     if (coaligned) {
@@ -490,9 +489,12 @@ extern "C" int mi355_nan_patch_copy(int dtype, void *dst, const void *peer, cons
         // phase) is aligned; own read unaligned if its phase differs. Element
         // by element when dst and peer differ in phase or dst is not
         // element-aligned.
+        // dst is peeled to its 128-byte line (whole-line stores, see
+        // combine_kernels.h vector_head) when n reaches it, else to 16 bytes.
         const uintptr_t pd = (uintptr_t)dst & 15;
         const bool vec = pd == ((uintptr_t)peer & 15) && pd % es == 0;
-        const size_t head = vec ? ((16 - pd) & 15) / es : 0;
+        const size_t lh = ((128 - ((uintptr_t)dst & 127)) & 127) / es;
+        const size_t head = !vec ? 0 : n >= lh ? lh : ((16 - pd) & 15) / es;
         const bool use_vec = vec && n >= head;
         PatchParams p{};
         p.nan_flag = nan_flag;

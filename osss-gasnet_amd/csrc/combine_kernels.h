@@ -698,27 +698,41 @@ template <int OP, int NSRC, typename T> struct OrdersShape {
     static constexpr int policy = POL_NT_LOAD;
 };
 
-// How a launch over these pointers can run as 16-byte vectors: 0 = every
-// pointer aligned; h > 0 = every pointer equally misaligned by whole elements
-// (a user offset into the arrays): fold the first h elements element-wise and
-// the rest as vectors from the advanced pointers (peeled to a 128-byte line
-// when all share the misalignment within the line, else to 16 bytes); -1 =
-// element-wise kernel.
+// Elements to peel so that every output starts on a 128-byte line, when the
+// outputs share their offset within one (the symmetric target on each PE)
+// and n reaches past it; else so that they start on 16 bytes. Outputs off
+// their line store partial lines at both ends of every wave's span: a fold
+// or copy whose target sits 16 bytes off its line ran 3-25 % slower warm and
+// up to 30 % slower from HBM (profiles/r05/cold/linepeel_*.jsonl). pd: the
+// outputs' common phase within 16 bytes (a multiple of the element size).
+// 16-byte elements: no head (the kernels fold a head only for V > 1).
 template <typename T>
-long vector_head(const void *const *ptrs, int np, size_t n) {
-    constexpr int V = 16 / sizeof(T);
-    uintptr_t orbits = 0;
-    for (int k = 0; k < np; ++k) orbits |= (uintptr_t)ptrs[k];
-    if ((orbits & 15) == 0) return 0;
-    if (V == 1) return -1;
-    uintptr_t mis = (uintptr_t)ptrs[0] & 127;
+size_t line_head(const void *const *outs, int nout, uintptr_t pd, size_t n) {
+    if (sizeof(T) >= 16) return 0;
+    const uintptr_t pl = (uintptr_t)outs[0] & 127;
     bool line = true;
-    for (int k = 1; k < np; ++k) line = line && ((uintptr_t)ptrs[k] & 127) == mis;
-    if (!line) mis &= 15;
-    bool same = mis % sizeof(T) == 0;
-    for (int k = 1; k < np; ++k) same = same && ((uintptr_t)ptrs[k] & (line ? 127 : 15)) == mis;
-    const size_t head = ((line ? 128 : 16) - mis) / sizeof(T);
-    return same && n > head ? (long)head : -1;
+    for (int k = 1; k < nout; ++k) line = line && ((uintptr_t)outs[k] & 127) == pl;
+    const size_t h = ((128 - pl) & 127) / sizeof(T);
+    return line && n > h ? h : ((16 - pd) & 15) / sizeof(T);
+}
+
+// How a launch over these pointers can run as 16-byte vectors: h >= 0 =
+// every pointer at one phase within 16 bytes, by whole elements (0 or a user
+// offset into the arrays): fold the first h elements (line_head) element-wise
+// and the rest as vectors from the advanced pointers; -1 = not vectorisable
+// this way (shift_head below, else the element-wise kernel).
+template <typename T>
+long vector_head(const void *const *outs, int nout, const void *const *ins, int nin, size_t n) {
+    constexpr int V = 16 / sizeof(T);
+    const uintptr_t pd = (uintptr_t)(nout > 0 ? outs[0] : ins[0]) & 15;
+    bool same = pd % sizeof(T) == 0;
+    for (int k = 0; k < nout; ++k) same = same && ((uintptr_t)outs[k] & 15) == pd;
+    for (int k = 0; k < nin; ++k) same = same && ((uintptr_t)ins[k] & 15) == pd;
+    if (!same) return -1;
+    if (V == 1 || nout == 0) return pd == 0 ? 0 : -1;
+    const size_t head = line_head<T>(outs, nout, pd, n);
+    if (head == 0 || n > head) return (long)head;
+    return pd == 0 ? 0 : -1;
 }
 
 // Outputs 16-byte aligned after peeling whole elements and every source at
@@ -739,7 +753,7 @@ long shift_head(const void *const *outs, int nout, const void *const *srcs, int 
         for (int k = 1; k < nsrc; ++k)
             if (((uintptr_t)srcs[k] & 15) != ps) return -1;
         if (pd % es != 0) return -1;
-        const size_t head = ((16 - pd) & 15) / es;
+        const size_t head = line_head<T>(outs, nout, pd, n);
         if (((ps + head * es) & 15) == 0 || n < head + V) return -1;
         return (long)head;
     }
@@ -755,7 +769,7 @@ int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, b
     ptrs[0] = dst;
     for (int k = 0; k < NSRC; ++k) p.src[k] = ptrs[1 + k] = srcs[k];
     constexpr int V = 16 / sizeof(T);
-    const long head = vector_head<T>(ptrs, NSRC + 1, n);
+    const long head = vector_head<T>(&ptrs[0], 1, &ptrs[1], NSRC, n);
     if (head >= 0) {
         if (head > 0) {
             p.head = (uint32_t)head;
@@ -798,15 +812,15 @@ int launch_fixed(void *dst, const void *const *srcs, size_t n, hipStream_t st, b
 template <int OP, typename T, int NSRC>
 int launch_orders_fixed(void *const *dsts, const void *const *srcs, size_t n, hipStream_t st) {
     OrdersParams p{};
-    const void *ptrs[2 * kMaxSrc];
-    int np = 0;
+    const void *outs[kMaxSrc];
+    int nout = 0;
     for (int k = 0; k < NSRC; ++k) {
-        p.src[k] = ptrs[np++] = srcs[k];
+        p.src[k] = srcs[k];
         p.dst[k] = dsts[k];
-        if (dsts[k] != nullptr) ptrs[np++] = dsts[k];
+        if (dsts[k] != nullptr) outs[nout++] = dsts[k];
     }
     constexpr int V = 16 / sizeof(T);
-    const long head = vector_head<T>(ptrs, np, n);
+    const long head = vector_head<T>(outs, nout, srcs, NSRC, n);
     if (head >= 0) {
         if (head > 0) {
             p.head = (uint32_t)head;
@@ -836,10 +850,6 @@ int launch_orders_fixed(void *const *dsts, const void *const *srcs, size_t n, hi
         const unsigned grid = grid_for((uint64_t)kBlock * S::unroll, p.nvec, bpc);
         return launch(k, dim3(grid), st, p);
     }
-    const void *outs[kMaxSrc];
-    int nout = 0;
-    for (int k = 0; k < NSRC; ++k)
-        if (dsts[k] != nullptr) outs[nout++] = dsts[k];
     const long sh = nout > 0 ? shift_head<T>(outs, nout, srcs, NSRC, n) : -1;
     if constexpr (!std::is_same<T, x80>::value) {
         if (sh >= 0) {

@@ -563,6 +563,49 @@ def test_combine_orders_shifted_sources(shm, dev, op, dtype, nsrc):
             dev.free()
 
 
+LINE_TYPES = [("sum", "short"), ("xor", "int"), ("sum", "float"), ("max", "float"), ("sum", "double"),
+              ("prod", "complexf"), ("sum", "complexd"), ("sum", "longdouble")]
+
+
+@pytest.mark.parametrize("op,dtype", LINE_TYPES)
+def test_targets_peeled_to_their_line(shm, dev, op, dtype):
+    """Targets 16-112 bytes off a 128-byte line (a symmetric offset into the
+    arrays): the fold, the every-member fold and the copy peel the target to
+    its line (combine_kernels.h line_head, combine.hip seg_plan), folding or
+    copying the head element-wise; sources on their line, at the target's
+    offset, or (shifted loads) at another 16-byte phase. Sizes around the
+    head: n below it (16-byte peel or element-wise), at it, just past it,
+    one vector past it, many vectors."""
+    import ctypes
+    import gen_golden
+    es = np.dtype(oracle.NP[dtype]).itemsize
+    rng = np.random.default_rng(6100 + es)
+    cases = [(16, 0), (48, 48), (112, 0), (64 + es, 0)] if es < 16 else [(16, 0), (112, 0), (48, 48)]
+    for doff, soff in cases:
+        h = ((128 - doff) & 127) // es
+        for n in sorted({1, max(1, h - 1), h, h + 1, h + 16 // es + 1, 5000}):
+            srcs = [gen_golden.values(rng, op, dtype, n) for _ in range(3)]
+            ptrs = [_upload_at(dev, x, soff) for x in srcs]
+            out = dev.empty(n * es + 128) + doff
+            assert shm.combine(op, dtype, out, ptrs, n) == 0
+            shm.sync()
+            ctx = f"target +{doff}, sources +{soff}, n={n}"
+            assert_match(shm.get(out, n, dtype), oracle.reduce_pe(op, dtype, srcs, 0), op, dtype, ctx=ctx)
+            dp = [dev.empty(n * es + 128) + doff for _ in range(3)]
+            assert shm.combine_orders(op, dtype, dp, ptrs, n) == 0
+            shm.sync()
+            for q in range(3):
+                assert_match(shm.get(dp[q], n, dtype), oracle.reduce_pe(op, dtype, srcs, q), op, dtype,
+                             ctx=f"member {q}, {ctx}")
+            nb = n * es
+            d = dev.empty(nb + 128) + doff
+            dsts, sps, nbs = (ctypes.c_void_p * 1)(d), (ctypes.c_void_p * 1)(ptrs[0]), (ctypes.c_size_t * 1)(nb)
+            assert shm.lib.mi355_copy_segments(dsts, sps, nbs, 1, None) == 0
+            shm.sync()
+            assert (shm.get(d, nb, np.uint8) == srcs[0].view(np.uint8)).all(), ctx
+            dev.free()
+
+
 # ---------------------------------------------------------------------------
 # NaN payloads: the golden_nan_* families (float, double and complex sum/prod
 # on NaN-rich operands, outputs of the reference's compiled operators) through
@@ -631,7 +674,9 @@ def test_nan_patch_copy_phases_and_flag(shm, dev, dtype):
     quiet = ut(1 << 22) if es == 4 else ut(1 << 51)
     rng = np.random.default_rng(91)
     words = {v: _upload_at(dev, np.array([v], np.uint64), 0) for v in (0, 1)}
-    for doff, ooff in ((0, 0), (es, 0), (0, 8), (8, es), (12 if es == 4 else 8, 4 if es == 4 else 0)):
+    # (48, 0), (72, 0): dst and peer off their 128-byte line, peeled to it
+    for doff, ooff in ((0, 0), (es, 0), (0, 8), (8, es), (12 if es == 4 else 8, 4 if es == 4 else 0), (48, 0),
+                       (72, 0)):
         for n in (1, 5, 1000, 70001):
             peer = gen_golden.values(rng, "sum", dtype, n)
             own = gen_golden.values(rng, "sum", dtype, n)

@@ -403,6 +403,7 @@ static size_t g_pool_bytes;
 static size_t g_skew;      // extra bytes between consecutive buffers (orders_skew)
 static int g_skew_from;    // ... from buffer index g_skew_from on
 static size_t g_dst_mis;   // bytes added to every output pointer (misaligned-target probe)
+static size_t g_src_mis;   // ... to every source pointer (linepeel)
 
 static void emit(const char *kernel, const char *variant, size_t alg, int nsets, Stat w, Stat c) {
     printf("{\"kernel\": \"%s\", \"variant\": \"%s\", \"alg_bytes\": %zu, \"sets\": %d, \"footprint_MiB\": %zu, "
@@ -449,7 +450,7 @@ static void lib_copy(size_t bytes, const char *name = "copy_segments<4,1>") {
     const int nsets = sets_for(2 * bytes);
     auto launch = [&](int s) {
         void *d[1] = {buf(s, 1, 2, bytes) + g_dst_mis};
-        const void *sr[1] = {buf(s, 0, 2, bytes)};
+        const void *sr[1] = {buf(s, 0, 2, bytes) + g_src_mis};
         size_t nb[1] = {bytes - (g_dst_mis ? 16 : 0)};
         if (mi355_copy_segments(d, sr, nb, 1, nullptr) != 0) exit(2);
     };
@@ -464,7 +465,7 @@ static void lib_fold(const char *name, int op, int dtype, int k, size_t bytes) {
     const size_t n = bytes / mi355_dtype_size(dtype);
     auto launch = [&](int s) {
         const void *sr[8];
-        for (int j = 0; j < k; ++j) sr[j] = buf(s, j, nbuf, bytes);
+        for (int j = 0; j < k; ++j) sr[j] = buf(s, j, nbuf, bytes) + g_src_mis;
         if (mi355_combine(op, dtype, buf(s, k, nbuf, bytes) + g_dst_mis, sr, k, n - (g_dst_mis ? 1 : 0), nullptr) != 0) exit(2);
     };
     Stat w = timed_lib(launch, nsets, false, 30);
@@ -482,7 +483,7 @@ static void lib_orders(const char *name, int op, int dtype, int k, size_t bytes)
         const void *sr[8];
         void *ds[8];
         for (int j = 0; j < k; ++j) {
-            sr[j] = buf(s, j, nbuf, bytes);
+            sr[j] = buf(s, j, nbuf, bytes) + g_src_mis;
             ds[j] = buf(s, k + j, nbuf, bytes) + g_dst_mis;
         }
         if (mi355_combine_orders(op, dtype, ds, sr, k, n - (g_dst_mis ? 1 : 0), nullptr) != 0) exit(2);
@@ -723,6 +724,37 @@ int main(int argc, char **argv) {
             snprintf(nm, sizeof nm, "combine_orders_vec<sum,double,8> dst+%zu", mis);
             if (mis % 8 == 0) lib_orders(nm, MI355_OP_SUM, MI355_DOUBLE, 8, 32 * MiB);
         }
+        g_dst_mis = 0;
+        g_skew = 0;
+    }
+    if (what == "linepeel") {   // targets off a 128-byte line: aligned (+16, +48) and shifted (+8, +72)
+        g_skew = 4352;
+        for (size_t mis : {(size_t)16, (size_t)48, (size_t)8, (size_t)72}) {
+            g_dst_mis = mis;
+            char nm[96];
+            snprintf(nm, sizeof nm, "copy_segments dst+%zu", mis);
+            lib_copy(S, nm);
+            snprintf(nm, sizeof nm, "combine_vec<sum,double,2> dst+%zu", mis);
+            lib_fold(nm, MI355_OP_SUM, MI355_DOUBLE, 2, S);
+            snprintf(nm, sizeof nm, "combine_vec<sum,float,2> dst+%zu", mis);
+            lib_fold(nm, MI355_OP_SUM, MI355_FLOAT, 2, S);
+            snprintf(nm, sizeof nm, "combine_orders_vec<sum,double,8> dst+%zu", mis);
+            lib_orders(nm, MI355_OP_SUM, MI355_DOUBLE, 8, 32 * MiB);
+        }
+        g_dst_mis = 0;
+        // sources off their line, target on it; both 16 bytes off
+        for (size_t dm : {(size_t)0, (size_t)16}) {
+            g_src_mis = 16;
+            g_dst_mis = dm;
+            char nm[96];
+            snprintf(nm, sizeof nm, "copy_segments src+16 dst+%zu", dm);
+            lib_copy(S, nm);
+            snprintf(nm, sizeof nm, "combine_vec<sum,double,2> src+16 dst+%zu", dm);
+            lib_fold(nm, MI355_OP_SUM, MI355_DOUBLE, 2, S);
+            snprintf(nm, sizeof nm, "combine_orders_vec<sum,double,8> src+16 dst+%zu", dm);
+            lib_orders(nm, MI355_OP_SUM, MI355_DOUBLE, 8, 32 * MiB);
+        }
+        g_src_mis = 0;
         g_dst_mis = 0;
         g_skew = 0;
     }
