@@ -552,14 +552,14 @@ static void signal_init (void)
     shmemi.sig_epoch = 0;
 }
 
-/* A stream the library needs only on some paths, created on first use. Every
- * stream takes one of the process's hardware queues (HIP's
- * GPU_MAX_HW_QUEUES, 4 by default), and the device-side waits of the fused
- * kernel and the device barriers need every member's queue scheduled at
- * once: with 6 PEs sharing one GPU and 4 queues each, the hardware
- * time-sliced the queues and a 64 KiB fused call took 22 ms instead of
- * 40 us (2 queues each). A PE that never stages host buffers or runs the
- * persistent server keeps two: the null stream and the library's stream. */
+/* Creates a stream if it does not exist yet (the staging and server paths
+ * call it before use; init creates them). The library's streams are created
+ * together at init, so that HIP deals them distinct hardware queues: created
+ * later, after other code's streams, the staging copy-in and copy-out
+ * streams shared one and host-staged calls serialised their two directions
+ * (256 MiB: 10.1 ms against 6.15 ms per call, round 5). Many PEs sharing one
+ * GPU are a matter of GPU_MAX_HW_QUEUES (device_wait_test below), not of how
+ * many streams a process has. */
 void shmemi_lazy_stream (hipStream_t *st, unsigned flags)
 {
     if (*st == NULL)
@@ -578,7 +578,7 @@ static void server_init (void)
     memset (h, 0, sizeof (MI355ServerMailbox));
     shmemi.srv.mb = (MI355ServerMailbox *) h;
     shmemi.srv.seq = 1;
-    shmemi.srv.st = NULL; /* created by the first server start (shmemi_lazy_stream) */
+    SHMEMI_HIP (hipStreamCreateWithFlags (&shmemi.srv.st, hipStreamNonBlocking));
     static const char *pe_env[] = {"SHMEM_PERSISTENT", NULL};
     static const char *idle_env[] = {"SHMEM_PERSISTENT_IDLE_US", NULL};
     shmemi.srv.enabled = env_long (pe_env, 0) != 0;
@@ -1397,8 +1397,8 @@ void pshmem_init (void)
     SHMEMI_HIP (hipSetDevice (shmemi.device));
     /* blocking: ordered after the null stream, see shmemi_order_after_caller */
     SHMEMI_HIP (hipStreamCreateWithFlags (&shmemi.stream, hipStreamDefault));
-    /* stream_in / stream_out (host staging) and the server's stream come with
-     * their first use (shmemi_lazy_stream) */
+    SHMEMI_HIP (hipStreamCreateWithFlags (&shmemi.stream_in, hipStreamDefault));
+    SHMEMI_HIP (hipStreamCreateWithFlags (&shmemi.stream_out, hipStreamDefault));
     for (int i = 0; i < 2; ++i) {
         SHMEMI_HIP (hipEventCreateWithFlags (&shmemi.ev_in[i], hipEventDisableTiming));
         SHMEMI_HIP (hipEventCreateWithFlags (&shmemi.ev_out[i], hipEventDisableTiming));
