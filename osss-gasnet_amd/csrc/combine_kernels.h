@@ -735,11 +735,13 @@ long vector_head(const void *const *outs, int nout, const void *const *ins, int 
     return pd == 0 ? 0 : -1;
 }
 
-// Outputs 16-byte aligned after peeling whole elements and every source at
-// one other phase: the vector kernels with unaligned source loads (SHIFT).
-// Returns the elements to peel, or -1 (sources at mixed phases, an output
-// not element-aligned, no whole vector, long double). The aligned launch
-// shapes (cold_probe unal: the same rates at 2 or 4 blocks per CU).
+// Outputs 16-byte aligned after peeling whole elements and the sources at
+// any phases, one or several (an offset into some of the arrays): the vector
+// kernels with unaligned source loads (SHIFT; an unaligned-form load of an
+// aligned address is the same instruction). Returns the elements to peel,
+// or -1 (outputs at different phases or not element-aligned, no whole
+// vector, long double). The aligned launch shapes (cold_probe unal: the
+// same rates at 2 or 4 blocks per CU).
 template <typename T>
 long shift_head(const void *const *outs, int nout, const void *const *srcs, int nsrc, size_t n) {
     if constexpr (std::is_same<T, x80>::value) {
@@ -747,14 +749,14 @@ long shift_head(const void *const *outs, int nout, const void *const *srcs, int 
     } else {
         constexpr size_t es = sizeof(T);
         constexpr size_t V = 16 / es;
-        const uintptr_t pd = (uintptr_t)outs[0] & 15, ps = (uintptr_t)srcs[0] & 15;
+        const uintptr_t pd = (uintptr_t)outs[0] & 15;
         for (int k = 1; k < nout; ++k)
             if (((uintptr_t)outs[k] & 15) != pd) return -1;
-        for (int k = 1; k < nsrc; ++k)
-            if (((uintptr_t)srcs[k] & 15) != ps) return -1;
         if (pd % es != 0) return -1;
         const size_t head = line_head<T>(outs, nout, pd, n);
-        if (((ps + head * es) & 15) == 0 || n < head + V) return -1;
+        bool aligned = true;
+        for (int k = 0; k < nsrc; ++k) aligned = aligned && (((uintptr_t)srcs[k] + head * es) & 15) == 0;
+        if (aligned || n < head + V) return -1;
         return (long)head;
     }
 }

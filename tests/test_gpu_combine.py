@@ -492,8 +492,8 @@ def _upload_at(dev, arr, off):
 
 def test_combine_target_and_sources_misaligned_differently(shm, dev):
     """Target one element off, sources three off: the sources share a phase
-    the target lacks, so the fold runs as vectors with shifted loads
-    (funnel16); sources at different phases from each other run element-wise.
+    the target lacks, so the fold runs as vectors with unaligned source
+    loads; sources at different phases from each other too (shift_head).
     Results as the oracle's."""
     import gen_golden
     n, es = 3001, 8
@@ -604,6 +604,37 @@ def test_targets_peeled_to_their_line(shm, dev, op, dtype):
             shm.sync()
             assert (shm.get(d, nb, np.uint8) == srcs[0].view(np.uint8)).all(), ctx
             dev.free()
+
+
+@pytest.mark.parametrize("op,dtype", SHIFT_TYPES)
+def test_combine_mixed_source_phases(shm, dev, op, dtype):
+    """Sources at different 16-byte phases from each other (an offset into
+    some of the arrays only): the fold and the every-member fold run as
+    vectors with unaligned loads from every source (shift_head); targets on
+    and off their phase. Every value as the oracle's."""
+    import gen_golden
+    es = np.dtype(oracle.NP[dtype]).itemsize
+    rng = np.random.default_rng(700 + es)
+    for nsrc in (2, 3, 8):
+        soffs = [(k * es) % 16 + (16 if k % 3 == 2 else 0) for k in range(nsrc)]
+        if len({o % 16 for o in soffs}) == 1:
+            soffs[1] += 8   # 16-byte elements (complex double: 8-byte aligned in C)
+        for doff in (0, es if es < 16 else 8, 48):
+            for n in (5, 1000, 65537):
+                srcs = [gen_golden.values(rng, op, dtype, n) for _ in range(nsrc)]
+                sp = [_upload_at(dev, x, o) for x, o in zip(srcs, soffs)]
+                ctx = f"sources +{soffs}, target +{doff}, n={n}"
+                out = dev.empty(n * es + 64) + doff
+                assert shm.combine(op, dtype, out, sp, n) == 0
+                shm.sync()
+                assert_match(shm.get(out, n, dtype), oracle.reduce_pe(op, dtype, srcs, 0), op, dtype, ctx=ctx)
+                dp = [dev.empty(n * es + 64) + doff for _ in range(nsrc)]
+                assert shm.combine_orders(op, dtype, dp, sp, n) == 0
+                shm.sync()
+                for q in range(nsrc):
+                    assert_match(shm.get(dp[q], n, dtype), oracle.reduce_pe(op, dtype, srcs, q), op, dtype,
+                                 ctx=f"member {q}, {ctx}")
+                dev.free()
 
 
 # ---------------------------------------------------------------------------
