@@ -63,11 +63,14 @@ int mi355_op_supported (int op, int dtype);
  * for i < n: a left fold with the accumulator on the left, exactly the
  * operand order of reduce-op.c:247-248. Sources may be peer (xGMI) pointers.
  * dst may alias srcs[0] exactly; other overlaps are undefined. nsrc >= 1
- * (nsrc == 1 is a copy). Any element-aligned pointers: 16-byte vectors when
- * every pointer shares one 16-byte phase, or when the sources share one and
- * dst another (unaligned source loads); element by element otherwise. The
- * same holds for mi355_combine_orders (outputs vs sources) and, per segment,
- * for mi355_copy_segments at byte granularity. */
+ * (nsrc == 1 is a copy). Any element-aligned pointers: 16-byte vectors, the
+ * target peeled to its 128-byte line (the head folded element by element),
+ * the sources read aligned when they share the target's 16-byte phase and
+ * with unaligned loads at any other phases. Element by element: a 16-byte
+ * element type (complex double, long double) whose target is not 16-byte
+ * aligned, and long double sources off the target's phase. The same holds for mi355_combine_orders while its
+ * outputs share one 16-byte phase (element by element otherwise) and, per
+ * segment, for mi355_copy_segments at byte granularity. */
 int mi355_combine (int op, int dtype, void *dst, const void *const *srcs,
                    int nsrc, size_t n, void *stream);
 
