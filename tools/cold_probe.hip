@@ -548,6 +548,31 @@ static void fold_shapes(const char *name, size_t bytes) {
     }
 }
 
+// ---- the library's combine_orders_vec at a chosen shape (o8shapes)
+template <int OP, typename T, int U>
+static void orders_shape(const char *name, size_t bytes, int bpc) {
+    constexpr int NS = 8;
+    const int nbuf = 2 * NS;
+    const int nsets = sets_for(nbuf * (bytes + g_skew));
+    const uint64_t nvec = bytes / 16;
+    const unsigned grid = (unsigned)std::min<uint64_t>((nvec + 256ull * U - 1) / (256ull * U), (uint64_t)g_cus * bpc);
+    auto launch = [&](int st) {
+        mi355k::OrdersParams p{};
+        for (int k = 0; k < NS; ++k) {
+            p.src[k] = buf(st, k, nbuf, bytes);
+            p.dst[k] = buf(st, NS + k, nbuf, bytes);
+        }
+        p.nvec = nvec;
+        hipLaunchKernelGGL((mi355k::combine_orders_vec<OP, T, NS, U, mi355k::POL_NT_LOAD, true, false>), dim3(grid),
+                           dim3(256), 0, 0, p);
+    };
+    Stat w = timed(launch, nsets, false, 30);
+    Stat c = timed(launch, nsets, true, std::max(40, 2 * nsets));
+    char v[96];
+    snprintf(v, sizeof v, "8 x %zu MiB U=%d bpc=%d grid=%u", bytes / MiB, U, bpc, grid);
+    emit(name, v, (size_t)nbuf * bytes, nsets, w, c);
+}
+
 int main(int argc, char **argv) {
     const std::string what = argc > 1 ? argv[1] : "all";
     CHECK(hipDeviceGetAttribute(&g_cus, hipDeviceAttributeMultiprocessorCount, 0));
@@ -693,6 +718,21 @@ int main(int argc, char **argv) {
         fold_shapes<MI355_OP_MAX, float>("combine_vec<max,float,8>", 64 * MiB);
         fold_shapes<MI355_OP_AND, long long>("combine_vec<and,longlong,8>", 64 * MiB);
         fold_shapes<MI355_OP_SUM, double>("combine_vec<sum,double,8>", 8 * MiB);
+        g_skew = 0;
+    }
+    if (what == "o8shapes") {   // the every-member fold's shape at shard sizes (library: float max U=1 bpc=8, double sum U=4 bpc=8)
+        g_skew = 4352;
+        for (int bpc : {2, 4, 8}) {
+            orders_shape<MI355_OP_MAX, float, 1>("combine_orders_vec<max,float,8>", 8 * MiB, bpc);
+            orders_shape<MI355_OP_MAX, float, 2>("combine_orders_vec<max,float,8>", 8 * MiB, bpc);
+        }
+        orders_shape<MI355_OP_MAX, float, 1>("combine_orders_vec<max,float,8>", 32 * MiB, 8);
+        orders_shape<MI355_OP_MAX, float, 2>("combine_orders_vec<max,float,8>", 32 * MiB, 4);
+        for (int bpc : {2, 4, 8}) {
+            orders_shape<MI355_OP_SUM, double, 2>("combine_orders_vec<sum,double,8>", 8 * MiB, bpc);
+            orders_shape<MI355_OP_SUM, double, 4>("combine_orders_vec<sum,double,8>", 8 * MiB, bpc);
+        }
+        orders_shape<MI355_OP_SUM, double, 4>("combine_orders_vec<sum,double,8>", 32 * MiB, 8);
         g_skew = 0;
     }
     if (what == "k2types") {   // the two-source fold per element type (Shape<2, T> tuning)
