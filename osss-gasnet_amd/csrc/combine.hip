@@ -151,9 +151,10 @@ __global__ __launch_bounds__(kBlock) void copy_segments(SegParams<NS> p) {
 }
 
 // A launch with a segment whose source is at another 16-byte phase than its
-// target (a byte offset into one of the buffers): the target peeled to 16
-// bytes, then copy_segments' pipelined loop with unaligned source loads
-// (combine_kernels.h ld16_src; 0.77 of peak against 0.24 in 8-byte words). Only such launches take this kernel, so
+// target (a byte offset into one of the buffers): the target peeled to its
+// 128-byte line (seg_plan), then copy_segments' pipelined loop with unaligned source loads
+// (combine_kernels.h ld16_src; 0.87 of peak with the target on its line,
+// against 0.24 in 8-byte words). Only such launches take this kernel, so
 // copy_segments' code stays as measured.
 template <int UNROLL, int NS>
 __global__ __launch_bounds__(kBlock) void copy_segments_shift(SegParams<NS> p) {
@@ -165,9 +166,9 @@ __global__ __launch_bounds__(kBlock) void copy_segments_shift(SegParams<NS> p) {
     const u32x4 *s = (const u32x4 *)(src + head);   // not 16-byte aligned: read with ld16_src<.., true>
     u32x4 *d = (u32x4 *)(dst + head);
     const uint64_t nvec = (nb - head) / 16;
-    // copy_segments' pipelined loop, two blocks per CU (cold_probe
-    // misaligned, 256 MiB: 87 us = 0.77 of peak; one vector per lane per pass:
-    // 119 us)
+    // copy_segments' pipelined loop, two blocks per CU (cold_probe linepeel,
+    // 256 MiB: 77 us = 0.87 of peak, 87 us before the target was peeled to
+    // its line; one vector per lane per pass: 119 us)
     const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
     uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
     u32x4 x[UNROLL];
