@@ -494,10 +494,17 @@ def offset_target_leg(shm, S, me, npes, src, k, check):
     alg = info["alg_bytes"] // max(1, info["launches"])
     kt = k_avg_ms * 1e-3
     achieved = alg / kt / 1e9 if kt > 0 else 0.0
-    return {"value": round(npes * n * 8 / t / GIB, 2), "unit": "GiB/s", "ms_per_step": round(t * 1e3, 4), "steps": k,
-            "target_offset_bytes": 8, "schedule": info["schedule"], "kernel": info["kernel"],
-            "kernel_avg_us": round(k_avg_ms * 1e3, 2), "launches_timed": nk, "alg_bytes_per_launch": alg,
-            "achieved_GB_s": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4), "check": ck}
+    rec = {"value": round(npes * n * 8 / t / GIB, 2), "unit": "GiB/s", "ms_per_step": round(t * 1e3, 4), "steps": k,
+           "target_offset_bytes": 8, "schedule": info["schedule"], "kernel": info["kernel"],
+           "kernel_avg_us": round(k_avg_ms * 1e3, 2), "launches_timed": nk, "alg_bytes_per_launch": alg,
+           "achieved_GB_s": round(achieved, 1), "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+           "check": ck}
+    # unaligned 16-byte loads span two lines: PMC bytes show whether the
+    # line one wave shares with the next is fetched twice
+    rec["traffic_note"] = traffic_for(rec, "offset_target_copy_shift", False)
+    if rec.get("traffic"):
+        rec["traffic_over_alg"] = round(rec["traffic"] / alg, 4)
+    return rec
 
 
 # ---------------------------------------------------------------------------
@@ -840,9 +847,13 @@ def main():
             fused_p = fused_same_gpu(2, 4096 if args.no_small is False else 512, persistent=True)
     t_init0 = time.perf_counter()
 
-    # N = 1: room for headline_rotating's extra pairs too
+    # N = 1: room for headline_rotating's extra pairs too, and for the offset
+    # leg's target (freed before the rotating leg allocates)
     pairs = ROT_PAIRS if world == 1 and not args.host and not args.no_rotating else 1
-    os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(2 * S * pairs + (64 << 20)))
+    heap = 2 * S * pairs
+    if world == 1 and not args.host:
+        heap = max(heap, 3 * S)
+    os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(heap + (64 << 20)))
     os.environ.setdefault("SHMEM_DEVICE_SCRATCH_SIZE", str(96 << 20))
     # a PE that never arrives ends the bench within two minutes with the
     # library's diagnostic (the library default, 600 s, suits long jobs)

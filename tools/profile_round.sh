@@ -39,6 +39,7 @@ while read -r key sub grid; do
     python3 tools/pmc_traffic.py "$OUT/fetch" "$OUT/write" "${sub//\~/ }" "$grid" "$key" "$J" > /dev/null
 done <<'EOF'
 n1_256mib copy_segments<4,~1> 1000
+offset_target_copy_shift copy_segments_shift<4,~1> 1000
 kernel_fold_k2_double_sum combine_vec<0,~double,~2, 1000
 kernel_fold_k8_double_sum combine_vec<0,~double,~8, 1000
 kernel_rs_shard_n8_double_sum combine_orders_vec<0,~double,~8, 1000
