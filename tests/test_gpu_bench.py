@@ -87,10 +87,13 @@ def test_bench_one_gpu_line():
     ot = d["headline_offset_target"]
     assert ot["check"].startswith("bit-exact") and ot["kernel"].startswith("void mi355k::copy_segments_shift"), ot
     assert 0.4 < ot["frac"] <= 1.0 and ot["target_offset_bytes"] == 8, ot
+    assert ot["traffic"] is None or ot["traffic_over_alg"] < 1.03, ot   # PMC profile of this build, when committed
     assert d["coherence_selftest"] is None
     # north_star's host-memory rate: page-locked host arrays, staged over PCIe in each call
     hs = d["host_staged"]
-    assert hs["check"].startswith("bit-exact") and hs["value"] > 0 and 0.2 < hs["pcie_frac"] < 1.2, hs
+    # >= 0.7 of the two-way PCIe rate: copy-in and copy-out overlap (0.55 when
+    # the staging streams shared a hardware queue, runtime.c shmemi_lazy_stream)
+    assert hs["check"].startswith("bit-exact") and hs["value"] > 0 and 0.7 < hs["pcie_frac"] < 1.2, hs
     assert hs["pcie"]["both_GB_s_each_direction"] > 0, hs
     k = d["kernels"]
     for name in ("fold_k2_double_sum", "fold_k8_double_sum", "rs_shard_n8_double_sum", "fold_k8_float_max",
