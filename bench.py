@@ -142,7 +142,7 @@ def cpu_baseline(S, n_gpus, budget_s):
     return out
 
 
-def fused_same_gpu(npes, calls, persistent=False):
+def fused_same_gpu(npes, calls, persistent=False, config1=False):
     """The fused one-launch schedule (fused.hip), which every call up to 2 MiB
     per PE takes at N > 1, measured on this box's one GPU: `npes` PE processes
     of tools/fused_bench.py sharing it (started from this process before it
@@ -158,7 +158,8 @@ def fused_same_gpu(npes, calls, persistent=False):
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
         env.pop(k, None)
     script = os.path.join(ROOT, "tools", "fused_bench.py")
-    procs = [subprocess.Popen([sys.executable, script, str(calls)], env=dict(env, SHMEM_PE=str(pe)),
+    procs = [subprocess.Popen([sys.executable, script, str(calls)] + (["--config1"] if config1 else []),
+                              env=dict(env, SHMEM_PE=str(pe)),
                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True) for pe in range(npes)]
     outs = []
     for p in procs:
@@ -381,8 +382,12 @@ def host_staged_leg(shm, loop, S, me, npes, k, check):
     shm.free(hdst)
     shm.free(hsrc)
     gbs = S / t / 1e9
+    # the same bytes with copy-in and copy-out one after the other: a staged
+    # call at or above this did not overlap its two PCIe directions
+    serial_ms = (S / (pcie["h2d_GB_s"] * 1e9) + S / (pcie["d2h_GB_s"] * 1e9)) * 1e3
     return {"bytes_per_pe": S, "calls": k, "ms_per_call": round(t * 1e3, 3), "value": round(npes * S / t / GIB, 2),
             "unit": "GiB/s", "GB_s_per_pe": round(gbs, 1), "schedule": info["schedule"], "pcie": pcie,
+            "serial_copies_ms": round(serial_ms, 3), "overlap": round(serial_ms / (t * 1e3), 3),
             "pcie_frac": round(gbs / pcie["both_GB_s_each_direction"], 4), "check": ck,
             "note": "source and target in shmem_malloc's page-locked host arrays (the reference's heap is host "
                     "memory): each call stages S in over PCIe, reduces and stages S out; the headline value is "
@@ -505,6 +510,210 @@ def offset_target_leg(shm, S, me, npes, src, k, check):
     if rec.get("traffic"):
         rec["traffic_over_alg"] = round(rec["traffic"] / alg, 4)
     return rec
+
+
+def full_check(shm, dst, n, op, dtype, gen, npes, me, host=False, chunk=1 << 22):
+    """Every element of this PE's target against the oracle's result for this
+    PE (oracle.reduce_pe(..., me): the reference's fold order for member me,
+    reduce-op.c:226-264) on the sources regenerated from their generator, in
+    chunks; SHA-256 of the target and of the expected array over the same
+    bytes. Returns (mismatched elements, target sha256 hex, expected sha256
+    hex). Run after the timed regions."""
+    import hashlib
+    from concurrent.futures import ThreadPoolExecutor
+    import oracle
+    es = np.dtype(shmem_reduce.NP[dtype]).itemsize
+    hg, hw = hashlib.sha256(), hashlib.sha256()
+    bad = 0
+    local = max(1, int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))))
+    threads = max(1, min(8, npes, (os.cpu_count() or 8) // local))
+    with ThreadPoolExecutor(threads) as ex:
+        for b in range(0, n, chunk):
+            m = min(chunk, n - b)
+            idx = np.arange(b, b + m, dtype=np.uint64)
+            srcs = list(ex.map(lambda p: gen(p, idx), range(npes)))
+            want = oracle.reduce_pe(op, dtype, srcs, me)
+            if host:
+                import ctypes
+                got = np.empty(m, dtype=want.dtype)
+                ctypes.memmove(got.ctypes.data, dst + b * es, m * es)
+            else:
+                got = shm.get(dst + b * es, m, dtype)
+            gb, wb = got.view(np.uint8), want.view(np.uint8)
+            hg.update(gb)
+            hw.update(wb)
+            bad += int((gb != wb).reshape(m, es).any(axis=1).sum())
+    return bad, hg.hexdigest(), hw.hexdigest()
+
+
+def full_check_record(shm, npes, me, bad, hg, hw, max_over_pes):
+    """Job-wide verdict of full_check: mismatches summed over PEs (each PE's
+    own count, max-reduced so that every PE learns the worst), and whether
+    every PE's target hashed to its expected array's SHA-256."""
+    worst = int(max_over_pes(bad))
+    hash_bad = int(max_over_pes(0 if hg == hw else 1))
+    ok = worst == 0 and hash_bad == 0
+    return ("bit-exact, every element, every PE (SHA-256 of each PE's target = that of the oracle's result for "
+            "that PE)" if ok else "MISMATCH: %d elements on the worst PE, %s" %
+            (worst, "hashes differ" if hash_bad else "hashes equal")), hg[:16]
+
+
+def xgmi_ceiling_leg(shm, S, me, npes, src, buf, reps=20):
+    """N > 1, one GPU per PE: what this GPU can pull from all N-1 peers at
+    once -- the all-gather leg's exact pattern (reduce.c gather_segments:
+    every PE copies shard q of peer q's array into its own buffer, all PEs
+    together), measured two ways on the same peer mappings
+    (shmemx_peer_device_ptr): the library's copy kernel (mi355_copy_segments,
+    one launch of N-1 segments, HIP event pair per launch) and the copy
+    engines (hipMemcpyAsync device-to-device from each peer's mapping, one
+    stream per peer, wall clock). GB/s into this GPU = (N-1) shard bytes /
+    time; each figure the minimum over PEs (the slowest GPU's ingress). This
+    is the measured ceiling the N > 1 roofline's link constants stand beside."""
+    import ctypes
+    L, vp = shm.lib, ctypes.c_void_p
+    shard = (S // npes) // 256 * 256
+    peers = [q for q in range(npes) if q != me]
+    psrc = [shm.peer_device_ptr(src, q) for q in peers]
+    if any(not p for p in psrc):
+        raise RuntimeError("a peer's device heap is not mapped here")
+    dsts = (vp * len(peers))(*[buf + q * shard for q in peers])
+    sps = (vp * len(peers))(*[p + q * shard for p, q in zip(psrc, peers)])
+    nbs = (ctypes.c_size_t * len(peers))(*[shard] * len(peers))
+    L.mi355_time_next_launch.argtypes = [vp, vp]
+    L.mi355_time_next_launch.restype = None
+    L.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), vp, vp]
+    ev = [vp() for _ in range(2 * reps)]
+    for e in ev:
+        L.hipEventCreate(ctypes.byref(e))
+    if L.mi355_copy_segments(dsts, sps, nbs, len(peers), None) != 0:
+        raise RuntimeError("mi355_copy_segments failed")
+    shm.sync()
+    shm.barrier_all()
+    t0 = time.perf_counter()
+    for r in range(reps):
+        L.mi355_time_next_launch(ev[2 * r], ev[2 * r + 1])
+        if L.mi355_copy_segments(dsts, sps, nbs, len(peers), None) != 0:
+            raise RuntimeError("mi355_copy_segments failed")
+    shm.sync()
+    t_wall_k = (time.perf_counter() - t0) / reps
+    ts = []
+    for r in range(reps):
+        ms = ctypes.c_float()
+        L.hipEventElapsedTime(ctypes.byref(ms), ev[2 * r], ev[2 * r + 1])
+        ts.append(ms.value * 1e-3)
+    for e in ev:
+        L.hipEventDestroy(e)
+    t_k = float(np.mean(ts))
+    # the copy engines: one stream per peer, all at once
+    L.hipMemcpyAsync.argtypes = [vp, vp, ctypes.c_size_t, ctypes.c_int, vp]
+    L.hipStreamSynchronize.argtypes = [vp]
+    L.hipStreamCreate.argtypes = [ctypes.POINTER(vp)]
+    L.hipStreamDestroy.argtypes = [vp]
+    st = [vp() for _ in peers]
+    for x in st:
+        L.hipStreamCreate(ctypes.byref(x))
+
+    def sdma_round():
+        for i in range(len(peers)):
+            if L.hipMemcpyAsync(vp(dsts[i]), vp(sps[i]), shard, 3, st[i]) != 0:
+                raise RuntimeError("hipMemcpyAsync from a peer mapping failed")
+    sdma_round()
+    for x in st:
+        L.hipStreamSynchronize(x)
+    shm.barrier_all()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sdma_round()
+    for x in st:
+        L.hipStreamSynchronize(x)
+    t_s = (time.perf_counter() - t0) / reps
+    for x in st:
+        L.hipStreamDestroy(x)
+    # every segment landed (the last copy engine round): spot-check against the source's generator
+    idx = np.arange(0, shard // 8, max(1, shard // 8 // 4096), dtype=np.uint64)
+    bad = 0
+    for q in peers:
+        got = shm.get(buf + q * shard + 0, shard // 8, "double")[idx.astype(np.int64)]
+        want = synth(q, idx + np.uint64(q * shard // 8))
+        bad += int((got.view(np.uint64) != want.view(np.uint64)).sum())
+    ingress = (npes - 1) * shard
+    return {"bytes_into_each_pe": ingress, "shard_bytes": shard, "reps": reps,
+            "kernel": "mi355_copy_segments (%d segments, one launch)" % len(peers),
+            "kernel_avg_us": t_k * 1e6, "kernel_wall_us": t_wall_k * 1e6,
+            "kernel_GB_s": ingress / t_k / 1e9, "sdma_us": t_s * 1e6, "sdma_GB_s": ingress / t_s / 1e9,
+            "bad": bad}
+
+
+def peer_fold_shapes_leg(shm, S, me, npes, src, out, reps=10):
+    """N = 4 or 8, one GPU per PE: the every-member fold of config 3's shard
+    (N sources of S/N bytes, N-1 of them on peers) at the library's launch
+    shape (mi355_combine_orders) and at the other shapes of
+    tools/libpeershapes.so (the same kernel template, other vectors per lane /
+    blocks per CU), all PEs at once, HIP event pair per launch; every
+    variant's N outputs compared byte for byte with the library's. The
+    library's shape was tuned with every source in local HBM; this says
+    whether xGMI's latency wants another one."""
+    import ctypes
+    import hashlib
+    L, vp = shm.lib, ctypes.c_void_p
+    P = ctypes.CDLL(os.path.join(ROOT, "tools", "libpeershapes.so"))
+    P.peer_shapes_orders_double_sum.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp),
+                                                ctypes.c_size_t, vp, vp, vp]
+    L.mi355_time_next_launch.argtypes = [vp, vp]
+    L.hipEventElapsedTime.argtypes = [ctypes.POINTER(ctypes.c_float), vp, vp]
+    lo, hi = shmem_reduce.shard_bounds(L, S // 8, 8, npes, me)
+    n = (hi - lo) // 2 * 2
+    shard_b = n * 8
+    slot = (shard_b + 255) // 256 * 256 + 256 + 4096   # the library's version-slot spacing (reduce.c ver_slot_bytes)
+    srcs = [(shm.peer_device_ptr(src, q) or 0) + lo * 8 for q in range(npes)]
+    if any(s == lo * 8 for s in srcs):
+        raise RuntimeError("a peer's device heap is not mapped here")
+    outs = [out + q * slot for q in range(npes)]
+    D = (vp * npes)(*outs)
+    Sx = (vp * npes)(*srcs)
+    ev = [vp() for _ in range(2 * reps)]
+    for e in ev:
+        L.hipEventCreate(ctypes.byref(e))
+
+    def timed(launch):
+        assert launch(None, None) == 0
+        shm.sync()
+        shm.barrier_all()
+        for r in range(reps):
+            assert launch(ev[2 * r], ev[2 * r + 1]) == 0
+        shm.sync()
+        ts = []
+        for r in range(reps):
+            ms = ctypes.c_float()
+            L.hipEventElapsedTime(ctypes.byref(ms), ev[2 * r], ev[2 * r + 1])
+            ts.append(ms.value * 1e-3)
+        h = hashlib.sha256()
+        for o in outs:
+            h.update(shm.get(o, n, "double").view(np.uint8))
+        return float(np.mean(ts)), h.hexdigest()
+
+    def lib_launch(e0, e1):
+        if e0 is not None:
+            L.mi355_time_next_launch(e0, e1)
+        return shm.combine_orders("sum", "double", outs, srcs, n)
+
+    t_lib, h_lib = timed(lib_launch)
+    alg = 2 * npes * shard_b
+    remote = (npes - 1) * shard_b
+    rows = [{"shape": "library (mi355_combine_orders)", "kernel_avg_us": round(t_lib * 1e6, 2),
+             "remote_read_GB_s": round(remote / t_lib / 1e9, 1), "hbm_frac": round(alg / t_lib / 1e9 / HBM_PEAK_GBS, 4),
+             "same_outputs": True}]
+    u, b = ctypes.c_int(), ctypes.c_int()
+    for v in range(P.peer_shapes_count()):
+        P.peer_shapes_describe(v, ctypes.byref(u), ctypes.byref(b))
+        t, h = timed(lambda e0, e1, v=v: P.peer_shapes_orders_double_sum(v, npes, D, Sx, n, e0, e1, None))
+        rows.append({"shape": f"{u.value} vectors/lane, {b.value} blocks/CU", "kernel_avg_us": round(t * 1e6, 2),
+                     "remote_read_GB_s": round(remote / t / 1e9, 1), "hbm_frac": round(alg / t / 1e9 / HBM_PEAK_GBS, 4),
+                     "same_outputs": h == h_lib})
+    for e in ev:
+        L.hipEventDestroy(e)
+    return {"kernel": "combine_orders_vec<sum,double,%d>" % npes, "sources": npes, "peer_sources": npes - 1,
+            "bytes_per_source": shard_b, "reps": reps, "rows": rows}
 
 
 # ---------------------------------------------------------------------------
@@ -842,7 +1051,7 @@ def main():
     fused = fused_p = None
     if world == 1 and not args.no_fused and not args.host:
         with timed_leg("fused_same_gpu"):
-            fused = fused_same_gpu(2, 4096 if args.no_small is False else 512)
+            fused = fused_same_gpu(2, 4096 if args.no_small is False else 512, config1=True)
         with timed_leg("fused_same_gpu_persistent"):
             fused_p = fused_same_gpu(2, 4096 if args.no_small is False else 512, persistent=True)
     t_init0 = time.perf_counter()
@@ -851,8 +1060,8 @@ def main():
     # leg's target (freed before the rotating leg allocates)
     pairs = ROT_PAIRS if world == 1 and not args.host and not args.no_rotating else 1
     heap = 2 * S * pairs
-    if world == 1 and not args.host:
-        heap = max(heap, 3 * S)
+    if not args.host:
+        heap = max(heap, 3 * S)   # N = 1: the offset leg's target; N > 1: peer_fold_shapes' outputs
     os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(heap + (64 << 20)))
     os.environ.setdefault("SHMEM_DEVICE_SCRATCH_SIZE", str(96 << 20))
     # a PE that never arrives ends the bench within two minutes with the
@@ -1163,15 +1372,15 @@ def main():
 
     # correctness of the last result on a sample: every PE holds the
     # reference's result for itself (own source first, then ascending)
-    check = "skipped"
-    if not args.no_check:
+    check, check_sha = "skipped", None
+    if not args.no_check and not rccl_fallback:
+        # every element of every PE's target against the oracle's result for
+        # that PE (a stale line from a peer would not hide in a sample)
+        bad, hg, hw = full_check(shm, dst, n, "sum", "double", synth, npes, me, host=args.host)
+        check, check_sha = full_check_record(shm, npes, me, bad, hg, hw, max_over_pes)
+    elif not args.no_check:
         idx = np.unique(np.random.default_rng(me).integers(0, n, 1 << 16).astype(np.uint64))
-        if args.host:
-            import ctypes
-            got_full = np.empty(n)
-            ctypes.memmove(got_full.ctypes.data, dst, S)
-        else:
-            got_full = shm.get(dst, n, "double")
+        got_full = shm.get(dst, n, "double")
         got = got_full[idx.astype(np.int64)]
         import oracle
         srcs = [synth(p, idx) for p in range(npes)]
@@ -1183,13 +1392,60 @@ def main():
             check = ("RCCL fallback (peer heap reads failed the init self-test): within 2(N-1)u sum|x| of the "
                      "reference's per-PE result on every PE, %d samples each" % len(idx) if bad == 0
                      else "MISMATCH %d of %d samples beyond the FP bound (worst PE)" % (bad, len(idx)))
-        else:
-            bad = int((got.view(np.uint64) != want.view(np.uint64)).sum())
-            bad = int(max_over_pes(bad))
-            check = "bit-exact vs the reference's per-PE order on every PE, %d samples each" % len(idx) if bad == 0 \
-                else "MISMATCH %d of %d samples (worst PE)" % (bad, len(idx))
         del got_full
     legs_s["check"] = round(time.perf_counter() - t_check0, 2)
+
+    # N > 1, one GPU per PE: the measured xGMI ceiling (all peers at once,
+    # the all-gather's pattern) and the every-member fold's launch shapes
+    # with N-1 remote sources; before op_coverage rewrites the sources
+    xgmi_ceiling = peer_shapes = None
+    if npes > 1 and not args.host:
+        na = {"not_applicable": "the PEs share a GPU: peer reads are this GPU's own HBM, no link is involved"}
+        if shared_gpu:
+            xgmi_ceiling, peer_shapes = dict(na), dict(na)
+        elif rccl_fallback:
+            xgmi_ceiling = peer_shapes = {"not_applicable": "peer heap reads failed the init self-test"}
+        else:
+            with timed_leg("xgmi_ceiling", optional=solo):
+                xc = xgmi_ceiling_leg(shm, S, me, npes, src, dst)
+                xgmi_ceiling = {k: v for k, v in xc.items() if k not in ("kernel_avg_us", "kernel_GB_s", "sdma_us",
+                                                                         "sdma_GB_s", "bad", "kernel_wall_us")}
+                slow_k = max_over_pes(xc["kernel_avg_us"])
+                slow_s = max_over_pes(xc["sdma_us"])
+                xgmi_ceiling.update({
+                    "kernel_avg_us": round(slow_k, 2), "kernel_GB_s_into_each_pe": round(xc["bytes_into_each_pe"] / slow_k / 1e3, 1),
+                    "sdma_us": round(slow_s, 2), "sdma_GB_s_into_each_pe": round(xc["bytes_into_each_pe"] / slow_s / 1e3, 1),
+                    "check": "bit-exact (sampled, every peer's segment)" if int(max_over_pes(xc["bad"])) == 0
+                    else "MISMATCH",
+                    "note": "every PE pulls shard q of peer q's array from all N-1 peers at once (the all-gather's "
+                            "pattern) through the peer mappings: the library's copy kernel and the copy engines; "
+                            "GB/s into each GPU, slowest PE"})
+                xgmi_ceiling["peak_measured_GB_s"] = max(xgmi_ceiling["kernel_GB_s_into_each_pe"],
+                                                         xgmi_ceiling["sdma_GB_s_into_each_pe"])
+            if npes in (4, 8):
+                with timed_leg("peer_fold_shapes", optional=solo):
+                    out_buf = shm.malloc_device(S + npes * 8192)
+                    if not out_buf:
+                        raise RuntimeError("no room in the device heap for the peer fold's outputs")
+                    try:
+                        peer_shapes = peer_fold_shapes_leg(shm, S, me, npes, src, out_buf)
+                    finally:
+                        shm.free_device(out_buf)
+                    for r in peer_shapes["rows"]:
+                        r["kernel_avg_us"] = round(max_over_pes(r["kernel_avg_us"]), 2)
+                        r["remote_read_GB_s"] = round(peer_shapes["bytes_per_source"] * (npes - 1)
+                                                      / r["kernel_avg_us"] / 1e3, 1)
+                        r["hbm_frac"] = round(2 * npes * peer_shapes["bytes_per_source"] / r["kernel_avg_us"] / 1e3
+                                              / HBM_PEAK_GBS, 4)
+                        r["same_outputs"] = int(max_over_pes(0 if r["same_outputs"] else 1)) == 0
+                    best = min(peer_shapes["rows"], key=lambda r: r["kernel_avg_us"])
+                    peer_shapes["fastest"] = best["shape"]
+                    peer_shapes["note"] = ("config 3's every-member fold with N-1 sources on peers, at the library's "
+                                           "launch shape and at tools/libpeershapes.so's (same kernel template), all "
+                                           "PEs at once; kernel_avg_us max over PEs; same_outputs: every output equal "
+                                           "to the library's on every PE")
+            else:
+                peer_shapes = {"not_applicable": "the shape variants are 4- and 8-source folds (N = %d)" % npes}
 
     # N = 1: north_star's host-memory rate -- the same call on shmem_malloc's
     # page-locked host arrays, staged over PCIe inside each call, with the
@@ -1236,18 +1492,38 @@ def main():
                 shm.sync()
                 t_op = max_over_pes(time.perf_counter() - to0) / k
                 shm.barrier_all()
-                ck = "skipped"
+                ck, sha = "skipped", None
                 if not args.no_check:
-                    idx = np.unique(np.random.default_rng(100 + me).integers(0, no, 1 << 14)).astype(np.uint64)
-                    got = shm.get(dst, no, dtype)[idx.astype(np.int64)]
-                    want = oracle.reduce_pe(op, dtype, [gen(p, idx) for p in range(npes)], me)
-                    bad = int(max_over_pes(int((got.view(np.uint8) != want.view(np.uint8)).sum())))
-                    ck = "bit-exact, %d samples" % len(idx) if bad == 0 else "MISMATCH in %d bytes" % bad
+                    bad, hg, hw = full_check(shm, dst, no, op, dtype, gen, npes, me)
+                    ck, sha = full_check_record(shm, npes, me, bad, hg, hw, max_over_pes)
                 ops[name] = {"bytes_per_pe": ob, "steps": k, "us_per_call": round(t_op * 1e6, 2),
                              "value": round(npes * ob / t_op / GIB, 2), "per_pe_gib_s": round(ob / t_op / GIB, 2),
-                             "check": ck}
+                             "check": ck, "target_sha256_pe0": sha}
             ops["note"] = ("BASELINE config 4 (op coverage): shmem_float_max_to_all and shmem_longlong_and_to_all, "
                            "64 MiB per PE, GiB/s reduced whole job; longlong words with bits 1 at p = 7/8")
+
+    # BASELINE config 1's call through the library (2 PEs, 4 KiB int sum, host
+    # and device heap): at N = 1 from fused_same_gpu's two PE processes, at
+    # N > 1 on PEs 0 and 1 of this job, beside the CPU's figure for the same call
+    config1_call = None
+    if not args.host:
+        with timed_leg("config1_call", optional=solo):
+            if npes > 1:
+                sys.path.insert(0, os.path.join(ROOT, "tools"))
+                import fused_bench
+                config1_call = fused_bench.config1(shm, 4096, max_over_pes)
+                config1_call["layout"] = ("PEs 0 and 1 of this job" +
+                                          (" (sharing one GPU)" if shared_gpu else ", one GPU each"))
+            elif fused and fused.get("config1"):
+                config1_call = dict(fused["config1"], layout="2 PE processes sharing this GPU (fused_same_gpu)")
+            if config1_call is not None:
+                cpu_c1 = (cpu or {}).get("config1", {}).get("us_per_call")
+                config1_call["cpu_us_per_call"] = cpu_c1
+                config1_call["note"] = ("BASELINE config 1's call: shmem_int_sum_to_all, 4 KiB, active set of 2 PEs; "
+                                        "host_heap = shmem_malloc's arrays (host memory, as the reference's heap), "
+                                        "device_heap = shmemx_malloc_device's; us per call entry-to-return, max over "
+                                        "the 2 PEs; cpu_us_per_call = cpu_baseline.config1 (the reference algorithm "
+                                        "on 2 host cores)")
 
     # N > 1: the same call on plain hipMalloc buffers (a framework's tensors,
     # outside the symmetric heap: the members map each other's allocations for
@@ -1340,14 +1616,18 @@ def main():
                     "call": sched}
         if rotating and "frac" in rotating:
             # which figure is HBM: the timed region re-reads one pair, the
-            # rotating leg streams every byte from HBM
-            roofline["hbm_only"] = {k: rotating[k] for k in ("kernel_avg_us", "achieved_GB_s", "frac",
-                                                             "footprint_MiB", "launches_timed")}
+            # rotating leg streams every byte from HBM. Scalar keys: the
+            # driver's record of the line keeps no nested objects.
+            roofline.update({"hbm_only_frac": rotating["frac"], "hbm_only_kernel_avg_us": rotating["kernel_avg_us"],
+                             "hbm_only_achieved": rotating["achieved_GB_s"],
+                             "hbm_only_footprint_MiB": rotating["footprint_MiB"],
+                             "hbm_only_launches_timed": rotating["launches_timed"]})
             roofline["attribution"] = (
                 "frac is the timed region's: the same 256 MiB source/target pair every call (512 MiB per call), "
                 "part of which the 256 MiB Infinity Cache serves, so it is a device-memory rate, not HBM alone; "
-                "hbm_only is the same kernel over %d disjoint pairs taken in turn (headline_rotating, %d MiB "
+                "hbm_only_* is the same kernel over %d disjoint pairs taken in turn (headline_rotating, %d MiB "
                 "footprint): every byte from HBM" % (ROT_PAIRS, rotating["footprint_MiB"]))
+        roofline.update({"call_schedule": sched["schedule"], "call_launches": sched["launches_per_call"]})
     else:
         # N > 1: the reduce-scatter fold reads N-1 of its N shard sources from
         # peers over xGMI, so its bound is the links into this GPU: achieved =
@@ -1359,13 +1639,23 @@ def main():
         hbm_gbs = alg_bytes / kt_s / 1e9 if k_avg_ms > 0 else 0.0
         if rccl_fallback:
             kname = "ncclAllReduce (RCCL fallback: P2P self-test failed; the whole exchange, not one leg)"
+        measured = (xgmi_ceiling or {}).get("peak_measured_GB_s")
+        # a bound that this run's own pull exceeds is no bound: take the measured ceiling
+        peak_source = "(N-1) x 153 GB/s"
+        if measured and measured > peak:
+            peak, peak_source = measured, "measured (xgmi_ceiling): above (N-1) x 153 GB/s"
         roofline = {"bound": "xgmi", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
                     "frac": round(achieved / peak, 4), "traffic": None, "kernel": kname,
                     "alg_bytes_per_launch": remote // launches, "kernel_avg_us": round(k_avg_ms * 1e3, 2),
                     "launches_timed": nk, "ms_per_step_with_events": round(t_local_ev / args.steps * 1e3, 4),
                     "call": sched,
                     "peak_note": "(N-1) links x 153 GB/s into this GPU (SURVEY 8d); if 153.6 GB/s counts both "
-                                 "directions the one-way bound is half: see xgmi.frac_one_direction",
+                                 "directions the one-way bound is half: see xgmi.frac_one_direction; "
+                                 "peak_measured_GB_s = this run's all-peers pull ceiling (xgmi_ceiling)",
+                    "peak_measured_GB_s": measured, "peak_source": peak_source,
+                    "frac_of_measured": round(achieved / measured, 4) if measured and achieved <= measured else None,
+                    "call_schedule": sched["schedule"], "call_launches": sched["launches_per_call"],
+                    "hbm_frac": round(hbm_gbs / HBM_PEAK_GBS, 4),
                     "hbm": {"bytes_per_launch": alg_bytes // launches, "achieved": round(hbm_gbs, 1),
                             "peak": HBM_PEAK_GBS, "frac": round(hbm_gbs / HBM_PEAK_GBS, 4),
                             "note": "the same fold counted as local HBM traffic: its %d shard sources read + %d "
@@ -1382,21 +1672,22 @@ def main():
             # call's first entry and its last return, so this is a lower
             # bound on the rate the folds achieved together (<= 1 of HBM by
             # construction). One launch's own rate is kept as per_launch_*.
-            xv = {k: roofline.pop(k) for k in ("bound", "achieved", "peak", "frac", "alg_bytes_per_launch",
-                                               "peak_note")}
+            for k in ("bound", "achieved", "peak", "frac", "alg_bytes_per_launch", "peak_note", "peak_measured_GB_s",
+                      "frac_of_measured", "peak_source"):
+                roofline.pop(k)
             h = roofline.pop("hbm")
             dev = pes_on_gpu * alg_bytes / t_step / 1e9
             roofline = {"bound": "hbm", "achieved": round(dev, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(dev / HBM_PEAK_GBS, 4), "traffic": None,
                         "alg_bytes_per_launch": h["bytes_per_launch"], "pes_on_gpu": pes_on_gpu,
                         "per_launch_achieved": h["achieved"], "per_launch_frac": h["frac"],
-                        **roofline, "hbm_note": h["note"], "xgmi_view": xv,
+                        **roofline, "hbm_note": h["note"], "xgmi_view": None,
+                        "xgmi_view_note": "not applicable: the PEs share a GPU, no link carries the peer reads",
                         "note": "the PEs share ONE GPU (test layout): every 'remote' read is this GPU's own HBM, "
                                 "so the fold is HBM-bound here; achieved = %d PEs x one call's fold bytes / the "
                                 "call's wall time (max over PEs), a window holding every PE's launches: a lower "
                                 "bound on their combined rate; per_launch_* = one launch's bytes over its own "
-                                "duration; xgmi_view is what the line reports with one GPU per PE (not a link "
-                                "rate here)" % pes_on_gpu}
+                                "duration; with one GPU per PE the line reports the link view instead" % pes_on_gpu}
     roofline["traffic_note"] = traffic_for(roofline, f"n{npes}_{args.mib}mib", args.host)
 
     # N > 1: bus bandwidth of the reduce-scatter + all-gather exchange against
@@ -1417,7 +1708,16 @@ def main():
                 "ag_kernel_remote_read_GB_s": round((npes - 1) / npes * S / (ag_avg_ms * 1e-3) / 1e9, 1)
                 if nag and ag_avg_ms > 0 else None,
                 "note": "busbw = 2(N-1)/N * S / t_step = bytes each PE receives over xGMI per second; "
-                        "bound = (N-1) links x 153 GB/s (SURVEY 8d), or x 76.8 GB/s if 153.6 is both directions"}
+                        "bound = (N-1) links x 153 GB/s (SURVEY 8d), or x 76.8 GB/s if 153.6 is both directions; "
+                        "peak_measured = this run's all-peers pull ceiling (xgmi_ceiling)"}
+        pm = (xgmi_ceiling or {}).get("peak_measured_GB_s")
+        xgmi["peak_measured_GB_s"] = pm
+        xgmi["frac_of_measured"] = round(busbw / pm, 4) if pm and busbw <= pm else None
+        # a constant bound below what this run moved is refuted, not exceeded
+        for k, b in (("frac", bound), ("frac_one_direction", bound_dir)):
+            if xgmi[k] is not None and xgmi[k] > 1:
+                xgmi[k] = None
+                xgmi[k + "_refuted"] = "busbw %.1f GB/s exceeds this bound (%.1f GB/s)" % (busbw, b)
         import ctypes
         lt, hp = ctypes.c_int(), ctypes.c_int()
         links = {}
@@ -1426,8 +1726,11 @@ def main():
                 links[str(q)] = {"type": {4: "xgmi", 2: "pcie"}.get(lt.value, str(lt.value)), "hops": hp.value}
         xgmi["links_from_pe0"] = links or None
         if shared_gpu:
+            # no link: a fraction of a link bound would be meaningless (> 1)
+            for k in ("frac", "frac_one_direction", "frac_of_measured"):
+                xgmi[k] = None
             xgmi["note"] = ("the PEs share ONE GPU (test layout): peer 'xGMI' reads are local HBM reads, so "
-                            "these figures are not xGMI rates")
+                            "these figures are not xGMI rates and no link fraction is given")
 
     if me == 0:
         out = {
@@ -1472,7 +1775,11 @@ def main():
             "small_call_graph": small_graph,
             "coherence_selftest": coherence,
             "check": check,
+            "target_sha256_pe0": check_sha,
+            "xgmi_ceiling": xgmi_ceiling,
+            "peer_fold_shapes": peer_shapes,
             "op_coverage": ops,
+            "config1_call": config1_call,
             "external_buffers": external,
             "link_probe": link_probe,
             "kernels": kernels,

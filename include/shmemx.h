@@ -24,6 +24,11 @@ void *shmemx_malloc_device (size_t size);
 void shmemx_free_device (void *ptr);
 /* 1 if ptr lies in this PE's device symmetric heap. */
 int shmemx_is_device_symmetric (const void *ptr);
+/* PE pe's copy of the device-heap object at ptr as an address kernels on this
+ * PE's GPU can load from and store to (an IPC mapping of pe's heap; xGMI
+ * traffic when pe is on another GPU); NULL if ptr is not in the device heap or
+ * pe's heap is not mapped. Not dereferenceable by the host. */
+void *shmemx_peer_device_ptr (const void *ptr, int pe);
 
 /* Device buffers outside the heap (hipMalloc, a framework's tensors) as
  * *_to_all target/source with PE_size > 1: the members export the

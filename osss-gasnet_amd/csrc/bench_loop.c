@@ -67,3 +67,11 @@ void shmemb_longlong_and_loop (long long *target, long long *source, int nreduce
     for (int i = 0; i < iters; ++i)
         shmem_longlong_and_to_all (target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync);
 }
+
+/* BASELINE config 1's call: shmem_int_sum_to_all (4 KiB at 2 PEs) */
+void shmemb_int_sum_loop (int *target, int *source, int nreduce, int PE_start, int logPE_stride, int PE_size,
+                          int *pWrk, long *pSync, int iters)
+{
+    for (int i = 0; i < iters; ++i)
+        shmem_int_sum_to_all (target, source, nreduce, PE_start, logPE_stride, PE_size, pWrk, pSync);
+}

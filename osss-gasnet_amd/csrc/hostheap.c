@@ -163,14 +163,24 @@ void *shmemi_host_malloc (size_t size)
             break;
         off = (*pp)->off + (*pp)->size;
     }
-    if (need > shmemi.hheap_size - off)
-        shmemi_fatal ("shmem_malloc(%zu): the symmetric host heap (%zu bytes) has no room left "
-                      "(set SHMEM_SYMMETRIC_HEAP_SIZE)", size, shmemi.hheap_size);
+    /* No room, or no pages to commit: NULL, as the reference's shmalloc
+     * (symmem.c:150-153: a NOTICE trace, malloc_error set, the caller's
+     * barrier still entered by pshmem_malloc). Every PE sees the same
+     * exhaustion (same call sequence, same heap size); a full /dev/shm is
+     * this PE's alone, and its caller's NULL check is the reference's. */
+    if (need > shmemi.hheap_size - off) {
+        SHMEMI_TRACE (SHMEMI_LOG_NOTICE, "shmem_malloc(%zu) failed: the symmetric host heap (%zu bytes) has no room "
+                                         "left (SHMEM_SYMMETRIC_HEAP_SIZE)", size, shmemi.hheap_size);
+        return NULL;
+    }
     if (shmemi.hheap_fd >= 0) {
         const int e = posix_fallocate (shmemi.hheap_fd, (off_t) off, (off_t) need);
-        if (e != 0)
-            shmemi_fatal ("shmem_malloc(%zu): committing the symmetric host heap's pages failed: %s "
-                          "(is /dev/shm full?)", size, strerror (e));
+        if (e != 0) {
+            SHMEMI_TRACE (SHMEMI_LOG_NOTICE, "shmem_malloc(%zu) failed: committing the symmetric host heap's pages: "
+                                             "%s (is /dev/shm full?)", size, strerror (e));
+            release_pages (off, need); /* whatever part was committed */
+            return NULL;
+        }
     }
     struct shmemi_hostblk *h = (struct shmemi_hostblk *) calloc (1, sizeof *h);
     if (h == NULL)

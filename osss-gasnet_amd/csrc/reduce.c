@@ -322,6 +322,16 @@ void shmemi_dev_barrier (int PE_start, int stride, int PE_size, int me, int last
  * same collective calls) -- whose parity picks the NaN word the owner's fold
  * sets (MI355_SIG_NANFLAG_AT; it clears the other parity's, which the previous
  * call's gather has finished reading) and the other member's gather reads. */
+/* nan_pair's NaN word can carry the owner's "no NaN" to the other member:
+ * the owner's signal region is mapped there and peers' stores into signal
+ * regions were seen at init (without that, sig_broken: host barriers, and the
+ * gather patches unconditionally). */
+static int nan_word_ok (const struct aset *s)
+{
+    const int other_pe = aset_pe (s, 1 - s->me);
+    return !shmemi.sig_broken && shmemi.sigmem != NULL && shmemi.peer_sig[other_pe] != NULL;
+}
+
 static long long pair_next (int chan, const struct aset *s)
 {
     if (shmemi.pair_calls == NULL) {
@@ -340,8 +350,19 @@ static int fold_shard (int op, int dtype, size_t es, size_t dst_off, size_t src_
                                                                        : MI355_ORDERS_MAX_SOURCES];
     size_t lo, hi;
     mi355_shard_bounds (n, es, s->size, s->me, &lo, &hi);
-    if (hi <= lo)
+    if (hi <= lo) {
+        /* no fold: clear the word the next call's fold would have (this
+         * call's stays as the previous call of its parity left it, but the
+         * other member's gather of an empty shard reads nothing) */
+        if (pair && nan_word_ok (s)) {
+            const int other = aset_pe (s, 1 - s->me);
+            const hipError_t e = hipMemsetAsync (shmemi.sigmem + MI355_SIG_NANFLAG_AT (chan, (pair_k + 1) & 1, other),
+                                                 0, sizeof (unsigned long long), st);
+            if (e != hipSuccess)
+                return (int) e;
+        }
         return 0;
+    }
     const void **spp = sp;
     if (s->size > (int) (sizeof sp / sizeof sp[0])) {
         spp = (const void **) malloc (sizeof (void *) * (size_t) s->size);
@@ -357,7 +378,7 @@ static int fold_shard (int op, int dtype, size_t es, size_t dst_off, size_t src_
     }
     void *dst = shmemi_peer_ptr (shmemi.mype, dst_off + lo * es);
     int rc;
-    if (pair) {
+    if (pair && nan_word_ok (s)) {
         const int other = aset_pe (s, 1 - s->me);
         mi355_nan_flag_next_launch (shmemi.sigmem + MI355_SIG_NANFLAG_AT (chan, pair_k & 1, other),
                                     shmemi.sigmem + MI355_SIG_NANFLAG_AT (chan, (pair_k + 1) & 1, other));
@@ -413,7 +434,9 @@ static int pair_gather (int dtype, size_t es, size_t dst_off, size_t src_off, si
     return mi355_nan_patch_copy (dtype, shmemi_peer_ptr (shmemi.mype, dst_off + l * es),
                                  shmemi_peer_ptr (other_pe, dst_off + l * es),
                                  shmemi_peer_ptr (shmemi.mype, src_off + l * es), h > l ? h - l : 0,
-                                 shmemi.peer_sig[other_pe] + MI355_SIG_NANFLAG_AT (chan, pair_k & 1, shmemi.mype),
+                                 nan_word_ok (s) ? shmemi.peer_sig[other_pe] +
+                                                       MI355_SIG_NANFLAG_AT (chan, pair_k & 1, shmemi.mype)
+                                                 : NULL, /* no word: always patch */
                                  st);
 }
 
@@ -504,6 +527,10 @@ static void p2p_range (int op, int dtype, size_t es, size_t dst_off, size_t src_
             shmemi_fatal ("combine kernel launch failed (op %d, dtype %d, %d sources, %zu elements): %d", op,
                           dtype, s->size, n, rc);
         shmemi_wait_signal ();
+    } else if (pair) { /* an empty shard: fold_shard only clears the next call's NaN word */
+        const int rc = fold_shard (op, dtype, es, dst_off, src_off, n, s, ordered, pk, SHMEMI_CHAN_HOST, shmemi.stream);
+        if (rc != 0)
+            shmemi_fatal ("NaN word clear failed: %d", rc);
     }
     shmemi_barrier_set (s->start, s->stride, s->size); /* every shard is reduced */
     shmemi_peer_acquire (shmemi.stream);

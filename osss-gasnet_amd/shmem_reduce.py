@@ -60,7 +60,7 @@ def load(path=LIB_PATH):
         "shmem_global_exit": ([_i], None),
         "shmemx_barrier_on_stream": ([_i, _i, _i, _vp], None),
         "shmemx_malloc_device": ([_sz], _vp), "shmemx_free_device": ([_vp], None),
-        "shmemx_is_device_symmetric": ([_vp], _i),
+        "shmemx_is_device_symmetric": ([_vp], _i), "shmemx_peer_device_ptr": ([_vp, _i], _vp),
         "shmemx_set_reduce_algorithm": ([_i], _i), "shmemx_get_reduce_algorithm": ([], _i),
         "shmemx_set_reduce_order": ([_i], _i), "shmemx_get_reduce_order": ([], _i),
         "shmemx_set_persistent": ([_i], _i),
@@ -131,6 +131,11 @@ class Shmem:
 
     def free_device(self, ptr):
         self.lib.shmemx_free_device(ptr)
+
+    def peer_device_ptr(self, ptr, pe):
+        """PE pe's copy of a device-heap object, addressable by kernels on
+        this PE's GPU (shmemx_peer_device_ptr); None if not mapped."""
+        return self.lib.shmemx_peer_device_ptr(ptr, pe)
 
     def malloc(self, nbytes):
         return self.lib.shmem_malloc(nbytes)

@@ -154,3 +154,34 @@ def test_get_put_with_null_buffer_name_it(tmp_path):
         assert rc != 0 and "UNREACHABLE" not in out, out
     assert any("shmem_getmem: NULL dest" in out for _, out in res), res
     assert any("shmem_putmem: NULL source" in out or "aborting" in out for _, out in res), res
+
+
+def test_job_above_32_pes(tmp_path):
+    """A job of more PEs than a device barrier holds (MI355_FUSED_MAX_MEMBERS
+    = 32): the bootstrap, host barriers, the symmetric host heap and an
+    fcollect over all 40 PEs. On a GPU such a job skips the init's timed
+    device barrier (runtime.c device_wait_test) and its collectives take the
+    host-barrier schedules (reduce.c device_flags_ok)."""
+    body = """
+    import numpy as np
+    L = shm.lib
+    vp, sz, i = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int
+    L.shmem_fcollect64.argtypes = [vp, vp, sz, i, i, i, vp]
+    L.shmem_getmem.argtypes = [vp, vp, sz, i]
+    psync = (ctypes.c_long * 128)(*([-1] * 128))
+    s = shm.malloc(64); t = shm.malloc(npes * 64)
+    np.ctypeslib.as_array(ctypes.cast(s, ctypes.POINTER(ctypes.c_int64)), shape=(8,))[:] = me * 100 + np.arange(8)
+    shm.barrier_all()
+    L.shmem_fcollect64(t, s, 8, 0, 0, npes, psync)
+    got = np.ctypeslib.as_array(ctypes.cast(t, ctypes.POINTER(ctypes.c_int64)), shape=(npes * 8,)).reshape(npes, 8)
+    assert (got == np.arange(npes)[:, None] * 100 + np.arange(8)).all()
+    out = np.zeros(8, dtype=np.int64)
+    L.shmem_getmem(out.ctypes.data, s, 64, (me + 17) % npes)
+    assert (out == ((me + 17) % npes) * 100 + np.arange(8)).all()
+    shm.barrier_all()
+    print('ok', me)
+    shm.finalize()
+    """
+    res = spawn(40, body, tmp_path, timeout=240)
+    for rc, out in res:
+        assert rc == 0 and "ok" in out, out

@@ -39,7 +39,28 @@ def run(cmd, timeout=240, env=None):
     return json.loads(lines[0])
 
 
+def fractions(d, path=""):
+    """Every roofline fraction the line prints: (path, value) for keys named
+    frac / *_frac / frac_* (the VALU-floor ratio and the PCIe ratio are
+    bounded separately)."""
+    if isinstance(d, dict):
+        for k, v in d.items():
+            p = f"{path}.{k}"
+            if (k == "frac" or k.endswith("_frac") or k.startswith("frac_")) and k not in ("valu_frac", "pcie_frac"):
+                yield p, v
+            else:
+                yield from fractions(v, p)
+    elif isinstance(d, list):
+        for i, v in enumerate(d):
+            yield from fractions(v, f"{path}[{i}]")
+
+
 def common(d, n):
+    # no fraction of a roofline above 1 anywhere in the line (VERDICT r05: a bound the run
+    # exceeded is reported as refuted or not applicable, never as a fraction > 1)
+    fr = list(fractions(d))
+    assert fr and all(v is None or (isinstance(v, (int, float)) and 0 < v <= 1.0) for _, v in fr), \
+        [x for x in fr if x[1] is not None and not 0 < x[1] <= 1.0]
     assert "legs_s" in d and d["legs_s"]["total_before_print"] > 0, d.get("legs_s")
     pc = d["per_call"]
     assert 0 < pc["p10_us"] <= pc["median_us"] <= pc["p90_us"] <= pc["max_us"] and pc["calls"] == d["steps"], pc
@@ -53,13 +74,19 @@ def common(d, n):
     else:
         # N > 1: the reduce-scatter fold's remote reads against the links into the GPU; here
         # (PEs sharing the test GPU) its local-HBM view, the link view kept aside
-        x = r["xgmi_view"]
-        assert x["bound"] == "xgmi" and x["peak"] == (n - 1) * 153.0 and x["achieved"] > 0
-        assert x["alg_bytes_per_launch"] == (n - 1) * (d["config"]["bytes_per_pe"] // n)
+        assert r["xgmi_view"] is None and "not applicable" in r["xgmi_view_note"], r
         assert r["bound"] == "hbm" and r["peak"] == 8000.0 and 0 < r["frac"] <= 1.0
         assert 0 < r["per_launch_frac"] <= 1.0, r
+    # every element of every PE's target, headline and both op-coverage calls
+    assert d["check"].startswith("bit-exact, every element, every PE"), d["check"]
+    assert len(d["target_sha256_pe0"]) == 16, d["target_sha256_pe0"]
     for name in ("float_max", "longlong_and"):
-        assert d["op_coverage"][name]["check"].startswith("bit-exact"), d["op_coverage"]
+        assert d["op_coverage"][name]["check"].startswith("bit-exact, every element, every PE"), d["op_coverage"]
+    # BASELINE config 1's call through the library, host and device heap, beside the CPU's
+    c1 = d["config1_call"]
+    for kind in ("host_heap", "device_heap"):
+        assert c1[kind]["check"].startswith("bit-exact") and c1[kind]["us_per_call"] > 0, c1
+    assert c1["cpu_us_per_call"] is None or c1["cpu_us_per_call"] > 0, c1
     assert d["small_call"]["us_per_call"] > 0
     g = d["small_call_graph"]
     assert g["us_per_call"] > 0 and g["check"].startswith("bit-exact") and g["calls"] == 4096, g
@@ -82,7 +109,8 @@ def test_bench_one_gpu_line():
     # the HBM-only figure: the same call over disjoint pairs taken in turn, >= 2 GiB of footprint
     hr = d["headline_rotating"]
     assert hr["check"].startswith("bit-exact") and hr["footprint_MiB"] >= 2048 and hr["kernel"] == r["kernel"], hr
-    assert 0 < hr["frac"] <= 1.0 and r["hbm_only"]["frac"] == hr["frac"] and "Infinity Cache" in r["attribution"]
+    assert 0 < hr["frac"] <= 1.0 and r["hbm_only_frac"] == hr["frac"] and "Infinity Cache" in r["attribution"]
+    assert r["hbm_only_kernel_avg_us"] == hr["kernel_avg_us"] and r["call_schedule"] == "identity", r
     # a target one element off the source's 16-byte phase: unaligned-load copy, not 8-byte words
     ot = d["headline_offset_target"]
     assert ot["check"].startswith("bit-exact") and ot["kernel"].startswith("void mi355k::copy_segments_shift"), ot
@@ -91,9 +119,11 @@ def test_bench_one_gpu_line():
     assert d["coherence_selftest"] is None
     # north_star's host-memory rate: page-locked host arrays, staged over PCIe in each call
     hs = d["host_staged"]
-    # >= 0.7 of the two-way PCIe rate: copy-in and copy-out overlap (0.55 when
-    # the staging streams shared a hardware queue, runtime.c shmemi_lazy_stream)
-    assert hs["check"].startswith("bit-exact") and hs["value"] > 0 and 0.7 < hs["pcie_frac"] < 1.2, hs
+    # copy-in and copy-out overlap: a staged call takes less than the two
+    # copies one after the other (round 5: 6.2 ms against 9.4; 10.1 ms when the
+    # staging streams shared a hardware queue); the rate itself is reported
+    assert hs["check"].startswith("bit-exact") and hs["value"] > 0 and 0 < hs["pcie_frac"] < 1.2, hs
+    assert hs["ms_per_call"] < 0.9 * hs["serial_copies_ms"] and hs["overlap"] > 1.1, hs
     assert hs["pcie"]["both_GB_s_each_direction"] > 0, hs
     k = d["kernels"]
     for name in ("fold_k2_double_sum", "fold_k8_double_sum", "rs_shard_n8_double_sum", "fold_k8_float_max",
@@ -148,7 +178,7 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
     assert re.fullmatch(r"void mi355k::combine_vec<0, double, 2, \d, \d, false>\(mi355k::CombineParams\)", r["kernel"]), r
     shard = S // 2
     assert r["call"]["schedule"] == "p2p" and r["call"]["sources"] == 2 and r["call"]["outputs"] == 1, r
-    assert r["xgmi_view"]["alg_bytes_per_launch"] == shard and r["alg_bytes_per_launch"] == 3 * shard, r
+    assert r["alg_bytes_per_launch"] == 3 * shard, r
     # both PEs' folds share this GPU's HBM: the device rate counts both PEs' bytes over the call's
     # wall time (a window holding both launches), so it cannot pass the peak
     assert r["pes_on_gpu"] == 2 and 0 < r["frac"] <= 1.0, r
@@ -184,6 +214,10 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
     # every leg's wall time, and no optional leg failed
     assert d["legs_s"]["headline"] > 0 and d["legs_s"]["cpu_baseline"] > 0, d["legs_s"]
     assert not any(isinstance(v, dict) and "error" in v and k != "rccl_compare" for k, v in d.items()), d
+    # the xGMI legs need one GPU per PE: here they say why they did not run
+    assert "not_applicable" in d["xgmi_ceiling"] and "not_applicable" in d["peer_fold_shapes"], d
+    assert d["xgmi"]["frac"] is None and d["xgmi"]["frac_one_direction"] is None, d["xgmi"]
+    assert d["config1_call"]["layout"].startswith("PEs 0 and 1"), d["config1_call"]
     # the same call on plain hipMalloc buffers: mapped by the peers, not staged
     e = d["external_buffers"]
     assert e["schedule"] == "mapped-p2p" and e["check"].startswith("bit-exact") and e["mappings_opened"] >= 1, e

@@ -189,14 +189,11 @@ def test_nan_payload_fixtures_on_every_pe(tmp_path, fused_max, oneshot_max):
                          ctx=f"nan golden {c['op']}/{c['dtype']} case {c['golden']} PE {i}:")
 
 
-@pytest.mark.parametrize("fused_max", ["0", "2M"], ids=["multi-launch", "fused"])
-def test_two_member_calls_alternating_nan_and_finite(tmp_path, fused_max):
-    """The two-member float/double schedule (reduce.c nan_pair): the owner's
-    fold sets a per-call NaN word (parity of the call number with that
-    partner) and the other member patches its gather only when it is set. A
-    sequence on one pair alternating NaN-rich calls (golden_nan rows) and
-    NaN-free ones, in place and not, so each parity's word goes from set to
-    clear and back; every call bit-exact on both PEs."""
+def two_member_nan_sequence(tmp_path, extra_env):
+    """A sequence on one pair alternating NaN-rich calls (golden_nan rows),
+    NaN-free ones and tiny ones whose second shard is empty (no fold on PE 1:
+    it only clears the next call's NaN word), in place and not; every call
+    checked bit-exact on both PEs."""
     cases, cid = [], 0
     for rep in range(2):
         for op in ("sum", "prod"):
@@ -209,7 +206,10 @@ def test_two_member_calls_alternating_nan_and_finite(tmp_path, fused_max):
                     cases.append({"id": cid, "op": op, "dtype": dtype, "n": 70001 + cid, "sets": [[0, 0, 2]],
                                   "mode": mode, "algorithm": "p2p", "seed": 900 + cid})
                     cid += 1
-    results = run_pes(2, cases, tmp_path, extra_env={"SHMEM_FUSED_MAX_BYTES": fused_max})
+                    cases.append({"id": cid, "op": op, "dtype": dtype, "n": 3 + rep, "sets": [[0, 0, 2]],
+                                  "mode": mode, "algorithm": "p2p", "seed": 950 + cid})
+                    cid += 1
+    results = run_pes(2, cases, tmp_path, extra_env=extra_env)
     for c in cases:
         if "golden" in c:
             g = np.load(os.path.join(HERE, "golden", f"golden_nan_{c['op']}_{c['dtype']}.npz"))
@@ -220,6 +220,24 @@ def test_two_member_calls_alternating_nan_and_finite(tmp_path, fused_max):
         for i in range(2):
             assert_match(results[i][str(c["id"])], outs[i], c["op"], c["dtype"], strict=True,
                          ctx=f"case {c['id']} {c['mode']} {c['op']}/{c['dtype']} PE {i}:")
+
+
+@pytest.mark.parametrize("fused_max", ["0", "2M"], ids=["multi-launch", "fused"])
+def test_two_member_calls_alternating_nan_and_finite(tmp_path, fused_max):
+    """The two-member float/double schedule (reduce.c nan_pair): the owner's
+    fold sets a per-call NaN word (parity of the call number with that
+    partner) and the other member patches its gather only when it is set;
+    alternating NaN-rich and NaN-free calls take each parity's word from set
+    to clear and back."""
+    two_member_nan_sequence(tmp_path, {"SHMEM_FUSED_MAX_BYTES": fused_max})
+
+
+def test_two_member_nan_calls_without_signal_regions(tmp_path):
+    """The same sequence when PE 1 cannot map its peer's signal region
+    (SHMEM_TEST_IPC_FAIL=sig): host barriers, and no NaN word to read -- the
+    gather patches unconditionally (reduce.c nan_word_ok) instead of loading
+    through a NULL mapping."""
+    two_member_nan_sequence(tmp_path, {"SHMEM_TEST_IPC_FAIL": "sig"})
 
 
 def test_pe_start_order_within_stated_fp_tolerance(tmp_path):

@@ -11,7 +11,8 @@ with the fused kernel's own HIP event stamps (its average duration), and every
 PE's result checked bit-exact against the oracle's result for that PE (the
 reference's own-source-first order). PE 0 prints one JSON line.
 
-usage: fused_bench.py [calls] [sizes in bytes...]
+usage: fused_bench.py [calls] [sizes in bytes...] [--config1]
+(--config1: also BASELINE config 1's call, config1() below)
 """
 import json
 import os
@@ -29,9 +30,69 @@ def synth(pe, n):
     return (np.random.default_rng(1000 + pe).random(n) - 0.5) * np.exp2(np.random.default_rng(pe).integers(0, 8, n))
 
 
+def config1(shm, calls, max_over_pes):
+    """BASELINE config 1's call through this library: shmem_int_sum_to_all on
+    4 KiB (1,024 ints) over the active set {PE 0, PE 1} (PE_start 0,
+    logPE_stride 0, PE_size 2; other PEs of the job only take part in the
+    allocations and barriers), on shmem_malloc's symmetric host heap -- host
+    memory, as the reference's heap is (symmem.c:212-236) -- and on the
+    device heap. K back-to-back calls from the C loop (csrc/bench_loop.c),
+    entry-to-return per call, max over the two PEs; every element checked
+    bit-exact against the oracle's result for each PE."""
+    import ctypes
+    import oracle
+    me = shm.my_pe()
+    member = me < 2
+    loop = shmem_reduce.bench_loop(name="int_sum")
+    n = 1024
+    out = {}
+    for kind in ("host_heap", "device_heap"):
+        alloc = shm.malloc if kind == "host_heap" else shm.malloc_device
+        src, dst = alloc(n * 4), alloc(n * 4)
+        if not src or not dst:
+            raise RuntimeError("allocation for the config-1 leg failed")
+        xs = [np.random.default_rng(4100 + p).integers(-2**31, 2**31, n).astype(np.int32) for p in range(2)]
+        if member:
+            if kind == "host_heap":
+                ctypes.memmove(src, xs[me].ctypes.data, n * 4)
+            else:
+                shm.put(src, xs[me])
+            loop(dst, src, n, 0, 0, 2, None, shm._psync_ptr, 20)
+        shm.barrier_all()
+        t0 = time.perf_counter()
+        if member:
+            loop(dst, src, n, 0, 0, 2, None, shm._psync_ptr, calls)
+        t = time.perf_counter() - t0
+        info = shm.last_call_info() if member else None
+        bad = 0
+        if member:
+            if kind == "host_heap":
+                got = np.empty(n, dtype=np.int32)
+                ctypes.memmove(got.ctypes.data, dst, n * 4)
+            else:
+                got = shm.get(dst, n, "int")
+            bad = int((got != oracle.reduce_pe("sum", "int", xs, me)).sum())
+        t = max_over_pes(t if member else 0.0) / calls
+        bad = int(max_over_pes(bad))
+        sched = info["schedule"] if info else None
+        out[kind] = {"us_per_call": round(t * 1e6, 2), "calls": calls, "schedule": sched,
+                     "check": "bit-exact vs the reference's per-PE order, every element, both PEs" if bad == 0
+                     else f"MISMATCH {bad} elements"}
+        shm.barrier_all()
+        if kind == "host_heap":
+            shm.free(dst)
+            shm.free(src)
+        else:
+            shm.free_device(dst)
+            shm.free_device(src)
+    return out
+
+
 def main():
-    calls = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
-    sizes = [int(x) for x in sys.argv[2:]] or [64 << 10, 1 << 20]
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    calls = int(args[0]) if args else 4096
+    sizes = [int(x) for x in args[1:]] or [64 << 10, 1 << 20]
+    with_config1 = "--config1" in sys.argv
     os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(8 << 20))
     os.environ.setdefault("SHMEM_DEVICE_SCRATCH_SIZE", "3M")
     os.environ.setdefault("SHMEM_DEVICE_ORDER_SIZE", "8M")
@@ -85,8 +146,9 @@ def main():
         shm.barrier_all()
     shm.free_device(dst)
     shm.free_device(src)
+    c1 = config1(shm, calls, max_over_pes) if with_config1 else None
     if me == 0:
-        print(json.dumps({"npes": npes, "same_gpu": bool(anyshared[0]), "legs": out}), flush=True)
+        print(json.dumps({"npes": npes, "same_gpu": bool(anyshared[0]), "legs": out, "config1": c1}), flush=True)
     shm.finalize()
 
 

@@ -1,0 +1,82 @@
+// peer_shapes.hip -- launch-shape variants of the library's every-member fold
+// for bench.py's `peer_fold_shapes` leg (a measurement probe, not part of the
+// library; tools/libpeershapes.so, built by tools/Makefile `peershapes`).
+//
+// Why: the fold's launch shape (combine_kernels.h Shape<8> / OrdersShape: 4
+// vectors per lane, 8 blocks per CU) was tuned with all 8 sources in local
+// HBM. In BASELINE config 3 at N = 8 each GPU folds its shard with 7 of its 8
+// sources on other GPUs, read over xGMI with several times HBM's latency, so
+// the bytes in flight per CU that hide it may differ. This library
+// instantiates the library's own kernel template (combine_orders_vec<sum,
+// double, 8, U, non-temporal loads, every output>) at other (U, blocks per
+// CU) shapes; bench.py times them beside the library's own launch
+// (mi355_combine_orders) on the same peer-mapped sources and checks every
+// variant's outputs against the library's.
+//
+// C ABI:
+//   int peer_shapes_count(void);
+//   int peer_shapes_describe(int v, int *unroll, int *blocks_per_cu);
+//   int peer_shapes_orders_double_sum(int v, int nsrc, void *const *dsts, const void *const *srcs,
+//                                     size_t n, hipEvent_t start, hipEvent_t stop, hipStream_t st);
+// nsrc = 4 or 8 (BASELINE config 3 at N = 4 / 8).
+// Sources and outputs 16-byte aligned, n a multiple of 2 (whole vectors);
+// returns 0 or a HIP error code / -1 for an unsupported call.
+#include "combine_kernels.h"
+
+namespace {
+
+using namespace mi355k;
+
+struct Variant {
+    int unroll, bpc;
+};
+// the library's shape first (4, 8), then fewer vectors per lane with more
+// blocks, and the deeper queue with more blocks queued
+constexpr Variant kVariants[] = {{4, 8}, {2, 8}, {1, 16}, {2, 16}, {4, 16}};
+constexpr int kCount = sizeof(kVariants) / sizeof(kVariants[0]);
+
+template <int NSRC, int U>
+int run(int bpc, void *const *dsts, const void *const *srcs, size_t n, hipEvent_t e0, hipEvent_t e1,
+        hipStream_t st) {
+    OrdersParams p{};
+    for (int k = 0; k < NSRC; ++k) {
+        p.src[k] = srcs[k];
+        p.dst[k] = dsts[k];
+    }
+    p.nvec = n / 2;
+    auto kern = combine_orders_vec<MI355_OP_SUM, double, NSRC, U, POL_NT_LOAD, true>;
+    const unsigned grid = grid_for((uint64_t)kBlock * U, p.nvec, bpc);
+    hipExtLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, e0, e1, 0, p);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+
+template <int NSRC>
+int dispatch(int v, void *const *dsts, const void *const *srcs, size_t n, hipEvent_t e0, hipEvent_t e1,
+             hipStream_t st) {
+    switch (kVariants[v].unroll) {
+    case 1: return run<NSRC, 1>(kVariants[v].bpc, dsts, srcs, n, e0, e1, st);
+    case 2: return run<NSRC, 2>(kVariants[v].bpc, dsts, srcs, n, e0, e1, st);
+    case 4: return run<NSRC, 4>(kVariants[v].bpc, dsts, srcs, n, e0, e1, st);
+    default: return -1;
+    }
+}
+
+}  // namespace
+
+extern "C" int peer_shapes_count(void) { return kCount; }
+
+extern "C" int peer_shapes_describe(int v, int *unroll, int *blocks_per_cu) {
+    if (v < 0 || v >= kCount) return -1;
+    *unroll = kVariants[v].unroll;
+    *blocks_per_cu = kVariants[v].bpc;
+    return 0;
+}
+
+extern "C" int peer_shapes_orders_double_sum(int v, int nsrc, void *const *dsts, const void *const *srcs, size_t n,
+                                             hipEvent_t e0, hipEvent_t e1, hipStream_t st) {
+    if (v < 0 || v >= kCount || n % 2 != 0 || (nsrc != 4 && nsrc != 8)) return -1;
+    for (int k = 0; k < nsrc; ++k)
+        if (((uintptr_t)dsts[k] | (uintptr_t)srcs[k]) & 15) return -1;
+    return nsrc == 4 ? dispatch<4>(v, dsts, srcs, n, e0, e1, st) : dispatch<8>(v, dsts, srcs, n, e0, e1, st);
+}
