@@ -1587,10 +1587,20 @@ def main():
                 shm.set_fused_max(f0)
                 shm.set_oneshot_max(o0)
             wins = [r["bytes"] for r in rows if r["fused_us"] < r["multi_launch_us"]]
+            cal = shm.threshold_calibration()
             threshold_sweep = {
                 "fused_vs_multi_launch": rows, "oneshot_vs_twoshot": oneshot,
                 "largest_size_fused_wins": max(wins) if wins else 0,
                 "defaults": {"fused_max": f0, "oneshot_max": o0},
+                "calibrated_at_init": None if cal is None else {
+                    "fused_max": f0, "oneshot_max": o0,
+                    "fused_vs_multi_launch_us": [[b, round(a, 2), round(m, 2)] for b, a, m in cal["fused"]],
+                    "oneshot_vs_twoshot_us": [[b, round(a, 2), round(m, 2)] for b, a, m in cal["oneshot"]],
+                    "note": "set by shmem_init on this layout (shmemx_threshold_calibration): each threshold is the "
+                            "largest size of the prefix where the fused (one-shot) call's median, max over PEs, was "
+                            "no slower"},
+                "fused_no_slower_up_to_fused_max": all(r["fused_us"] <= r["multi_launch_us"] for r in rows
+                                                       if r["bytes"] <= f0),
                 "check": "bit-exact (first 4096 elements, every PE, every size and mode)" if bad_total == 0
                 else "MISMATCH in %d elements" % bad_total,
                 "note": "us per shmem_double_sum_to_all call (200 calls, max over PEs) with the fused path forced "
@@ -1715,9 +1725,9 @@ def main():
         xgmi["frac_of_measured"] = round(busbw / pm, 4) if pm and busbw <= pm else None
         # a constant bound below what this run moved is refuted, not exceeded
         for k, b in (("frac", bound), ("frac_one_direction", bound_dir)):
-            if xgmi[k] is not None and xgmi[k] > 1:
+            if not shared_gpu and xgmi[k] is not None and xgmi[k] > 1:
                 xgmi[k] = None
-                xgmi[k + "_refuted"] = "busbw %.1f GB/s exceeds this bound (%.1f GB/s)" % (busbw, b)
+                xgmi["refuted_" + k] = "busbw %.1f GB/s exceeds this bound (%.1f GB/s)" % (busbw, b)
         import ctypes
         lt, hp = ctypes.c_int(), ctypes.c_int()
         links = {}

@@ -80,6 +80,15 @@ size_t shmemx_set_fused_max_bytes (size_t bytes);
 size_t shmemx_set_oneshot_max_bytes (size_t bytes);
 size_t shmemx_get_fused_max_bytes (void);
 size_t shmemx_get_oneshot_max_bytes (void);
+/* Whether init set the two thresholds above from measurement (PE_size > 1,
+ * SHMEM_FUSED_MAX_BYTES / SHMEM_ONESHOT_MAX_BYTES not given,
+ * SHMEM_THRESHOLD_CALIBRATE not 0): 1 if it did. us[0..21] (n entries
+ * filled): the job-wide median call times in microseconds of the measured
+ * double sums -- fused then multi-launch at 64K, 256K, 512K, 1M, 2M, 4M
+ * bytes, one-shot then two-shot at 16K, 32K, 64K, 128K, 256K (0: size not
+ * measured, larger than the scratch buffers). Each threshold is the largest
+ * size of the prefix of sizes where the fused (one-shot) call was no slower. */
+int shmemx_threshold_calibration (double *us, int n);
 
 /* Whose result the P2P schedules (and the stream-ordered calls) deliver
  * (env SHMEM_REDUCE_ORDER=reference|pe_start sets the default at init):

@@ -1149,6 +1149,103 @@ static void debug_check (const char *fn, int op, int dtype, const void *target, 
     shmemi_debug_exchange (&r, PE_start, 1 << logPE_stride, PE_size);
 }
 
+/* SHMEM_FUSED_MAX_BYTES and SHMEM_ONESHOT_MAX_BYTES from measurement, at
+ * init, on this job's own layout (PE_size > 1, the variable not given): the
+ * fused one-launch schedule saves the multi-launch schedule's barrier
+ * launches (barrier-linear.c:57-85's two barriers and the gather's own) but
+ * pays its device-side flag round trips in one grid; where it stops paying
+ * depends on the links (round 5, two PEs on one GPU: 1 MiB, not the 2 MiB
+ * default; bench.py threshold_sweep). Double sums over the whole job between
+ * scratch buffers A and B: each size timed both ways (median of 9 blocking
+ * calls after 2 warm-ups, entry to return), the medians max-reduced over the
+ * PEs through the bootstrap segment, and the threshold set to the largest
+ * size of the prefix of sizes where the fused (one-shot) call was no slower
+ * -- the same decision on every PE. About 250 calls, a few ms. */
+void shmemi_calibrate_thresholds (int fused, int oneshot)
+{
+    static const size_t fsz[SHMEMI_CALIB_NF] = {64 << 10, 256 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20};
+    static const size_t osz[SHMEMI_CALIB_NO] = {16 << 10, 32 << 10, 64 << 10, 128 << 10, 256 << 10};
+    const int np = shmemi.npes, me = shmemi.mype, K = 9, W = 2;
+    struct aset s = {0, 1, np, me};
+    const size_t src_off = shmemi.scratch_off, dst_off = shmemi.scratch_off + shmemi.scratch_chunk;
+    const size_t f0 = shmemi.fused_max, o0 = shmemi.oneshot_max;
+    const unsigned mask0 = shmemi_trace_mask;
+    shmemi_trace_mask &= ~(1u << SHMEMI_LOG_REDUCTION); /* no schedule lines for these calls */
+    SHMEMI_HIP (hipMemset (shmemi.heap + src_off, 0, shmemi.scratch_chunk));
+    SHMEMI_HIP (hipDeviceSynchronize ());
+    shmemi_barrier_set (0, 1, np);
+    uint64_t mine[SHMEMI_CALIB_SLOTS] = {0};
+    /* slot of (kind, size): kind 0 fused / 1 multi-launch / 2 one-shot / 3 two-shot */
+#define SLOT(kind, i) ((kind) < 2 ? (kind) * SHMEMI_CALIB_NF + (i) : 2 * SHMEMI_CALIB_NF + ((kind) - 2) * SHMEMI_CALIB_NO + (i))
+    for (int kind = 0; kind < 4; ++kind) {
+        if ((kind < 2 && !fused) || (kind >= 2 && !oneshot))
+            continue;
+        const int nsz = kind < 2 ? SHMEMI_CALIB_NF : SHMEMI_CALIB_NO;
+        for (int i = 0; i < nsz; ++i) {
+            const size_t bytes = kind < 2 ? fsz[i] : osz[i];
+            if (bytes > shmemi.scratch_chunk)
+                continue; /* 0 = not measured: ends the prefix below */
+            shmemi.fused_max = kind == 1 ? 0 : (size_t) 1 << 30;
+            shmemi.oneshot_max = kind == 2 ? (size_t) 1 << 30 : kind == 3 ? 0 : o0;
+            double t[16];
+            for (int r = 0; r < W + K; ++r) {
+                caller_order_pending = 1;
+                const double t0 = shmemi_now ();
+                reduce_symmetric (MI355_OP_SUM, MI355_DOUBLE, 8, dst_off, src_off, bytes / 8, &s);
+                if (r >= W)
+                    t[r - W] = shmemi_now () - t0;
+            }
+            for (int a = 1; a < K; ++a) /* median: insertion sort of 9 */
+                for (int b = a; b > 0 && t[b] < t[b - 1]; --b) {
+                    const double x = t[b];
+                    t[b] = t[b - 1];
+                    t[b - 1] = x;
+                }
+            mine[SLOT (kind, i)] = (uint64_t) (t[K / 2] * 1e9) + 1;
+        }
+    }
+    struct shmemi_pe_info *info = shmemi_seg_info (me);
+    for (int k = 0; k < SHMEMI_CALIB_SLOTS; ++k)
+        __atomic_store_n (&info->calib_ns[k], mine[k], __ATOMIC_RELEASE);
+    shmemi_barrier_set (0, 1, np);
+    for (int k = 0; k < SHMEMI_CALIB_SLOTS; ++k) {
+        uint64_t w = 0;
+        for (int q = 0; q < np; ++q) {
+            const uint64_t v = __atomic_load_n (&shmemi_seg_info (q)->calib_ns[k], __ATOMIC_ACQUIRE);
+            w = v == 0 || w == UINT64_MAX ? UINT64_MAX : v > w ? v : w; /* unmeasured anywhere: unmeasured */
+        }
+        shmemi.calib_us[k] = w == UINT64_MAX ? 0.0 : (double) w * 1e-3;
+    }
+    shmemi_barrier_set (0, 1, np); /* nobody reads the records any more */
+    /* the largest size of the prefix where the fused / one-shot call was no slower */
+    size_t fm = f0, om = o0;
+    if (fused) {
+        fm = 0;
+        for (int i = 0; i < SHMEMI_CALIB_NF; ++i) {
+            const double a = shmemi.calib_us[SLOT (0, i)], b = shmemi.calib_us[SLOT (1, i)];
+            if (a <= 0.0 || b <= 0.0 || a > b)
+                break;
+            fm = fsz[i];
+        }
+    }
+    if (oneshot) {
+        om = 0;
+        for (int i = 0; i < SHMEMI_CALIB_NO; ++i) {
+            const double a = shmemi.calib_us[SLOT (2, i)], b = shmemi.calib_us[SLOT (3, i)];
+            if (a <= 0.0 || b <= 0.0 || a > b)
+                break;
+            om = osz[i];
+        }
+    }
+#undef SLOT
+    shmemi.fused_max = fm;
+    shmemi.oneshot_max = om;
+    shmemi.calib_ran = 1;
+    shmemi_trace_mask = mask0;
+    SHMEMI_TRACE (SHMEMI_LOG_INIT, "thresholds from measurement: fused path up to %zu bytes, one-shot up to %zu bytes",
+                  fm, om);
+}
+
 static void reduce_impl (int op, int dtype, const char *fn, void *target, const void *source,
                          int nreduce, int PE_start, int logPE_stride, int PE_size, long *pSync)
 {

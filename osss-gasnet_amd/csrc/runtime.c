@@ -669,7 +669,7 @@ static void settings_publish (void)
 {
     seg_info (shmemi.mype)->settings =
         (struct shmemi_settings) {shmemi.algorithm, shmemi.order, shmemi.debug != 0, shmemi.srv.enabled,
-                                  shmemi.ext_map, 0, shmemi.order_chunk, shmemi.fused_max, shmemi.oneshot_max, shmemi.scratch_chunk,
+                                  shmemi.ext_map, shmemi.calib_want, shmemi.order_chunk, shmemi.fused_max, shmemi.oneshot_max, shmemi.scratch_chunk,
                                   shmemi.user_size, shmemi.hheap_size};
 }
 
@@ -688,6 +688,7 @@ static void settings_check (void)
         S (order, "SHMEM_REDUCE_ORDER")
         S (debug, "SHMEM_DEBUG")
         S (ext_map, "SHMEM_EXTERNAL_MAP")
+        S (calibrate, "SHMEM_THRESHOLD_CALIBRATE (or SHMEM_FUSED_MAX_BYTES / SHMEM_ONESHOT_MAX_BYTES set on some PEs only)")
         S (order_chunk, "SHMEM_DEVICE_ORDER_SIZE")
         S (fused_max, "SHMEM_FUSED_MAX_BYTES")
         S (oneshot_max, "SHMEM_ONESHOT_MAX_BYTES")
@@ -1358,6 +1359,18 @@ void pshmem_free (void *ptr)
 /* ---------------------------------------------------------------------- */
 static void finalize_atexit (void) { pshmem_finalize (); }
 
+/* The fused / one-shot thresholds from measurement on this job's layout
+ * (reduce.c shmemi_calibrate_thresholds), where the environment did not set
+ * them: every PE decides alike (calib_want is a checked setting, and the
+ * self-test outcomes below are job-wide). */
+static void calibrate (void)
+{
+    if (shmemi.npes < 2 || shmemi.calib_want == 0 || shmemi.fused_off || shmemi.sig_broken || shmemi.dev_wait_slow ||
+        shmemi.p2p_broken || shmemi.algorithm == SHMEMX_REDUCE_EXACT || shmemi.algorithm == SHMEMX_REDUCE_RCCL)
+        return;
+    shmemi_calibrate_thresholds (shmemi.calib_want & 1, (shmemi.calib_want >> 1) & 1);
+}
+
 void pshmem_init (void)
 {
     if (shmemi.initialized)
@@ -1436,6 +1449,14 @@ void pshmem_init (void)
     if (shmemi.fused_max > ((size_t) 1 << 30))
         shmemi.fused_max = (size_t) 1 << 30;
     shmemi.oneshot_max = env_size ("SHMEM_ONESHOT_MAX_BYTES", (size_t) 64 << 10);
+    /* thresholds not given: measured at init (PE_size > 1, calibrate below);
+     * SHMEM_THRESHOLD_CALIBRATE=0 keeps the defaults above */
+    {
+        static const char *cal_env[] = {"SHMEM_THRESHOLD_CALIBRATE", NULL};
+        shmemi.calib_want = env_long (cal_env, 1) == 0 ? 0
+                                                       : (getenv ("SHMEM_FUSED_MAX_BYTES") == NULL ? 1 : 0) |
+                                                             (getenv ("SHMEM_ONESHOT_MAX_BYTES") == NULL ? 2 : 0);
+    }
 
     if (shmemi.npes == 1)
         hheap_setup ();
@@ -1460,6 +1481,7 @@ void pshmem_init (void)
         }
     }
     shmemi.initialized = 1;
+    calibrate ();
     shmemi_trace_show_levels ();
     if (shmemi_trace_mask & (1u << SHMEMI_LOG_INIT)) {
         char bus[64] = "";
@@ -1733,6 +1755,13 @@ void shmemx_coherence_producer (int *ran, int *fresh)
     if (fresh != NULL)
         for (int i = 0; i < 6; ++i)
             fresh[i] = shmemi.prod[i];
+}
+
+int shmemx_threshold_calibration (double *us, int n)
+{
+    for (int k = 0; us != NULL && k < n && k < SHMEMI_CALIB_SLOTS; ++k)
+        us[k] = shmemi.calib_us[k];
+    return shmemi.calib_ran;
 }
 
 void shmemx_device_wait_report (int *slow, double *us)

@@ -40,7 +40,7 @@ struct shmemi_dbg_rec {
 
 /* Settings every PE of a job must share (compared at init). */
 struct shmemi_settings {
-    int32_t algorithm, order, debug, persistent, ext_map, pad;
+    int32_t algorithm, order, debug, persistent, ext_map, calibrate;
     uint64_t order_chunk, fused_max, oneshot_max, scratch_chunk, user_size, hheap_size;
 };
 
@@ -56,6 +56,12 @@ struct shmemi_ext_rec {
     int32_t open_ok;            /* second round: this member opened every peer's buffer */
     int32_t pad;
 };
+
+/* init-time threshold calibration (reduce.c): fused vs multi-launch at
+ * SHMEMI_CALIB_NF sizes, one-shot vs two-shot at SHMEMI_CALIB_NO sizes */
+#define SHMEMI_CALIB_NF 6
+#define SHMEMI_CALIB_NO 5
+#define SHMEMI_CALIB_SLOTS (2 * SHMEMI_CALIB_NF + 2 * SHMEMI_CALIB_NO)
 
 struct shmemi_pe_info {
     int32_t pid;
@@ -73,6 +79,7 @@ struct shmemi_pe_info {
                                    host-wait ordering plain / sysload / acquire */
     uint64_t collect_bytes;     /* this PE's contribution to the current shmem_collect */
     uint64_t barrier_ns;        /* init: this PE's time per device barrier over the job (device_wait_test) */
+    uint64_t calib_ns[SHMEMI_CALIB_SLOTS]; /* init: this PE's median call times (shmemi_calibrate_thresholds) */
     struct shmemi_settings settings;
     struct shmemi_dbg_rec dbg;
     struct shmemi_ext_rec ext;
@@ -162,6 +169,9 @@ struct shmemi_state {
     size_t fused_max;           /* SHMEM_FUSED_MAX_BYTES: largest message on the fused path */
     size_t oneshot_max;         /* SHMEM_ONESHOT_MAX_BYTES: largest fused message folded one-shot */
     int fused_off;              /* a failed self-test disabled the fused path: the setters keep it off */
+    int calib_want;             /* init-time calibration: bit 0 fused_max, bit 1 oneshot_max (not set by env) */
+    int calib_ran;              /* the thresholds above came from the init-time calibration */
+    double calib_us[SHMEMI_CALIB_SLOTS]; /* its job-wide (max over PEs) median call times */
     int sig_broken;             /* peers' signal-region stores failed the init self-test */
     int dev_wait_slow;          /* device-side waits across PEs time-sliced (init timing): host barriers, no fused kernel */
     double dev_barrier_us;      /* that timing: the job's slowest PE, microseconds per device barrier */
@@ -269,6 +279,7 @@ int shmemi_dev_barrier_ok (int PE_start, int stride, int PE_size);
 void shmemi_dev_barrier (int PE_start, int stride, int PE_size, int me, int last);
 struct MI355FusedArgs;
 void shmemi_member_args (struct MI355FusedArgs *a, int PE_start, int stride, int PE_size, int me);
+void shmemi_calibrate_thresholds (int fused, int oneshot);
 void shmemi_arm_signal (void);
 void shmemi_wait_signal (void);
 unsigned shmemi_next_epoch (void);

@@ -68,6 +68,7 @@ def load(path=LIB_PATH):
         "shmemx_external_map_stats": ([ctypes.POINTER(ctypes.c_long)] * 3, None),
         "shmemx_external_map_flush": ([], None),
         "shmemx_device_id": ([], _i), "shmemx_device_synchronize": ([], None),
+        "shmemx_threshold_calibration": ([ctypes.POINTER(ctypes.c_double), _i], _i),
         "shmemx_peer_link": ([_i, ctypes.POINTER(_i), ctypes.POINTER(_i)], _i),
         "shmemx_memcpy": ([_vp, _vp, _sz], None), "shmemx_wtime": ([], ctypes.c_double),
         "shmemx_kernel_timing": ([_i], None),
@@ -131,6 +132,17 @@ class Shmem:
 
     def free_device(self, ptr):
         self.lib.shmemx_free_device(ptr)
+
+    def threshold_calibration(self):
+        """None, or the init-time threshold calibration (shmemx_threshold_calibration):
+        {"fused": [(bytes, fused_us, multi_launch_us)...], "oneshot": [(bytes, oneshot_us, twoshot_us)...]}"""
+        us = (ctypes.c_double * 22)()
+        if not self.lib.shmemx_threshold_calibration(us, 22):
+            return None
+        fs = [64 << 10, 256 << 10, 512 << 10, 1 << 20, 2 << 20, 4 << 20]
+        os_ = [16 << 10, 32 << 10, 64 << 10, 128 << 10, 256 << 10]
+        return {"fused": [(b, us[i], us[6 + i]) for i, b in enumerate(fs)],
+                "oneshot": [(b, us[12 + i], us[17 + i]) for i, b in enumerate(os_)]}
 
     def peer_device_ptr(self, ptr, pe):
         """PE pe's copy of a device-heap object, addressable by kernels on

@@ -34,6 +34,10 @@ _SHM = None
 # the device-side waits these tests are meant to cover; 2 queues each keeps up
 # to 8 PEs on the device path (the spawned PE processes inherit this).
 os.environ.setdefault("GPU_MAX_HW_QUEUES", "2")
+# the suite's multi-PE jobs keep the default thresholds (deterministic
+# schedules); the init-time calibration is tested on its own
+# (test_gpu_checks.py) and runs in the bench lines (test_gpu_bench.py)
+os.environ.setdefault("SHMEM_THRESHOLD_CALIBRATE", "0")
 
 
 @pytest.fixture(scope="session")

@@ -30,8 +30,9 @@ def free_port():
 
 def run(cmd, timeout=240, env=None):
     # the bench sizes its own device heap (the in-process tests' fixture sets a small one in os.environ)
+    # and calibrates its thresholds at init as the driver's run does
     env = {k: v for k, v in (env or os.environ).items()
-           if k not in ("SHMEM_DEVICE_HEAP_SIZE", "SHMEM_DEVICE_SCRATCH_SIZE")}
+           if k not in ("SHMEM_DEVICE_HEAP_SIZE", "SHMEM_DEVICE_SCRATCH_SIZE", "SHMEM_THRESHOLD_CALIBRATE")}
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
@@ -202,6 +203,14 @@ def test_bench_two_ranks_line_with_failed_rccl_comparison(tmp_path):
     # fused vs multi-launch and one-shot vs two-shot per size, schedules as forced, results exact
     ts = d["threshold_sweep"]
     assert ts["check"].startswith("bit-exact") and len(ts["fused_vs_multi_launch"]) == 6, ts
+    # the thresholds in force came from shmem_init's measurement on this layout
+    cal = ts["calibrated_at_init"]
+    assert cal is not None and cal["fused_max"] == ts["defaults"]["fused_max"], ts
+    fm = [b for b, f, m in cal["fused_vs_multi_launch_us"]]
+    assert cal["fused_max"] == 0 or cal["fused_max"] in fm, cal
+    for b, f, m in cal["fused_vs_multi_launch_us"]:
+        if b <= cal["fused_max"]:
+            assert 0 < f <= m, cal
     for r in ts["fused_vs_multi_launch"]:
         assert r["fused_schedule"].startswith("fused") and r["multi_launch_schedule"] == "p2p", r
     for r in ts["oneshot_vs_twoshot"]:

@@ -192,6 +192,75 @@ def test_timesliced_device_waits_use_host_barriers():
         assert parse(out, "BAD")[0][0] == "0", out
 
 
+CALIB = ("import oracle\n"
+         "cal = shm.threshold_calibration()\n"
+         "fm, om = shm.thresholds()\n"
+         "print('CAL', int(cal is not None), fm, om, flush=True)\n"
+         "if cal is not None:\n"
+         "    for b, f, m in cal['fused']: print('F', b, f, m, flush=True)\n"
+         "    for b, o, t in cal['oneshot']: print('O', b, o, t, flush=True)\n"
+         "d = shm.malloc_device(8 << 20); t = shm.malloc_device(8 << 20)\n"
+         "bad, scheds = 0, []\n"
+         "for k, nb in enumerate([16 << 10, 64 << 10, 256 << 10, 1 << 20, 2 << 20, 4 << 20, 8 << 20]):\n"
+         "    n = nb // 8\n"
+         "    xs = [np.random.default_rng(300 * k + p).random(n) - 0.5 for p in range(npes)]\n"
+         "    shm.put(d, xs[me])\n"
+         "    shm.to_all('sum', 'double', t, d, n, 0, 0, npes)\n"
+         "    scheds.append('%d:%s' % (nb, shm.last_call_info()['schedule']))\n"
+         "    got = shm.get(t, n, 'double')\n"
+         "    bad += int((got.view(np.uint64) != oracle.reduce_pe('sum', 'double', xs, me).view(np.uint64)).sum())\n"
+         "print('BAD', bad, flush=True)\n"
+         "print('SCHED', *scheds, flush=True)\n"
+         "shm.finalize()\n")
+
+
+def test_thresholds_calibrated_at_init():
+    """the fused / one-shot thresholds from measurement on the
+    job's own layout (reduce.c shmemi_calibrate_thresholds): every PE gets the
+    same thresholds, each the largest size of the prefix of measured sizes
+    where the fused (one-shot) call was no slower; calls below and above them
+    take the schedules they select, bit-exact on every PE."""
+    rcs, outs, _ = spawn(3, CALIB, extra={"SHMEM_THRESHOLD_CALIBRATE": "1", "SHMEM_DEVICE_SCRATCH_SIZE": "24M"})
+    cals = []
+    for rc, out in zip(rcs, outs):
+        assert rc == 0, out[-2000:]
+        cal = parse(out, "CAL")[0]
+        assert cal[0] == "1", out
+        fm, om = int(cal[1]), int(cal[2])
+        cals.append((fm, om))
+        fs = [(int(b), float(f), float(m)) for b, f, m in parse(out, "F")]
+        os_ = [(int(b), float(o), float(t)) for b, o, t in parse(out, "O")]
+        assert len(fs) == 6 and len(os_) == 5 and all(f > 0 and m > 0 for _, f, m in fs), out
+        # the rule: the largest size of the winning prefix
+        want_f = 0
+        for b, f, m in fs:
+            if f > m:
+                break
+            want_f = b
+        want_o = 0
+        for b, o, t in os_:
+            if o > t:
+                break
+            want_o = b
+        assert (fm, om) == (want_f, want_o), (fm, om, fs, os_)
+        assert parse(out, "BAD")[0] == ["0"], out
+        for x in parse(out, "SCHED")[0]:
+            nb, sched = x.split(":")
+            if int(nb) <= fm:
+                assert sched.startswith("fused-" + ("oneshot" if int(nb) <= om else "twoshot")), (x, fm, om)
+            else:
+                assert sched == "p2p", (x, fm)
+    assert len(set(cals)) == 1, cals   # one decision for the job
+
+
+def test_calibration_settings_must_agree():
+    """A threshold given on one PE only would make that PE skip the
+    calibration its peers run: init aborts naming the setting instead."""
+    rcs, outs, _ = spawn(2, "print('UP', flush=True)\nshm.finalize()\n", extra={"SHMEM_THRESHOLD_CALIBRATE": "1"},
+                         per_pe={1: {"SHMEM_FUSED_MAX_BYTES": "2M"}}, timeout=60)
+    assert any(rc != 0 for rc in rcs) and any("SHMEM_THRESHOLD_CALIBRATE" in o for o in outs), outs
+
+
 # ---------------------------------------------------------------------------
 # SHMEM_DEBUG=1 collective argument check
 # ---------------------------------------------------------------------------
