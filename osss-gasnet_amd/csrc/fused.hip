@@ -435,9 +435,16 @@ __device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &
         bool tail_plain = false;
         const uint64_t lo = oneshot ? 0 : (uint64_t)a.me * c.shard;
         const uint64_t hi = oneshot ? c.n : (lo + c.shard < c.n ? lo + c.shard : c.n);
+        // staged one-shot: nobody reads this PE's result but the caller, so
+        // the fold writes it straight to the caller's target (host memory
+        // over PCIe, or device memory) instead of to dst[me] and a stage-out
+        // copy after this PE's AGDONE (round 6: BASELINE config 1's 4 KiB
+        // call on shmem_malloc'd arrays)
+        const bool direct_out = staged && oneshot && (((uintptr_t)a.host_dst) & 15) == 0;
+        char *const out = direct_out ? (char *)a.host_dst : dst_of(a, c, a.me);
         if (hi > lo) {
             const uint64_t nv = (hi - lo) / V;
-            u32x4 *d = (u32x4 *)(dst_of(a, c, a.me) + lo * sizeof(T));
+            u32x4 *d = (u32x4 *)(out + lo * sizeof(T));
             for (uint64_t v = (uint64_t)blockIdx.x * kBlock + threadIdx.x; v < nv;
                  v += (uint64_t)gridDim.x * kBlock) {
                 if (versions) versions_vec<OP, T>(a, c, lo, v);
@@ -447,7 +454,7 @@ __device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &
             if (tail0 < hi && blockIdx.x == 0 && threadIdx.x < hi - tail0) {
                 const uint64_t i = tail0 + threadIdx.x;
                 if (!versions) {
-                    ((T *)dst_of(a, c, a.me))[i] = fold_elem<OP, T>(a, c, i, first);
+                    ((T *)out)[i] = fold_elem<OP, T>(a, c, i, first);
                 } else {
                     for (int j = 0; j < a.nmembers; ++j) {  // own version last (in place, as versions_vec)
                         const int q = j < a.me ? j : j + 1 < a.nmembers ? j + 1 : a.me;
@@ -504,7 +511,7 @@ __device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &
         PHASE_MAX(c, 5);
         if (last_block(mine + MI355_SIG_AG_COUNT)) {
             publish(a, cnt, MI355_SIG_AGDONE);
-            if (!staged) {
+            if (!staged || direct_out) {
                 __syncthreads();
                 if (!wait_members(a, mine, cnt, MI355_SIG_AGDONE, true, !a.no_acquire)) ok_all = 0;
                 __syncthreads();
@@ -514,7 +521,7 @@ __device__ __forceinline__ void fused_body(const MI355FusedArgs &a, const Call &
                 return;
             }
         }
-        if (!staged) return;
+        if (!staged || direct_out) return;
         // ---- stage out (every block): dst[me] is complete once this PE's own
         // AGDONE slot shows this call (published above by the gather's last
         // block, after every block's write-through stores drained); acquire,

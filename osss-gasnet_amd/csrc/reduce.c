@@ -776,6 +776,9 @@ static void server_start (int op, int dtype, size_t es, size_t n, int oneshot, c
 
 static void copy_local (size_t dst_off, size_t src_off, size_t nbytes, int timed);
 
+static void fused_launch (int op, int dtype, size_t es, size_t n, const struct aset *s, const void *const *srcs,
+                          void *const *dsts, int same, const void *host_src, void *host_dst);
+
 /* host_src/host_dst: device-accessible page-locked host buffers of this PE
  * staged in-kernel into src_off / out of dst_off (mi355_reduce.h), or NULL.
  * A one-member set (the 1-PE identity copy) comes here only with the
@@ -802,8 +805,31 @@ static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t sr
         begin_call ("identity");
         copy_local (dst_off, src_off, n * es, 1);
     } else {
+        const void *srcs[MI355_FUSED_MAX_MEMBERS];
+        void *dsts[MI355_FUSED_MAX_MEMBERS];
+        for (int i = 0; i < s->size; ++i) {
+            srcs[i] = shmemi_peer_ptr (aset_pe (s, i), src_off);
+            dsts[i] = shmemi_peer_ptr (aset_pe (s, i), dst_off);
+        }
+        fused_launch (op, dtype, es, n, s, srcs, dsts, dst_off == src_off, host_src, host_dst);
+    }
+    if (servable) {
+        /* the second call of a burst leaves the kernel resident for the next */
+        if (shmemi.srv.last_end >= 0.0 && t_call - shmemi.srv.last_end < shmemi.srv.idle_s)
+            server_start (op, dtype, es, n, n * es <= shmemi.oneshot_max && dst_off != src_off, s);
+        shmemi.srv.last_end = shmemi_now ();
+    }
+}
+
+/* One launch of the fused kernel over the members' buffers srcs[i] / dsts[i]
+ * (this PE's = member s->me's), waited for. `same`: target = source (no
+ * one-shot: it would overwrite a source others still read). */
+static void fused_launch (int op, int dtype, size_t es, size_t n, const struct aset *s, const void *const *srcs,
+                          void *const *dsts, int same, const void *host_src, void *host_dst)
+{
+    {
         SHMEMI_TRACE (SHMEMI_LOG_REDUCTION, "schedule: fused one-launch P2P, %s, %s (%zu elements, %d members)%s",
-                      n * es <= shmemi.oneshot_max && dst_off != src_off ? "one-shot" : "reduce-scatter + all-gather",
+                      n * es <= shmemi.oneshot_max && !same ? "one-shot" : "reduce-scatter + all-gather",
                       ordered_pair (op, dtype, s->size) ? "every member's reference order" : "PE_start order", n,
                       s->size, host_src != NULL ? ", staging host buffers in-kernel" : "");
         MI355FusedArgs a;
@@ -817,8 +843,8 @@ static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t sr
         for (int i = 0; i < s->size; ++i) {
             const int pe = aset_pe (s, i);
             a.pe[i] = pe;
-            a.src[i] = shmemi_peer_ptr (pe, src_off);
-            a.dst[i] = shmemi_peer_ptr (pe, dst_off);
+            a.src[i] = srcs[i];
+            a.dst[i] = dsts[i];
             a.sig[i] = shmemi.peer_sig[pe] + SHMEMI_CHAN_HOST * MI355_SIG_CHANNEL_WORDS;
         }
         a.host_flag = shmemi.sig_flag;
@@ -829,7 +855,7 @@ static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t sr
         a.host_dst = host_dst;
         a.share = shmemi.local_pes;
         a.no_acquire = shmemi.fused_no_acquire;
-        a.oneshot = n * es <= shmemi.oneshot_max && dst_off != src_off;
+        a.oneshot = n * es <= shmemi.oneshot_max && !same;
         fused_order (&a, s, SHMEMI_CHAN_HOST);
         shmemi_timed_begin (); /* the call's one (dominant) kernel */
         const int rc = mi355_fused_allreduce (&a, shmemi.stream);
@@ -841,12 +867,6 @@ static void fused_range (int op, int dtype, size_t es, size_t dst_off, size_t sr
         note_fused (s->size, a.ordered, a.oneshot, n, es, mi355_last_kernel ());
         if (shmemi_wait_flag (a.epoch) != a.epoch)
             shmemi_fatal ("fused reduction timed out waiting for the other PEs of the active set");
-    }
-    if (servable) {
-        /* the second call of a burst leaves the kernel resident for the next */
-        if (shmemi.srv.last_end >= 0.0 && t_call - shmemi.srv.last_end < shmemi.srv.idle_s)
-            server_start (op, dtype, es, n, n * es <= shmemi.oneshot_max && dst_off != src_off, s);
-        shmemi.srv.last_end = shmemi_now ();
     }
 }
 
