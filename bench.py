@@ -746,7 +746,7 @@ COLD_FOOTPRINT = 2304 << 20
 # and version slots, which the library spaces by a shard + 256 + VER_STAGGER
 # (4096) bytes (csrc/reduce.c ver_slot_bytes): nothing lines the streams up on
 # the same HBM channels. Buffers exactly a power of two apart would
-# (tools/cold_probe orders_skew2); each leg also reports that layout
+# (tools/probes/cold_probe orders_skew2); each leg also reports that layout
 # ("warm_aligned", separate hipMalloc'd buffers) for comparison.
 LEG_STAGGER = 4352
 # the long double legs' VALU floor: their per-element instruction streams in

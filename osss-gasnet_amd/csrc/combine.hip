@@ -87,7 +87,7 @@ __global__ __launch_bounds__(kBlock) void copy_segments(SegParams<NS> p) {
         const uint64_t nvec = (nb - head) / 16;
         const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
         // software-pipelined: the loads of pass k+1 are in flight while the
-        // stores of pass k issue (tools/copy_variants.hip: 78.3 vs 80.0 us for
+        // stores of pass k issue (tools/probes/copy_variants.hip: 78.3 vs 80.0 us for
         // 256 MiB at UNROLL 4, one block per CU, over all-loads-then-stores)
         uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
         u32x4 x[UNROLL];
@@ -448,7 +448,7 @@ static int copy_segments_impl(void *const *dsts, const void *const *srcs, const 
         fire_on_host((hipStream_t)stream);
         return 0;
     }
-    // pipelined UNROLL 4, one block per CU (tools/copy_variants.hip,
+    // pipelined UNROLL 4, one block per CU (tools/probes/copy_variants.hip,
     // profiles/r01/copy_variants.txt: 78.2-78.5 us for 256 MiB, the best of
     // grid-stride / per-block partition / 1-4 blocks per CU / UNROLL 4-16);
     // a segment whose source is at another phase than its target: the

@@ -27,7 +27,7 @@ constexpr int kMaxSrc = 8;
 // ---------------------------------------------------------------------------
 // Completion signal (mi355_signal_next_launch): the last block to finish
 // stores `epoch` into a host-visible word, so the host learns the result is
-// in memory ~4 us sooner than through hipStreamSynchronize (tools/latency.hip:
+// in memory ~4 us sooner than through hipStreamSynchronize (tools/probes/latency.hip:
 // 6.9 vs 10.7 us for a launch round trip on MI355X).
 struct Signal {
     unsigned *count;  // device word, 0 between launches (the last block resets it)
@@ -79,7 +79,7 @@ __device__ __forceinline__ void nan_flag_store(unsigned long long *w, unsigned l
     __hip_atomic_store(w, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Cache policy (tools/hbm_sweep.hip, MI355X, 256 MiB per buffer):
+// Cache policy (tools/probes/hbm_sweep.hip, MI355X, 256 MiB per buffer):
 //   stores: write-through to memory at agent scope, which makes the completion
 //     signal cheap: no per-block L2 write-back (that cost 60 us on a 256 MiB
 //     copy with 2048 blocks). The copy: `nt sc1`, as fast as plain
@@ -98,7 +98,7 @@ __device__ __forceinline__ void st16(u32x4 *p, u32x4 v) {
     asm volatile("global_store_dwordx4 %0, %1, off nt sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
 }
 // The folds' stores: write-through at agent scope WITHOUT the non-temporal
-// hint. Beside non-temporal loads this is the faster form (tools/fold_probe.hip,
+// hint. Beside non-temporal loads this is the faster form (tools/probes/fold_probe.hip,
 // profiles/r02/fold_probe_copy.txt, 256 MiB per source: k = 2 116.4 vs 127.9 us,
 // k = 3 158.7 vs 177.1, k = 8 393.5 vs 422); the copy keeps `nt sc1` (with
 // its plain loads `sc1` alone is 18 % slower).
@@ -111,7 +111,7 @@ __device__ __forceinline__ void st16_fold(u32x4 *p, u32x4 v) {
 // written as aligned vectors and each source vector is read with one 16-byte
 // load from its unaligned address. gfx950 runs in unaligned access mode (the
 // loads stay global_load_dwordx4; the type below only tells the compiler the
-// alignment it may assume). Measured (tools/cold_probe unal / shift / dpp,
+// alignment it may assume). Measured (tools/probes/cold_probe unal / shift / dpp,
 // 256 MiB double sum of two sources, target aligned, sources 8 bytes off):
 // 0.84 of peak warm / 0.76 cold -- against 0.59 element-wise, 0.73 / 0.70
 // assembling each vector from two aligned loads (v_alignbyte), 0.77 / 0.71
@@ -276,7 +276,7 @@ __device__ __forceinline__ void orders_element(const OrdersParams &p, int64_t i)
 // stores; with them it placed `s_waitcnt vmcnt` on the previous pass's stores
 // before the loads (the stores' data registers are reused as load addresses
 // across the branches), which halved the kernel's rate at 2-4 sources
-// (tools/orders_probe.hip; rocprofv3 160 vs 82 us at 4 x 64 MiB).
+// (tools/probes/orders_probe.hip; rocprofv3 160 vs 82 us at 4 x 64 MiB).
 // The software x87 sum/product: NSRC * (NSRC - 1) soft-float operations per
 // element are too much code to unroll over the members, and a register array
 // indexed by a rolled loop's variable lives in scratch memory. So the NSRC
@@ -639,7 +639,7 @@ inline unsigned grid_for(uint64_t units_per_block_pass, uint64_t units, int bloc
     return (unsigned)(want < cap ? want : cap);
 }
 
-// Launch shape per source count, from tools/hbm_sweep.hip and
+// Launch shape per source count, from tools/probes/hbm_sweep.hip and
 // tools/fold_bench.py on MI355X (256 MiB per source, double sums,
 // non-temporal loads + `nt sc1` stores at the time; the folds store `sc1`
 // since round 2, see st16_fold; GB/s counts (k+1) x 256 MiB;
@@ -652,7 +652,7 @@ inline unsigned grid_for(uint64_t units_per_block_pass, uint64_t units, int bloc
 // Box-to-box spread is +-3 %, so neighbours within that band are ties.
 // Long double is VALU-bound (x87 arithmetic in software): it wants many
 // waves to hide ALU latency, not deep per-lane load queues. Round 5
-// (tools/cold_probe k2types, 256 MiB): the float two-source fold at 4 blocks
+// (tools/probes/cold_probe k2types, 256 MiB): the float two-source fold at 4 blocks
 // per CU, 115 vs 122 us (its NaN checks cover four lanes per vector); the
 // float complex product's at 8 (ShapeOp), 131 vs 162 us -- its sum is faster
 // at 2 (120 vs 123 us), so that one is per operator.

@@ -122,7 +122,7 @@ __device__ __forceinline__ u32x4 ld16_sys(const void *p) {
 // The folds' form of the same load: one 16-byte `buffer_load_dwordx4 ...
 // sc0 sc1` from a wave-uniform base (a member's buffer) at a per-lane byte
 // offset, through the builtin so the compiler places the waits. Round 4
-// (tools/fold_probe S, profiles/r04/fold_probe_sysload16.txt): 16-byte
+// (tools/probes/fold_probe S, profiles/r04/fold_probe_sysload16.txt): 16-byte
 // system-coherent loads fold 2 sources in 134 us per 256 MiB against 143 us
 // for ld16_sys's two 8-byte loads (8 sources: 441 vs 459 us); non-temporal
 // loads take 116 / 381 us, so the multi-launch folds keep theirs.

@@ -220,7 +220,7 @@ static int nan_pair (int op, int dtype, const struct aset *s)
  * Consecutive slots are VER_STAGGER bytes further apart than a shard needs:
  * the every-member fold writes all its outputs at the same element offset,
  * and outputs a power-of-two shard size apart land in the same HBM channels
- * (tools/cold_probe orders_skew2, 8 x 32 MiB double sum: 0.62 of peak from
+ * (tools/probes/cold_probe orders_skew2, 8 x 32 MiB double sum: 0.62 of peak from
  * HBM with 256-byte gaps, 0.68-0.70 with 4 KiB-granular ones). */
 #define VER_STAGGER 4096
 static size_t ver_slot_bytes (size_t n, size_t es, int size)

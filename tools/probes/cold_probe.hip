@@ -14,9 +14,9 @@
 // the copy, variants of its loop compiled here (load / store policy, blocks
 // per CU, vectors per lane).
 //
-// build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -I include -I osss-gasnet_amd/csrc tools/cold_probe.hip \
-//          -L osss-gasnet_amd/lib -lshmem_reduce -Wl,-rpath,$PWD/osss-gasnet_amd/lib -o tools/cold_probe
-// run:   tools/cold_probe [lib|copy|all|copy2|orders]   (one JSON line per measurement)
+// build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off -std=c++17 -I include -I osss-gasnet_amd/csrc tools/probes/cold_probe.hip \
+//          -L osss-gasnet_amd/lib -lshmem_reduce -Wl,-rpath,$PWD/osss-gasnet_amd/lib -o tools/probes/cold_probe
+// run:   tools/probes/cold_probe [lib|copy|all|copy2|orders]   (one JSON line per measurement)
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

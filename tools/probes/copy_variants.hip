@@ -1,7 +1,7 @@
 // copy_variants.hip -- layouts of the 256 MiB streaming copy (the PE_size = 1
 // identity fold, the bench's dominant kernel), timed with HIP events
 // (tuning tool, not part of the library).
-//   build: hipcc --offload-arch=gfx950 -O3 tools/copy_variants.hip -o tools/copy_variants
+//   build: hipcc --offload-arch=gfx950 -O3 tools/probes/copy_variants.hip -o tools/probes/copy_variants
 //
 //   gs      the library's copy_segments: grid-stride, U vectors per lane spaced
 //           one block apart, all loads then all stores, `nt sc1` stores

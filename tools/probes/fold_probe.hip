@@ -3,7 +3,7 @@
 // shape, and the read-only ceiling of k concurrent streams (tuning tool, not
 // part of the library). 256 MiB per source, double sum, HIP events, median of
 // 7 launches.
-//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/fold_probe.hip -o tools/fold_probe
+//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/probes/fold_probe.hip -o tools/probes/fold_probe
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>

@@ -1,7 +1,7 @@
 // fold_variants.hip -- k-source double-sum fold (the reduce-scatter kernel),
 // grid-stride as in the library vs software-pipelined, 256 MiB per source,
 // timed with HIP events (tuning tool, not part of the library).
-//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/fold_variants.hip -o tools/fold_variants
+//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/probes/fold_variants.hip -o tools/probes/fold_variants
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>

@@ -3,8 +3,8 @@
 // k-source double-sum fold of the reduce-scatter leg). Standalone tuning tool,
 // not part of the library.
 //
-// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/hbm_sweep.hip -o tools/hbm_sweep
-// run:   tools/hbm_sweep [MiB]
+// build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/probes/hbm_sweep.hip -o tools/probes/hbm_sweep
+// run:   tools/probes/hbm_sweep [MiB]
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <stdio.h>

@@ -1,6 +1,6 @@
 // latency.hip -- host<->GPU round-trip costs that bound a small reduction call
 // (tuning tool, not part of the library).
-//   build: hipcc --offload-arch=gfx950 -O2 tools/latency.hip -o tools/latency
+//   build: hipcc --offload-arch=gfx950 -O2 tools/probes/latency.hip -o tools/probes/latency
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>

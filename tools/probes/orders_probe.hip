@@ -3,7 +3,7 @@
 // others in order) on one GPU, 256 MiB per PE split into K shards as in an
 // N = K PE call; double sum, `sc1` stores, non-temporal loads; HIP events,
 // median of 7 (tuning tool, not part of the library).
-//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/orders_probe.hip -o tools/orders_probe
+//   build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off tools/probes/orders_probe.hip -o tools/probes/orders_probe
 #include <hip/hip_runtime.h>
 #include <stdio.h>
 #include <stdlib.h>

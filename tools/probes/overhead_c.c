@@ -1,7 +1,7 @@
 /* overhead_c.c -- per-call cost of a 1-PE device-resident shmem_double_sum_to_all
  * from C (no Python in the loop). Tuning tool.
- *   gcc -O2 -Iinclude tools/overhead_c.c -Losss-gasnet_amd/lib -lshmem_reduce \
- *       -Wl,-rpath,$PWD/osss-gasnet_amd/lib -o tools/overhead_c */
+ *   gcc -O2 -Iinclude tools/probes/overhead_c.c -Losss-gasnet_amd/lib -lshmem_reduce \
+ *       -Wl,-rpath,$PWD/osss-gasnet_amd/lib -o tools/probes/overhead_c */
 #include <stdio.h>
 #include <stdlib.h>
 #include <shmem.h>

@@ -3,10 +3,10 @@
  * sweep; tuning tool, not part of the library). Device-resident buffers,
  * calls back to back from C, median of `reps` timed blocks, PE 0 prints one
  * JSON line per size (time = max over PEs via shmem_double_max_to_all).
- *   gcc -O2 -Iinclude tools/size_sweep.c -Losss-gasnet_amd/lib -lshmem_reduce \
- *       -Wl,-rpath,$PWD/osss-gasnet_amd/lib -o tools/size_sweep
- *   tools/oshrun -np 4 --same-device tools/size_sweep      (or run directly: 1 PE)
- *   tools/size_sweep host [max_bytes]    source/target from shmem_malloc (host memory, staged)
+ *   gcc -O2 -Iinclude tools/probes/size_sweep.c -Losss-gasnet_amd/lib -lshmem_reduce \
+ *       -Wl,-rpath,$PWD/osss-gasnet_amd/lib -o tools/probes/size_sweep
+ *   tools/oshrun -np 4 --same-device tools/probes/size_sweep      (or run directly: 1 PE)
+ *   tools/probes/size_sweep host [max_bytes]    source/target from shmem_malloc (host memory, staged)
  */
 #include <stdio.h>
 #include <stdlib.h>
