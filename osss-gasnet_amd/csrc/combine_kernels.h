@@ -511,7 +511,6 @@ template <int OP, typename T, int NSRC, int UNROLL, int POL, bool ALL, bool SHIF
 __global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
     constexpr int V = 16 / sizeof(T);
     const uint64_t nvec = p.nvec;
-    const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
     static_assert(!SHIFT || !std::is_same<T, x80>::value, "long double runs aligned or element-wise");
     if constexpr (std::is_same<T, x80>::value && (OP == MI355_OP_SUM || OP == MI355_OP_PROD)) {
         const uint64_t stride = (uint64_t)gridDim.x * kBlock;
