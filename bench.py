@@ -735,7 +735,41 @@ KERNEL_LEGS = [
     # what each GPU folds in BASELINE config 4's longlong and at N = 8: 8 shards of 8 MiB (64 MiB / 8);
     # bitwise and is order-free, so the P2P schedule runs the plain fold, one output per shard
     ("rs_shard_n8_longlong_and", "combine_vec<and,longlong,8>", "and", "longlong", 8, 8 << 20, False),
+    # the same every-member folds at a quarter of their shard: with the 8 and 32 MiB legs they fit
+    # t = fixed + bytes / rate per launch (FIXED_COST_FITS) -- why the small shards run below the big
+    ("rs_shard_n8_float_max_2mib", "combine_orders_vec<max,float,8>", "max", "float", 8, 2 << 20, True),
+    ("rs_shard_n8_double_sum_8mib", "combine_orders_vec<sum,double,8>", "sum", "double", 8, 8 << 20, True),
 ]
+# (kernel, [legs of that kernel at two or more shard sizes]) for the fixed-cost fit
+FIXED_COST_FITS = [("combine_orders_vec<max,float,8>", ["rs_shard_n8_float_max_2mib", "rs_shard_n8_float_max"]),
+                   ("combine_orders_vec<sum,double,8>", ["rs_shard_n8_double_sum_8mib", "rs_shard_n8_double_sum"])]
+
+
+def fixed_cost_fit(res):
+    """Least-squares t = a + alg_bytes / B over the cold launches of one
+    kernel at several shard sizes: a = the per-launch fixed cost (dispatch
+    ramp of the grid and drain of its last wave, microseconds), B = the
+    streaming rate between them; stream_frac = B / the HBM peak, what the
+    kernel reaches once a launch is long enough to hide a."""
+    out = {}
+    for kname, legs in FIXED_COST_FITS:
+        pts = [(res[g]["alg_bytes_per_launch"], res[g]["cold"]["kernel_avg_us"]) for g in legs
+               if g in res and res[g].get("cold")]
+        if len(pts) < 2:
+            continue
+        x = np.array([p[0] for p in pts], dtype=np.float64)
+        y = np.array([p[1] for p in pts], dtype=np.float64)
+        slope, a = np.polyfit(x, y, 1)
+        if slope <= 0:
+            continue
+        rate = 1.0 / slope * 1e6   # bytes per second
+        out[kname] = {"legs": legs, "fixed_us": round(float(a), 2), "stream_GB_s": round(rate / 1e9, 1),
+                      "stream_frac": round(rate / 1e9 / HBM_PEAK_GBS, 4),
+                      "fixed_share": {g: round(float(a) / res[g]["cold"]["kernel_avg_us"], 3) for g in legs}}
+    out["note"] = ("cold launches of one kernel at two shard sizes fitted to t = fixed + bytes / rate: fixed = the "
+                   "per-launch ramp and drain, rate = the streaming rate in between (stream_frac of the HBM peak); "
+                   "fixed_share = the fixed part's share of each leg's cold time")
+    return out
 # each leg is timed twice: warm (the same buffers every launch, as the leg's
 # own loop re-reads them) and cold (rotating disjoint buffer sets, >= 2 GiB of
 # footprint, so no byte is still in the 256 MiB Infinity Cache)
@@ -940,6 +974,7 @@ def kernel_legs(shm, reps, check):
         L.hipEventDestroy(e)
     for d in [pool0] + al_srcs + al_outs:
         L.hipFree(vp(d))
+    res["fixed_cost_fit"] = fixed_cost_fit(res)
     res["note"] = ("fold kernels timed alone (HIP event pair per launch on its stream), algorithmic bytes = "
                    "(sources + outputs) x bytes; frac against the 8 TB/s HBM peak; warm = the same buffers every "
                    "launch (a set under ~256 MiB stays in the Infinity Cache), cold = disjoint copies taken in "
@@ -975,6 +1010,9 @@ def main():
                          "256 MiB, config 3 / 4's per-GPU reduce-scatter shapes)")
     ap.add_argument("--no-external", action="store_true",
                     help="N > 1: skip the leg on plain hipMalloc buffers (outside the symmetric heap)")
+    ap.add_argument("--force-xgmi-legs", action="store_true",
+                    help="N > 1: run xgmi_ceiling and peer_fold_shapes even when the PEs share a GPU (a rehearsal of "
+                         "their code path; the figures are local HBM rates and feed no roofline)")
     ap.add_argument("--no-link-probe", action="store_true",
                     help="N > 1: skip PE 0's one-peer-at-a-time shmem_getmem / shmem_putmem rates")
     ap.add_argument("--kernel-reps", type=int, default=50)
@@ -1159,6 +1197,18 @@ def main():
     shm.barrier_all()
     t_calls = call_times(dst, src, n, 0, 0, npes, shm._psync_ptr, args.steps)
     legs_s["headline"] = round(time.perf_counter() - t_head0, 2)
+
+    # the call's fixed cost: the same entry point on 2 elements (one launch of
+    # the same copy kernel, its completion flag, the return) -- what a
+    # blocking call pays beside its kernel's duration
+    t_tiny = None
+    if npes == 1 and not args.host:
+        steps(50, 2)
+        ttq = time.perf_counter()
+        steps(2000, 2)
+        shm.sync()
+        t_tiny = (time.perf_counter() - ttq) / 2000
+        steps(1)   # the headline target again for the checks below
 
     # N = 1: the same call into a target one element off (offset_target_leg);
     # before the rotating leg, whose launches rocprof's split counts last
@@ -1401,7 +1451,7 @@ def main():
     xgmi_ceiling = peer_shapes = None
     if npes > 1 and not args.host:
         na = {"not_applicable": "the PEs share a GPU: peer reads are this GPU's own HBM, no link is involved"}
-        if shared_gpu:
+        if shared_gpu and not args.force_xgmi_legs:
             xgmi_ceiling, peer_shapes = dict(na), dict(na)
         elif rccl_fallback:
             xgmi_ceiling = peer_shapes = {"not_applicable": "peer heap reads failed the init self-test"}
@@ -1422,6 +1472,8 @@ def main():
                             "GB/s into each GPU, slowest PE"})
                 xgmi_ceiling["peak_measured_GB_s"] = max(xgmi_ceiling["kernel_GB_s_into_each_pe"],
                                                          xgmi_ceiling["sdma_GB_s_into_each_pe"])
+                if shared_gpu:   # a rehearsal: local HBM copies, not a link ceiling
+                    xgmi_ceiling["rehearsal_same_gpu"] = xgmi_ceiling.pop("peak_measured_GB_s")
             if npes in (4, 8):
                 with timed_leg("peer_fold_shapes", optional=solo):
                     out_buf = shm.malloc_device(S + npes * 8192)
@@ -1440,6 +1492,8 @@ def main():
                         r["same_outputs"] = int(max_over_pes(0 if r["same_outputs"] else 1)) == 0
                     best = min(peer_shapes["rows"], key=lambda r: r["kernel_avg_us"])
                     peer_shapes["fastest"] = best["shape"]
+                    if shared_gpu:
+                        peer_shapes["rehearsal_same_gpu"] = True
                     peer_shapes["note"] = ("config 3's every-member fold with N-1 sources on peers, at the library's "
                                            "launch shape and at tools/libpeershapes.so's (same kernel template), all "
                                            "PEs at once; kernel_avg_us max over PEs; same_outputs: every output equal "
@@ -1764,6 +1818,12 @@ def main():
                        "parallelism": f"pe{npes}"},
             "per_pe_gib_s": round(S / t_step / GIB, 2),
             "per_call": call_dist,
+            "fixed_cost": None if t_tiny is None else {
+                "tiny_call_us": round(t_tiny * 1e6, 2),
+                "step_minus_kernel_us": round(t_step * 1e6 - k_avg_ms * 1e3, 2),
+                "note": "tiny_call_us: the same call on 2 elements (one launch of the same copy kernel, its completion "
+                        "flag, the return), 2000 back to back; step_minus_kernel_us: ms_per_step minus the dominant "
+                        "kernel's event-timed duration -- the blocking call's launch and completion round trip"},
             "roofline": roofline,
             "xgmi": xgmi,
             "rccl_compare": rccl,

@@ -129,11 +129,16 @@ def test_bench_one_gpu_line():
     k = d["kernels"]
     for name in ("fold_k2_double_sum", "fold_k8_double_sum", "rs_shard_n8_double_sum", "fold_k8_float_max",
                  "fold_k8_longlong_and", "rs_shard_n8_float_max", "rs_shard_n8_longdouble_sum",
-                 "rs_shard_n8_longdouble_prod", "rs_shard_n8_complexf_prod", "rs_shard_n8_longlong_and"):
+                 "rs_shard_n8_longdouble_prod", "rs_shard_n8_complexf_prod", "rs_shard_n8_longlong_and",
+                 "rs_shard_n8_float_max_2mib", "rs_shard_n8_double_sum_8mib"):
         assert k[name]["check"].startswith("bit-exact"), (name, k[name])
         assert 0 < k[name]["frac"] <= 1.0 and k[name]["kernel_avg_us"] > 0, (name, k[name])
         assert 0 < k[name]["cold"]["frac"] <= 1.0 and k[name]["cold"]["footprint_MiB"] >= 2048, (name, k[name])
         assert 0 < k[name]["warm_aligned"]["frac"] <= 1.0, (name, k[name])
+    # the every-member folds' per-launch fixed cost, fitted from two shard sizes each
+    fc = k["fixed_cost_fit"]
+    for kn in ("combine_orders_vec<max,float,8>", "combine_orders_vec<sum,double,8>"):
+        assert fc[kn]["stream_GB_s"] > 0 and 0 < fc[kn]["stream_frac"] <= 1.0, fc
     # the x87 sum's own roofline: VALU issue, from this build's instruction stream
     ls = k["rs_shard_n8_longdouble_sum"]
     assert ls["bound"] == "valu" and 0.3 < ls["valu_frac"] < 1.05 and ls["valu_per_element_wave"] > 1000, ls
@@ -256,3 +261,29 @@ def test_bench_line_survives_a_dying_extra_legs_job():
         assert set(d[leg]) == {"error"} and "child job" in d[leg]["error"], (leg, d[leg])
     assert not any(isinstance(v, dict) and "error" in v for k, v in d.items()
                    if k not in ("external_buffers", "link_probe", "collectives")), d
+
+
+@pytest.mark.multipe
+def test_bench_xgmi_legs_rehearsal_four_ranks():
+    """The legs that only mean something with one GPU per PE -- the measured
+    all-peers pull ceiling (xgmi_ceiling) and the every-member fold's launch
+    shapes with N-1 peer sources (peer_fold_shapes) -- forced on with four
+    ranks sharing the test GPU (--force-xgmi-legs): their code path runs
+    (peer mappings, copy kernel, copy engines, the probe library's shapes),
+    every variant's outputs equal the library's, and the figures stay out of
+    the roofline (a rehearsal, marked so)."""
+    d = run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+             "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "bench.py", "--gpus", "4", "--steps",
+             "5", "--warmup", "2", "--mib", "64", "--force-xgmi-legs", "--no-cpu-baseline", "--no-small", "--no-ops",
+             "--no-threshold-sweep", "--no-rccl-compare", "--no-external", "--no-link-probe", "--no-collectives"],
+            timeout=400)
+    assert d["check"].startswith("bit-exact, every element, every PE"), d["check"]
+    xc = d["xgmi_ceiling"]
+    assert xc["check"].startswith("bit-exact") and xc["rehearsal_same_gpu"] > 0, xc
+    assert xc["kernel_GB_s_into_each_pe"] > 0 and xc["sdma_GB_s_into_each_pe"] > 0, xc
+    assert xc["bytes_into_each_pe"] == 3 * ((64 << 20) // 4), xc
+    ps = d["peer_fold_shapes"]
+    assert ps["rehearsal_same_gpu"] and ps["sources"] == 4 and ps["peer_sources"] == 3, ps
+    assert len(ps["rows"]) >= 4 and all(r["same_outputs"] and r["kernel_avg_us"] > 0 for r in ps["rows"]), ps
+    # the rehearsal feeds no bound: the roofline stays the shared-GPU HBM view
+    assert d["roofline"]["bound"] == "hbm" and d["xgmi"]["peak_measured_GB_s"] is None, d["roofline"]

@@ -42,11 +42,13 @@ n1_256mib copy_segments<4,~1> 1000
 offset_target_copy_shift copy_segments_shift<4,~1> 1000
 kernel_fold_k2_double_sum combine_vec<0,~double,~2, 1000
 kernel_fold_k8_double_sum combine_vec<0,~double,~8, 1000
-kernel_rs_shard_n8_double_sum combine_orders_vec<0,~double,~8, 1000
+kernel_rs_shard_n8_double_sum combine_orders_vec<0,~double,~8, 300000
+kernel_rs_shard_n8_double_sum_8mib combine_orders_vec<0,~double,~8, 1000:300000
 kernel_fold_k8_float_max combine_vec<6,~float,~8, 1000
 kernel_fold_k8_longlong_and combine_vec<2,~long,~8, 300000
 kernel_rs_shard_n8_longlong_and combine_vec<2,~long,~8, 1000:300000
-kernel_rs_shard_n8_float_max combine_orders_vec<6,~float,~8, 1000
+kernel_rs_shard_n8_float_max combine_orders_vec<6,~float,~8, 300000
+kernel_rs_shard_n8_float_max_2mib combine_orders_vec<6,~float,~8, 1000:300000
 kernel_rs_shard_n8_longdouble_sum combine_orders_vec<0,~x80,~8, 1000
 kernel_rs_shard_n8_longdouble_prod combine_orders_vec<1,~x80,~8, 1000
 kernel_rs_shard_n8_complexf_prod combine_orders_vec<1,~mi355::cplxf,~8, 1000
