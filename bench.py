@@ -1202,7 +1202,7 @@ def main():
     # the same copy kernel, its completion flag, the return) -- what a
     # blocking call pays beside its kernel's duration
     t_tiny = None
-    if npes == 1 and not args.host:
+    if npes == 1 and not args.host and not args.no_small:   # (profiling runs: the copy's rocprof average stays the headline's)
         steps(50, 2)
         ttq = time.perf_counter()
         steps(2000, 2)
@@ -1514,7 +1514,7 @@ def main():
         if npes == 1 and not args.no_kernels and not args.host:
             kernels = kernel_legs(shm, args.kernel_reps, not args.no_check)
             for name, leg in kernels.items():
-                if isinstance(leg, dict):
+                if isinstance(leg, dict) and "alg_bytes_per_launch" in leg:
                     leg["traffic_note"] = traffic_for(leg, f"kernel_{name}", False)
                     if leg.get("traffic"):
                         leg["traffic_over_alg"] = round(leg["traffic"] / leg["alg_bytes_per_launch"], 4)
