@@ -35,7 +35,7 @@ struct Variant {
 constexpr Variant kVariants[] = {{4, 8}, {2, 8}, {1, 16}, {2, 16}, {4, 16}};
 constexpr int kCount = sizeof(kVariants) / sizeof(kVariants[0]);
 
-template <int NSRC, int U>
+template <int OP, typename T, int NSRC, int U>
 int run(int bpc, void *const *dsts, const void *const *srcs, size_t n, hipEvent_t e0, hipEvent_t e1,
         hipStream_t st) {
     OrdersParams p{};
@@ -43,21 +43,21 @@ int run(int bpc, void *const *dsts, const void *const *srcs, size_t n, hipEvent_
         p.src[k] = srcs[k];
         p.dst[k] = dsts[k];
     }
-    p.nvec = n / 2;
-    auto kern = combine_orders_vec<MI355_OP_SUM, double, NSRC, U, POL_NT_LOAD, true>;
+    p.nvec = n / (16 / sizeof(T));
+    auto kern = combine_orders_vec<OP, T, NSRC, U, POL_NT_LOAD, true>;
     const unsigned grid = grid_for((uint64_t)kBlock * U, p.nvec, bpc);
     hipExtLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, e0, e1, 0, p);
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : (int)e;
 }
 
-template <int NSRC>
+template <int OP, typename T, int NSRC>
 int dispatch(int v, void *const *dsts, const void *const *srcs, size_t n, hipEvent_t e0, hipEvent_t e1,
              hipStream_t st) {
     switch (kVariants[v].unroll) {
-    case 1: return run<NSRC, 1>(kVariants[v].bpc, dsts, srcs, n, e0, e1, st);
-    case 2: return run<NSRC, 2>(kVariants[v].bpc, dsts, srcs, n, e0, e1, st);
-    case 4: return run<NSRC, 4>(kVariants[v].bpc, dsts, srcs, n, e0, e1, st);
+    case 1: return run<OP, T, NSRC, 1>(kVariants[v].bpc, dsts, srcs, n, e0, e1, st);
+    case 2: return run<OP, T, NSRC, 2>(kVariants[v].bpc, dsts, srcs, n, e0, e1, st);
+    case 4: return run<OP, T, NSRC, 4>(kVariants[v].bpc, dsts, srcs, n, e0, e1, st);
     default: return -1;
     }
 }
@@ -78,5 +78,17 @@ extern "C" int peer_shapes_orders_double_sum(int v, int nsrc, void *const *dsts,
     if (v < 0 || v >= kCount || n % 2 != 0 || (nsrc != 4 && nsrc != 8)) return -1;
     for (int k = 0; k < nsrc; ++k)
         if (((uintptr_t)dsts[k] | (uintptr_t)srcs[k]) & 15) return -1;
-    return nsrc == 4 ? dispatch<4>(v, dsts, srcs, n, e0, e1, st) : dispatch<8>(v, dsts, srcs, n, e0, e1, st);
+    return nsrc == 4 ? dispatch<MI355_OP_SUM, double, 4>(v, dsts, srcs, n, e0, e1, st)
+                     : dispatch<MI355_OP_SUM, double, 8>(v, dsts, srcs, n, e0, e1, st);
+}
+
+// The same shapes for BASELINE config 4's float max (8 sources): the
+// library runs it at one vector per lane (combine_kernels.h OrdersShape, min/
+// max chains); n a multiple of 4.
+extern "C" int peer_shapes_orders_float_max(int v, void *const *dsts, const void *const *srcs, size_t n, hipEvent_t e0,
+                                            hipEvent_t e1, hipStream_t st) {
+    if (v < 0 || v >= kCount || n % 4 != 0) return -1;
+    for (int k = 0; k < 8; ++k)
+        if (((uintptr_t)dsts[k] | (uintptr_t)srcs[k]) & 15) return -1;
+    return dispatch<MI355_OP_MAX, float, 8>(v, dsts, srcs, n, e0, e1, st);
 }
