@@ -271,16 +271,18 @@ def persistent_child(rank, world, calls):
 
 
 def extra_legs_child(rank, world, mib, steps, algorithm, flags):
-    """N > 1: external_buffers, link_probe and collectives, run by one child PE
-    process per rank on the rank's own GPU (tools/extra_legs.py), started
-    before this process touches the GPU, like persistent_child: none of them
-    had run with one GPU per PE before the driver's 8-GPU node, and a fatal
-    error in one (the library aborts the PE) or a hang would otherwise end
-    this rank before the headline line is printed. Returns rank 0's records,
-    or {"error": ...} under each leg's name."""
+    """N > 1: external_buffers, link_probe, collectives and (round 6) the
+    one-GPU-per-PE legs xgmi_ceiling and peer_fold_shapes (xgmi_legs), run by
+    one child PE process per rank on the rank's own GPU (tools/extra_legs.py),
+    started before this process touches the GPU, like persistent_child: none
+    of them had run with one GPU per PE before the driver's 8-GPU node, and a
+    fatal error in one (the library aborts the PE) or a hang would otherwise
+    end this rank before the headline line is printed. Returns rank 0's
+    records, or {"error": ...} under each leg's name."""
     import subprocess
     names = [k for k, f in (("external_buffers", "--no-external"), ("link_probe", "--no-link-probe"),
-                            ("collectives", "--no-collectives")) if f not in flags]
+                            ("collectives", "--no-collectives"), ("xgmi_ceiling", "--no-xgmi-legs"),
+                            ("peer_fold_shapes", "--no-xgmi-legs")) if f not in flags]
     if not names:
         return {}
     job = "xl%s-%d" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
@@ -716,6 +718,58 @@ def peer_fold_shapes_leg(shm, S, me, npes, src, out, reps=10):
             "bytes_per_source": shard_b, "reps": reps, "rows": rows}
 
 
+def xgmi_legs(shm, S, me, npes, src, dst, force, max_over_pes):
+    """N > 1: xgmi_ceiling_leg and (N = 4 or 8) peer_fold_shapes_leg on this
+    job's buffers (src holds synth(me, ...), dst and S + N x 8 KiB more of
+    device heap are free), their figures reduced over the PEs (slowest PE).
+    PEs sharing a GPU: not applicable, unless `force` (a rehearsal of the code
+    path, marked so, feeding no roofline). Run by tools/extra_legs.py, bench's
+    child job. Returns {"xgmi_ceiling": ..., "peer_fold_shapes": ...}."""
+    shared = np.array([sum(shm.lib.shmemx_pe_same_device(q) for q in range(npes) if q != me)], dtype=np.int32)
+    shared_gpu = int(max_over_pes(float(shared[0]))) != 0
+    na = {"not_applicable": "the PEs share a GPU: peer reads are this GPU's own HBM, no link is involved"}
+    if shared_gpu and not force:
+        return {"xgmi_ceiling": dict(na), "peer_fold_shapes": dict(na)}
+    xc = xgmi_ceiling_leg(shm, S, me, npes, src, dst)
+    xgmi_ceiling = {k: v for k, v in xc.items() if k not in ("kernel_avg_us", "kernel_GB_s", "sdma_us", "sdma_GB_s",
+                                                             "bad", "kernel_wall_us")}
+    slow_k = max_over_pes(xc["kernel_avg_us"])
+    slow_s = max_over_pes(xc["sdma_us"])
+    xgmi_ceiling.update({
+        "kernel_avg_us": round(slow_k, 2), "kernel_GB_s_into_each_pe": round(xc["bytes_into_each_pe"] / slow_k / 1e3, 1),
+        "sdma_us": round(slow_s, 2), "sdma_GB_s_into_each_pe": round(xc["bytes_into_each_pe"] / slow_s / 1e3, 1),
+        "check": "bit-exact (sampled, every peer's segment)" if int(max_over_pes(xc["bad"])) == 0 else "MISMATCH",
+        "note": "every PE pulls shard q of peer q's array from all N-1 peers at once (the all-gather's pattern) "
+                "through the peer mappings: the library's copy kernel and the copy engines; GB/s into each GPU, "
+                "slowest PE; measured in bench.py's child job (tools/extra_legs.py)"})
+    xgmi_ceiling["peak_measured_GB_s"] = max(xgmi_ceiling["kernel_GB_s_into_each_pe"],
+                                             xgmi_ceiling["sdma_GB_s_into_each_pe"])
+    if shared_gpu:   # a rehearsal: local HBM copies, not a link ceiling
+        xgmi_ceiling["rehearsal_same_gpu"] = xgmi_ceiling.pop("peak_measured_GB_s")
+    if npes not in (4, 8):
+        return {"xgmi_ceiling": xgmi_ceiling,
+                "peer_fold_shapes": {"not_applicable": "the shape variants are 4- and 8-source folds (N = %d)" % npes}}
+    out_buf = shm.malloc_device(S + npes * 8192)
+    if not out_buf:
+        raise RuntimeError("no room in the device heap for the peer fold's outputs")
+    try:
+        ps = peer_fold_shapes_leg(shm, S, me, npes, src, out_buf)
+    finally:
+        shm.free_device(out_buf)
+    for r in ps["rows"]:
+        r["kernel_avg_us"] = round(max_over_pes(r["kernel_avg_us"]), 2)
+        r["remote_read_GB_s"] = round(ps["bytes_per_source"] * (npes - 1) / r["kernel_avg_us"] / 1e3, 1)
+        r["hbm_frac"] = round(2 * npes * ps["bytes_per_source"] / r["kernel_avg_us"] / 1e3 / HBM_PEAK_GBS, 4)
+        r["same_outputs"] = int(max_over_pes(0 if r["same_outputs"] else 1)) == 0
+    ps["fastest"] = min(ps["rows"], key=lambda r: r["kernel_avg_us"])["shape"]
+    if shared_gpu:
+        ps["rehearsal_same_gpu"] = True
+    ps["note"] = ("config 3's every-member fold with N-1 sources on peers, at the library's launch shape and at "
+                  "tools/libpeershapes.so's (same kernel template), all PEs at once; kernel_avg_us max over PEs; "
+                  "same_outputs: every output equal to the library's on every PE; measured in bench.py's child job")
+    return {"xgmi_ceiling": xgmi_ceiling, "peer_fold_shapes": ps}
+
+
 # ---------------------------------------------------------------------------
 # kernel legs (N = 1): the fold kernels themselves, timed on one GPU
 # ---------------------------------------------------------------------------
@@ -1010,6 +1064,8 @@ def main():
                          "256 MiB, config 3 / 4's per-GPU reduce-scatter shapes)")
     ap.add_argument("--no-external", action="store_true",
                     help="N > 1: skip the leg on plain hipMalloc buffers (outside the symmetric heap)")
+    ap.add_argument("--no-xgmi-legs", action="store_true",
+                    help="N > 1: skip xgmi_ceiling and peer_fold_shapes (the child job's one-GPU-per-PE legs)")
     ap.add_argument("--force-xgmi-legs", action="store_true",
                     help="N > 1: run xgmi_ceiling and peer_fold_shapes even when the PEs share a GPU (a rehearsal of "
                          "their code path; the figures are local HBM rates and feed no roofline)")
@@ -1077,7 +1133,9 @@ def main():
             extra = extra_legs_child(rank, world, args.mib, args.steps, args.algorithm,
                                      [f for f, on in (("--no-check", args.no_check), ("--no-external", args.no_external),
                                                       ("--no-link-probe", args.no_link_probe),
-                                                      ("--no-collectives", args.no_collectives)) if on])
+                                                      ("--no-collectives", args.no_collectives),
+                                                      ("--no-xgmi-legs", args.no_xgmi_legs),
+                                                      ("--force-xgmi-legs", args.force_xgmi_legs)) if on])
     # CPU baseline, before this process initialises the GPU; at N > 1 the
     # other ranks wait for rank 0 in the bootstrap (SHMEM_BARRIER_TIMEOUT)
     cpu = None
@@ -1445,61 +1503,13 @@ def main():
         del got_full
     legs_s["check"] = round(time.perf_counter() - t_check0, 2)
 
-    # N > 1, one GPU per PE: the measured xGMI ceiling (all peers at once,
-    # the all-gather's pattern) and the every-member fold's launch shapes
-    # with N-1 remote sources; before op_coverage rewrites the sources
+    # N > 1, one GPU per PE: the measured xGMI ceiling and the peer-fold
+    # shapes, measured in the child job (extra_legs_child, before this rank
+    # touched the GPU: a failure there cannot take the headline with it)
     xgmi_ceiling = peer_shapes = None
     if npes > 1 and not args.host:
-        na = {"not_applicable": "the PEs share a GPU: peer reads are this GPU's own HBM, no link is involved"}
-        if shared_gpu and not args.force_xgmi_legs:
-            xgmi_ceiling, peer_shapes = dict(na), dict(na)
-        elif rccl_fallback:
-            xgmi_ceiling = peer_shapes = {"not_applicable": "peer heap reads failed the init self-test"}
-        else:
-            with timed_leg("xgmi_ceiling", optional=solo):
-                xc = xgmi_ceiling_leg(shm, S, me, npes, src, dst)
-                xgmi_ceiling = {k: v for k, v in xc.items() if k not in ("kernel_avg_us", "kernel_GB_s", "sdma_us",
-                                                                         "sdma_GB_s", "bad", "kernel_wall_us")}
-                slow_k = max_over_pes(xc["kernel_avg_us"])
-                slow_s = max_over_pes(xc["sdma_us"])
-                xgmi_ceiling.update({
-                    "kernel_avg_us": round(slow_k, 2), "kernel_GB_s_into_each_pe": round(xc["bytes_into_each_pe"] / slow_k / 1e3, 1),
-                    "sdma_us": round(slow_s, 2), "sdma_GB_s_into_each_pe": round(xc["bytes_into_each_pe"] / slow_s / 1e3, 1),
-                    "check": "bit-exact (sampled, every peer's segment)" if int(max_over_pes(xc["bad"])) == 0
-                    else "MISMATCH",
-                    "note": "every PE pulls shard q of peer q's array from all N-1 peers at once (the all-gather's "
-                            "pattern) through the peer mappings: the library's copy kernel and the copy engines; "
-                            "GB/s into each GPU, slowest PE"})
-                xgmi_ceiling["peak_measured_GB_s"] = max(xgmi_ceiling["kernel_GB_s_into_each_pe"],
-                                                         xgmi_ceiling["sdma_GB_s_into_each_pe"])
-                if shared_gpu:   # a rehearsal: local HBM copies, not a link ceiling
-                    xgmi_ceiling["rehearsal_same_gpu"] = xgmi_ceiling.pop("peak_measured_GB_s")
-            if npes in (4, 8):
-                with timed_leg("peer_fold_shapes", optional=solo):
-                    out_buf = shm.malloc_device(S + npes * 8192)
-                    if not out_buf:
-                        raise RuntimeError("no room in the device heap for the peer fold's outputs")
-                    try:
-                        peer_shapes = peer_fold_shapes_leg(shm, S, me, npes, src, out_buf)
-                    finally:
-                        shm.free_device(out_buf)
-                    for r in peer_shapes["rows"]:
-                        r["kernel_avg_us"] = round(max_over_pes(r["kernel_avg_us"]), 2)
-                        r["remote_read_GB_s"] = round(peer_shapes["bytes_per_source"] * (npes - 1)
-                                                      / r["kernel_avg_us"] / 1e3, 1)
-                        r["hbm_frac"] = round(2 * npes * peer_shapes["bytes_per_source"] / r["kernel_avg_us"] / 1e3
-                                              / HBM_PEAK_GBS, 4)
-                        r["same_outputs"] = int(max_over_pes(0 if r["same_outputs"] else 1)) == 0
-                    best = min(peer_shapes["rows"], key=lambda r: r["kernel_avg_us"])
-                    peer_shapes["fastest"] = best["shape"]
-                    if shared_gpu:
-                        peer_shapes["rehearsal_same_gpu"] = True
-                    peer_shapes["note"] = ("config 3's every-member fold with N-1 sources on peers, at the library's "
-                                           "launch shape and at tools/libpeershapes.so's (same kernel template), all "
-                                           "PEs at once; kernel_avg_us max over PEs; same_outputs: every output equal "
-                                           "to the library's on every PE")
-            else:
-                peer_shapes = {"not_applicable": "the shape variants are 4- and 8-source folds (N = %d)" % npes}
+        xgmi_ceiling = extra.get("xgmi_ceiling")
+        peer_shapes = extra.get("peer_fold_shapes")
 
     # N = 1: north_star's host-memory rate -- the same call on shmem_malloc's
     # page-locked host arrays, staged over PCIe inside each call, with the

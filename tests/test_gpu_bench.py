@@ -257,10 +257,10 @@ def test_bench_line_survives_a_dying_extra_legs_job():
              "5", "--warmup", "2", "--no-cpu-baseline", "--no-small", "--no-ops", "--no-threshold-sweep",
              "--no-rccl-compare"], env=env)
     assert d["value"] > 0 and d["check"].startswith("bit-exact"), d
-    for leg in ("external_buffers", "link_probe", "collectives"):
+    legs = ("external_buffers", "link_probe", "collectives", "xgmi_ceiling", "peer_fold_shapes")
+    for leg in legs:
         assert set(d[leg]) == {"error"} and "child job" in d[leg]["error"], (leg, d[leg])
-    assert not any(isinstance(v, dict) and "error" in v for k, v in d.items()
-                   if k not in ("external_buffers", "link_probe", "collectives")), d
+    assert not any(isinstance(v, dict) and "error" in v for k, v in d.items() if k not in legs), d
 
 
 @pytest.mark.multipe

@@ -9,9 +9,16 @@ process per rank on the rank's GPU, started before the bench rank touches the
 GPU), so that a failure in one of them -- a fatal error aborts a PE -- becomes
 an "error" entry of the driver's line instead of taking the headline with it.
 
+Round 6 adds the legs that only mean something with one GPU per PE, for the
+same reason: the measured all-peers xGMI pull ceiling and the every-member
+fold's launch shapes with N-1 remote sources (bench.py xgmi_legs; not
+applicable when the PEs share a GPU, unless --force-xgmi-legs).
+
 Run with SHMEM_PE / SHMEM_NPES / SHMEM_JOB_ID / SHMEM_DEVICE set; PE 0 prints
-one JSON line {"external_buffers": ..., "link_probe": ..., "collectives": ...}.
+one JSON line {"external_buffers": ..., "link_probe": ..., "collectives": ...,
+"xgmi_ceiling": ..., "peer_fold_shapes": ...}.
 usage: extra_legs.py MiB_per_PE steps algorithm [--no-check] [--no-external] [--no-link-probe] [--no-collectives]
+       [--no-xgmi-legs] [--force-xgmi-legs]
 """
 import ctypes
 import json
@@ -24,7 +31,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "osss-gasnet_amd"), os.path.join(ROOT, "oracle")]
 import shmem_reduce  # noqa: E402
-from bench import GIB, synth  # noqa: E402  (the same synthetic values as the bench rank's)
+from bench import GIB, synth, xgmi_legs  # noqa: E402  (the same synthetic values as the bench rank's)
 
 
 def main():
@@ -34,8 +41,10 @@ def main():
     flags = set(sys.argv[4:])
     check = "--no-check" not in flags
     n = S // 8
-    # link_probe: 2 x 16 MiB, collectives: at most (1 + N) x 4 MiB
-    os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str(128 << 20))
+    # link_probe: 2 x 16 MiB, collectives: at most (1 + N) x 4 MiB; the xGMI
+    # legs: source, target and the peer fold's staggered outputs (3 x S + a bit)
+    xgmi = "--no-xgmi-legs" not in flags
+    os.environ.setdefault("SHMEM_DEVICE_HEAP_SIZE", str((3 * S if xgmi else 0) + (128 << 20)))
     os.environ.setdefault("SHMEM_DEVICE_SCRATCH_SIZE", str(96 << 20))
     shm = shmem_reduce.Shmem()
     shm.init()
@@ -192,6 +201,22 @@ def main():
         guarded("link_probe", link_probe)
     if "--no-collectives" not in flags:
         guarded("collectives", collectives)
+    if xgmi and not rccl_fallback:
+        src, dst = shm.malloc_device(S), shm.malloc_device(S)
+        if not src or not dst:
+            out["xgmi_ceiling"] = out["peer_fold_shapes"] = {"error": "shmemx_malloc_device of 2 x S failed"}
+        else:
+            shm.put(src, synth(me, np.arange(n, dtype=np.uint64)))
+            shm.barrier_all()
+            try:
+                out.update(xgmi_legs(shm, S, me, npes, src, dst, "--force-xgmi-legs" in flags, max_over_pes))
+            except Exception as e:  # noqa: BLE001 -- reported in the line
+                out["xgmi_ceiling"] = out["peer_fold_shapes"] = {"error": f"{type(e).__name__}: {e}"}
+            shm.free_device(dst)
+            shm.free_device(src)
+    elif xgmi:
+        out["xgmi_ceiling"] = out["peer_fold_shapes"] = {
+            "not_applicable": "peer heap reads failed the init self-test (RCCL fallback)"}
     shm.barrier_all()
     if me == 0:
         print(json.dumps(out), flush=True)
