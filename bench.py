@@ -282,7 +282,7 @@ def extra_legs_child(rank, world, mib, steps, algorithm, flags):
     import subprocess
     names = [k for k, f in (("external_buffers", "--no-external"), ("link_probe", "--no-link-probe"),
                             ("collectives", "--no-collectives"), ("xgmi_ceiling", "--no-xgmi-legs"),
-                            ("peer_fold_shapes", "--no-xgmi-legs")) if f not in flags]
+                            ("peer_fold_shapes", "--no-xgmi-legs"), ("config1_call", "--no-config1")) if f not in flags]
     if not names:
         return {}
     job = "xl%s-%d" % (os.environ.get("MASTER_PORT", "0"), os.getppid())
@@ -1135,6 +1135,7 @@ def main():
                                                       ("--no-link-probe", args.no_link_probe),
                                                       ("--no-collectives", args.no_collectives),
                                                       ("--no-xgmi-legs", args.no_xgmi_legs),
+                                                      ("--no-config1", args.no_small),
                                                       ("--force-xgmi-legs", args.force_xgmi_legs)) if on])
     # CPU baseline, before this process initialises the GPU; at N > 1 the
     # other ranks wait for rank 0 in the bootstrap (SHMEM_BARRIER_TIMEOUT)
@@ -1568,19 +1569,18 @@ def main():
 
     # BASELINE config 1's call through the library (2 PEs, 4 KiB int sum, host
     # and device heap): at N = 1 from fused_same_gpu's two PE processes, at
-    # N > 1 on PEs 0 and 1 of this job, beside the CPU's figure for the same call
+    # N > 1 on PEs 0 and 1 of the child job, beside the CPU's figure for the same call
     config1_call = None
     if not args.host:
         with timed_leg("config1_call", optional=solo):
-            if npes > 1:
-                sys.path.insert(0, os.path.join(ROOT, "tools"))
-                import fused_bench
-                config1_call = fused_bench.config1(shm, 4096, max_over_pes)
-                config1_call["layout"] = ("PEs 0 and 1 of this job" +
-                                          (" (sharing one GPU)" if shared_gpu else ", one GPU each"))
+            if npes > 1:   # measured in the child job (extra_legs_child)
+                config1_call = extra.get("config1_call")
+                if config1_call is not None and "error" not in config1_call:
+                    config1_call["layout"] = ("PEs 0 and 1 of this job" +
+                                              (" (sharing one GPU)" if shared_gpu else ", one GPU each"))
             elif fused and fused.get("config1"):
                 config1_call = dict(fused["config1"], layout="2 PE processes sharing this GPU (fused_same_gpu)")
-            if config1_call is not None:
+            if config1_call is not None and "error" not in config1_call:
                 cpu_c1 = (cpu or {}).get("config1", {}).get("us_per_call")
                 config1_call["cpu_us_per_call"] = cpu_c1
                 config1_call["note"] = ("BASELINE config 1's call: shmem_int_sum_to_all, 4 KiB, active set of 2 PEs; "

@@ -258,6 +258,8 @@ def test_bench_line_survives_a_dying_extra_legs_job():
              "--no-rccl-compare"], env=env)
     assert d["value"] > 0 and d["check"].startswith("bit-exact"), d
     legs = ("external_buffers", "link_probe", "collectives", "xgmi_ceiling", "peer_fold_shapes")
+    # (--no-small: no config-1 leg either)
+    assert d["config1_call"] is None, d["config1_call"]
     for leg in legs:
         assert set(d[leg]) == {"error"} and "child job" in d[leg]["error"], (leg, d[leg])
     assert not any(isinstance(v, dict) and "error" in v for k, v in d.items() if k not in legs), d

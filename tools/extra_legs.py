@@ -16,9 +16,10 @@ applicable when the PEs share a GPU, unless --force-xgmi-legs).
 
 Run with SHMEM_PE / SHMEM_NPES / SHMEM_JOB_ID / SHMEM_DEVICE set; PE 0 prints
 one JSON line {"external_buffers": ..., "link_probe": ..., "collectives": ...,
-"xgmi_ceiling": ..., "peer_fold_shapes": ...}.
+"xgmi_ceiling": ..., "peer_fold_shapes": ..., "config1_call": ...} (config 1's
+2-PE 4 KiB int sum, tools/fused_bench.py config1, also new across GPUs).
 usage: extra_legs.py MiB_per_PE steps algorithm [--no-check] [--no-external] [--no-link-probe] [--no-collectives]
-       [--no-xgmi-legs] [--force-xgmi-legs]
+       [--no-xgmi-legs] [--force-xgmi-legs] [--no-config1]
 """
 import ctypes
 import json
@@ -217,6 +218,10 @@ def main():
     elif xgmi:
         out["xgmi_ceiling"] = out["peer_fold_shapes"] = {
             "not_applicable": "peer heap reads failed the init self-test (RCCL fallback)"}
+    if "--no-config1" not in flags:   # BASELINE config 1's call on PEs 0 and 1 (tools/fused_bench.py)
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import fused_bench
+        guarded("config1_call", lambda: fused_bench.config1(shm, 4096, max_over_pes))
     shm.barrier_all()
     if me == 0:
         print(json.dumps(out), flush=True)
