@@ -312,16 +312,6 @@ void shmemi_dev_barrier (int PE_start, int stride, int PE_size, int me, int last
         shmemi_fatal ("device barrier timed out waiting for the other PEs of the active set");
 }
 
-/* The reduce-scatter leg: fold this PE's shard of every member's source
- * into its target shard -- in member order, or (ordered) in every member's
- * reference order with the other members' versions going to this PE's
- * version area on channel `chan`. Returns the launch's status (0: queued, or
- * nothing to do: empty shard). */
-/* nan_pair: this call's number among the two-member calls with the other
- * member on channel chan -- the same on both members (every member makes the
- * same collective calls) -- whose parity picks the NaN word the owner's fold
- * sets (MI355_SIG_NANFLAG_AT; it clears the other parity's, which the previous
- * call's gather has finished reading) and the other member's gather reads. */
 /* nan_pair's NaN word can carry the owner's "no NaN" to the other member:
  * the owner's signal region is mapped there and peers' stores into signal
  * regions were seen at init (without that, sig_broken: host barriers, and the
@@ -332,6 +322,11 @@ static int nan_word_ok (const struct aset *s)
     return !shmemi.sig_broken && shmemi.sigmem != NULL && shmemi.peer_sig[other_pe] != NULL;
 }
 
+/* nan_pair: this call's number among the two-member calls with the other
+ * member on channel chan -- the same on both members (every member makes the
+ * same collective calls) -- whose parity picks the NaN word the owner's fold
+ * sets (MI355_SIG_NANFLAG_AT; it clears the other parity's, which the previous
+ * call's gather has finished reading) and the other member's gather reads. */
 static long long pair_next (int chan, const struct aset *s)
 {
     if (shmemi.pair_calls == NULL) {
@@ -342,6 +337,11 @@ static long long pair_next (int chan, const struct aset *s)
     return (long long) ++shmemi.pair_calls[(size_t) chan * (size_t) shmemi.npes + (size_t) aset_pe (s, 1 - s->me)];
 }
 
+/* The reduce-scatter leg: fold this PE's shard of every member's source
+ * into its target shard -- in member order, or (ordered) in every member's
+ * reference order with the other members' versions going to this PE's
+ * version area on channel `chan`. Returns the launch's status (0: queued, or
+ * nothing to do: empty shard). */
 static int fold_shard (int op, int dtype, size_t es, size_t dst_off, size_t src_off, size_t n, const struct aset *s,
                        int ordered, long long pair_k, int chan, hipStream_t st)
 {
