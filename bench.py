@@ -1839,6 +1839,13 @@ def main():
             "rccl_compare": rccl,
             "cpu_baseline": cpu,
             "vs_cpu_baseline": round(npes * S / t_step / GIB / cpu["value"], 1) if cpu and cpu.get("value") else None,
+            "vs_cpu_baseline_note": ("N = 1: both sides run the reference algorithm's 1-PE identity copy "
+                                     "(reduce-op.c:226-229) -- one host core's memcpy against the GPU's HBM copy, "
+                                     "so the ratio is a bandwidth ratio, not a reduction's; the combining "
+                                     "comparison is cpu_baseline.eight_pe (config 3's shape on 8 host cores) beside "
+                                     "an 8-GPU line" if npes == 1 else
+                                     "the reference algorithm on %d host cores (one PE each) against %d GPUs"
+                                     % (npes, npes)),
             "headline_rotating": rotating,
             "headline_offset_target": offset_target,
             "small_call": None if t_small is None else
