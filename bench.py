@@ -1237,7 +1237,7 @@ def main():
     # kernel duration: the same K steps again with a HIP event pair attached to
     # each dominant kernel launch (hipExtLaunchKernel stamps on the library's
     # stream). Kept out of the region above: attaching events adds ~12 us of
-    # host-side latency per call (tools/overhead.py), not kernel time.
+    # host-side latency per call (tools/probes/overhead.py), not kernel time.
     shm.kernel_timing(True)
     t1 = time.perf_counter()
     steps(args.steps)

@@ -639,7 +639,7 @@ inline unsigned grid_for(uint64_t units_per_block_pass, uint64_t units, int bloc
 }
 
 // Launch shape per source count, from tools/probes/hbm_sweep.hip and
-// tools/fold_bench.py on MI355X (256 MiB per source, double sums,
+// tools/probes/fold_bench.py on MI355X (256 MiB per source, double sums,
 // non-temporal loads + `nt sc1` stores at the time; the folds store `sc1`
 // since round 2, see st16_fold; GB/s counts (k+1) x 256 MiB;
 // profiles/r01/hbm_sweep_v5.txt, fold_bench_k_sources.jsonl):

@@ -4,7 +4,7 @@ symmetric-heap buffers, per message size. One JSON line per (kind, size) on
 PE 0.
 
     python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
-        --master-addr 127.0.0.1 --master-port 29655 tools/external_bench.py
+        --master-addr 127.0.0.1 --master-port 29655 tools/probes/external_bench.py
 """
 import ctypes
 import json
@@ -14,7 +14,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "osss-gasnet_amd"))
 import shmem_reduce  # noqa: E402
 

@@ -2,7 +2,7 @@
 # Fused one-launch kernel vs the multi-launch P2P schedule at mid sizes, with
 # PEs sharing this GPU (tools/fused_bench.py, one process per PE), run from
 # the repo root on the GPU box:
-#   tools/fused_sweep.sh OUTDIR [npes...]
+#   tools/probes/fused_sweep.sh OUTDIR [npes...]
 # For each PE count: the default thresholds (fused up to SHMEM_FUSED_MAX_BYTES
 # = 1 MiB, multi-launch above) and every size forced onto the fused kernel
 # (SHMEM_FUSED_MAX_BYTES=64M). One JSON line per run in OUTDIR/fused_sweep.jsonl.

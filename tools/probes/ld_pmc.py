@@ -2,13 +2,13 @@
 """Launch the every-member folds of one N = 8 reduce-scatter shape (8 sources
 x 32 MiB, 8 outputs) for long double and double sum, five times each, for a
 rocprofv3 --pmc pass (is the x87 software sum VALU-bound?). Measurement tool.
-usage: rocprofv3 --pmc <counters> -- python3 tools/ld_pmc.py"""
+usage: rocprofv3 --pmc <counters> -- python3 tools/probes/ld_pmc.py"""
 import os
 import sys
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "osss-gasnet_amd"))
 import shmem_reduce  # noqa: E402
 

@@ -6,7 +6,7 @@ algorithmic bytes 16 x 32 MiB), and through the plain 8-source fold
 back-to-back launches, GB/s and the fraction of the 8 TB/s HBM peak, so the
 pairs furthest below the roofline stand out. Inputs: gen_golden's values for
 the pair (realistic for its type, specials included). Measurement tool.
-usage: python3 tools/orders_sweep.py OUT.jsonl [op/dtype ...]   (default: all 44)"""
+usage: python3 tools/probes/orders_sweep.py OUT.jsonl [op/dtype ...]   (default: all 44)"""
 import json
 import os
 import sys
@@ -14,7 +14,7 @@ import time
 
 import numpy as np
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path[:0] = [os.path.join(ROOT, "osss-gasnet_amd"), os.path.join(ROOT, "oracle")]
 import oracle  # noqa: E402
 import shmem_reduce  # noqa: E402

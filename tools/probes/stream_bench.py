@@ -16,7 +16,7 @@ import subprocess
 import sys
 import uuid
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 CHILD = r'''
 import json, os, sys, time
 sys.path.insert(0, os.path.join(%r, "osss-gasnet_amd"))
