@@ -62,6 +62,86 @@ __global__ __launch_bounds__(kBlock) void copy_stamped(const u32x4 *s, u32x4 *d,
     }
 }
 
+// Dynamic variant: each WAVE takes chunks of 64 x U vectors from one of 8
+// per-XCD queues (queue q holds chunks q, q + 8, ...; an atomic head per
+// queue), moving on to the next queue when its own is empty. The atomic for
+// the chunk after next is issued before the next chunk's loads, so waiting
+// for its value never waits for those loads (vmcnt counts in issue order):
+// the queue costs no latency in the steady state. The last block to finish
+// resets the heads for the next launch.
+template <int U>
+__global__ __launch_bounds__(kBlock) void copy_dyn(const u32x4 *s, u32x4 *d, uint64_t nvec, unsigned *heads,
+                                                   unsigned *done_count, uint64_t *stamps) {
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    constexpr uint64_t CV = 64ull * U;
+    const uint64_t nchunks = (nvec + CV - 1) / CV;
+    const unsigned lane = threadIdx.x & 63;
+    int q = blockIdx.x & 7, tried = 1;
+    auto count_of = [&](int qq) -> uint64_t { return nchunks > (uint64_t)qq ? (nchunks - 1 - qq) / 8 + 1 : 0; };
+    auto issue = [&](int qq) -> unsigned {
+        unsigned k = 0;
+        if (lane == 0) k = __hip_atomic_fetch_add(heads + qq, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return k;
+    };
+    // chunk from a ticket of queue q, or the next queue's (blocking), or ~0
+    auto resolve = [&](unsigned ticket) -> uint64_t {
+        uint64_t k = __builtin_amdgcn_readfirstlane(ticket);
+        while (k >= count_of(q)) {
+            if (tried >= 8) return ~0ull;
+            q = (q + 1) & 7;
+            ++tried;
+            k = __builtin_amdgcn_readfirstlane(issue(q));
+        }
+        return (uint64_t)q + 8 * k;
+    };
+    uint64_t c = resolve(issue(q));
+    unsigned ticket = c != ~0ull ? issue(q) : 0u;
+    u32x4 x[U];
+    if (c != ~0ull) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = c * CV + (uint64_t)u * 64 + lane;
+            if (i < nvec) x[u] = s[i];
+        }
+    }
+    while (c != ~0ull) {
+        const uint64_t n = resolve(ticket);           // waits for the ticket only
+        if (n != ~0ull) ticket = issue(q);             // the chunk after n, before n's loads
+        u32x4 y[U];
+        if (n != ~0ull) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const uint64_t i = n * CV + (uint64_t)u * 64 + lane;
+                if (i < nvec) y[u] = s[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint64_t i = c * CV + (uint64_t)u * 64 + lane;
+            if (i < nvec) st16(d + i, x[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) x[u] = y[u];
+        c = n;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        stamps[2 * blockIdx.x] = t_start;
+        stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        const unsigned prev = __hip_atomic_fetch_add(done_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev + 1 == gridDim.x) {
+            for (int i = 0; i < 8; ++i) __hip_atomic_store(heads + i, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
+__global__ void fill(unsigned *p, uint64_t n, unsigned seed) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        p[i] = (unsigned)(i * 2654435761u) ^ seed;
+}
+
 int main() {
     const size_t S = 256ull << 20;
     const uint64_t nvec = S / 16;
@@ -69,24 +149,51 @@ int main() {
     CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     const int pairs = 5;
     std::vector<char *> bufs(2 * pairs);
-    for (auto &b : bufs) {
-        CHECK(hipMalloc((void **)&b, S));
-        CHECK(hipMemset(b, 1, S));
+    for (int i = 0; i < 2 * pairs; ++i) {
+        CHECK(hipMalloc((void **)&bufs[i], S));
+        fill<<<1024, 256>>>((unsigned *)bufs[i], S / 4, 977u * i);
     }
-    for (int bpc : {1, 2}) {
-        const unsigned grid = (unsigned)cus * bpc;
-        uint64_t *stamps;
-        CHECK(hipMalloc((void **)&stamps, 2 * grid * sizeof(uint64_t)));
-        std::vector<uint64_t> h(2 * grid);
+    unsigned *heads, *done;
+    CHECK(hipMalloc((void **)&heads, 64));
+    CHECK(hipMalloc((void **)&done, 64));
+    CHECK(hipMemset(heads, 0, 64));
+    CHECK(hipMemset(done, 0, 64));
+    uint64_t *stamps;
+    CHECK(hipMalloc((void **)&stamps, 2 * 4096 * sizeof(uint64_t)));
+    CHECK(hipDeviceSynchronize());
+    struct V { const char *name; int kind; int bpc; };   // kind 0 static<4>, 4/8/16 dyn<U>
+    const V vs[] = {{"static U4", 0, 1}, {"static U4", 0, 2}, {"dyn U4", 4, 1}, {"dyn U4", 4, 2}, {"dyn U8", 8, 1},
+                    {"dyn U8", 8, 2}, {"dyn U16", 16, 1}, {"dyn U4", 4, 4}};
+    std::vector<unsigned> hs(S / 4), hd(S / 4);
+    for (const V &v : vs) {
+        const unsigned grid = (unsigned)cus * v.bpc;
+        auto launch = [&](int p) {
+            const u32x4 *src = (const u32x4 *)bufs[2 * p];
+            u32x4 *dst = (u32x4 *)bufs[2 * p + 1];
+            switch (v.kind) {
+            case 0: copy_stamped<4><<<grid, kBlock>>>(src, dst, nvec, stamps); break;
+            case 4: copy_dyn<4><<<grid, kBlock>>>(src, dst, nvec, heads, done, stamps); break;
+            case 8: copy_dyn<8><<<grid, kBlock>>>(src, dst, nvec, heads, done, stamps); break;
+            default: copy_dyn<16><<<grid, kBlock>>>(src, dst, nvec, heads, done, stamps); break;
+            }
+        };
+        // correctness: pair 0 after a fresh fill of its target
+        CHECK(hipMemset(bufs[1], 0, S));
+        launch(0);
+        CHECK(hipDeviceSynchronize());
+        CHECK(hipMemcpy(hs.data(), bufs[0], S, hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(hd.data(), bufs[1], S, hipMemcpyDeviceToHost));
+        const bool ok = hs == hd;
         hipEvent_t e0, e1;
         CHECK(hipEventCreate(&e0));
         CHECK(hipEventCreate(&e1));
+        std::vector<uint64_t> h(2 * grid);
         for (int cold = 0; cold < 2; ++cold) {
-            std::vector<double> span, med_end, last_end, first_end, kern;
+            std::vector<double> med_end, last_end, first_end, kern;
             for (int r = 0; r < 60; ++r) {
                 const int p = cold ? r % pairs : 0;
                 CHECK(hipEventRecord(e0, 0));
-                copy_stamped<4><<<grid, kBlock>>>((const u32x4 *)bufs[2 * p], (u32x4 *)bufs[2 * p + 1], nvec, stamps);
+                launch(p);
                 CHECK(hipEventRecord(e1, 0));
                 CHECK(hipDeviceSynchronize());
                 float ms = 0;
@@ -106,19 +213,18 @@ int main() {
                 last_end.push_back(ends.back() * 0.01);
                 kern.push_back(ms * 1e3);
             }
-            auto mean = [](const std::vector<double> &v) {
-                double s = 0;
-                for (double x : v) s += x;
-                return s / v.size();
+            auto mean = [](const std::vector<double> &x) {
+                double t = 0;
+                for (double y : x) t += y;
+                return t / x.size();
             };
-            printf("{\"blocks_per_cu\": %d, \"grid\": %u, \"cold\": %s, \"kernel_event_us\": %.2f, "
-                   "\"first_block_end_us\": %.2f, \"median_block_end_us\": %.2f, \"last_block_end_us\": %.2f, "
-                   "\"tail_us\": %.2f, \"frac_event\": %.4f}\n",
-                   bpc, grid, cold ? "true" : "false", mean(kern), mean(first_end), mean(med_end), mean(last_end),
-                   mean(last_end) - mean(med_end), 2.0 * S / (mean(kern) * 1e-6) / 8e12);
+            printf("{\"variant\": \"%s\", \"blocks_per_cu\": %d, \"grid\": %u, \"cold\": %s, \"copy_ok\": %s, "
+                   "\"kernel_event_us\": %.2f, \"first_block_end_us\": %.2f, \"median_block_end_us\": %.2f, "
+                   "\"last_block_end_us\": %.2f, \"tail_us\": %.2f, \"frac_event\": %.4f}\n",
+                   v.name, v.bpc, grid, cold ? "true" : "false", ok ? "true" : "false", mean(kern), mean(first_end),
+                   mean(med_end), mean(last_end), mean(last_end) - mean(med_end), 2.0 * S / (mean(kern) * 1e-6) / 8e12);
             fflush(stdout);
         }
-        CHECK(hipFree(stamps));
     }
     for (auto b : bufs) CHECK(hipFree(b));
     return 0;
