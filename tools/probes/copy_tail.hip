@@ -143,6 +143,83 @@ __global__ __launch_bounds__(kBlock) void copy_dyn(const u32x4 *s, u32x4 *d, uin
     }
 }
 
+// Hybrid: the library's static grid-stride loop over the first part of the
+// vectors (whole passes, about 7/8), then every wave pulls chunks of the rest
+// (64 x UD vectors) from the 8 per-XCD queues: blocks that finish their static
+// share early take more of the tail. One grab per chunk, waited for at once
+// (the compiler drains the wave's loads there: the tail part only).
+template <int UD>
+__global__ __launch_bounds__(kBlock) void copy_hyb(const u32x4 *s, u32x4 *d, uint64_t nvec, uint64_t nstatic,
+                                                   unsigned *heads, unsigned *done_count, uint64_t *stamps) {
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    constexpr int UNROLL = 4;
+    const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
+    uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
+    u32x4 x[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+        const uint64_t i = base + (uint64_t)u * kBlock;
+        if (i < nstatic) x[u] = s[i];
+    }
+    while (base < nstatic) {
+        const uint64_t next = base + step;
+        u32x4 y[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = next + (uint64_t)u * kBlock;
+            if (i < nstatic) y[u] = s[i];
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = base + (uint64_t)u * kBlock;
+            if (i < nstatic) st16(d + i, x[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) x[u] = y[u];
+        base = next;
+    }
+    // the tail: chunks of CV vectors after nstatic, chunk g in queue g % 8
+    constexpr uint64_t CV = 64ull * UD;
+    const uint64_t nchunks = (nvec - nstatic + CV - 1) / CV;
+    const unsigned lane = threadIdx.x & 63;
+    auto count_of = [&](int qq) -> uint64_t { return nchunks > (uint64_t)qq ? (nchunks - 1 - qq) / 8 + 1 : 0; };
+    int q = blockIdx.x & 7;
+    for (int tried = 0; tried < 8;) {
+        unsigned k = 0;
+        if (lane == 0)
+            k = __hip_atomic_fetch_add(heads + (size_t)q * kHeadStride, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        k = __builtin_amdgcn_readfirstlane(k);
+        if (k >= count_of(q)) {
+            q = (q + 1) & 7;
+            ++tried;
+            continue;
+        }
+        const uint64_t b = nstatic + ((uint64_t)q + 8ull * k) * CV + lane;
+        u32x4 z[UD];
+        if (b + (UD - 1) * 64ull < nvec) {
+#pragma unroll
+            for (int u = 0; u < UD; ++u) z[u] = s[b + (uint64_t)u * 64];
+#pragma unroll
+            for (int u = 0; u < UD; ++u) st16(d + b + (uint64_t)u * 64, z[u]);
+        } else {
+            for (int u = 0; u < UD; ++u)
+                if (b + (uint64_t)u * 64 < nvec) st16(d + b + (uint64_t)u * 64, s[b + (uint64_t)u * 64]);
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        stamps[2 * blockIdx.x] = t_start;
+        stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        const unsigned prev = __hip_atomic_fetch_add(done_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (prev + 1 == gridDim.x) {
+            for (int i = 0; i < 8; ++i)
+                __hip_atomic_store(heads + (size_t)i * kHeadStride, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+}
+
 __global__ void fill(unsigned *p, uint64_t n, unsigned seed) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
         p[i] = (unsigned)(i * 2654435761u) ^ seed;
@@ -167,16 +244,23 @@ int main() {
     uint64_t *stamps;
     CHECK(hipMalloc((void **)&stamps, 2 * 4096 * sizeof(uint64_t)));
     CHECK(hipDeviceSynchronize());
-    struct V { const char *name; int kind; int bpc; };   // kind 0 static<4>, 4/8/16 dyn<U>
-    const V vs[] = {{"static U4", 0, 1}, {"dyn U16", 16, 1}, {"dyn U8", 8, 1}, {"dyn U8", 8, 2}, {"dyn U4", 4, 2}};
+    // kind 0 static<4>, 4/8/16 dyn<U>; 100 + t: hybrid, static share t/16, tail chunks of 64 x 8
+    struct V { const char *name; int kind; int bpc; };
+    const V vs[] = {{"static U4", 0, 1}, {"hybrid 15/16 UD8", 115, 1}, {"hybrid 14/16 UD8", 114, 1},
+                    {"hybrid 12/16 UD8", 112, 1}, {"hybrid 14/16 UD4", 214, 1}, {"hybrid 14/16 UD8", 114, 2}};
     std::vector<unsigned> hs(S / 4), hd(S / 4);
     for (const V &v : vs) {
         const unsigned grid = (unsigned)cus * v.bpc;
         auto launch = [&](int p) {
             const u32x4 *src = (const u32x4 *)bufs[2 * p];
             u32x4 *dst = (u32x4 *)bufs[2 * p + 1];
+            const uint64_t stp = (uint64_t)grid * kBlock * 4;
+            const uint64_t nst = v.kind >= 100 ? nvec * (uint64_t)(v.kind % 100) / 16 / stp * stp : 0;
             switch (v.kind) {
             case 0: copy_stamped<4><<<grid, kBlock>>>(src, dst, nvec, stamps); break;
+            case 112: case 114: case 115:
+                copy_hyb<8><<<grid, kBlock>>>(src, dst, nvec, nst, heads, done, stamps); break;
+            case 214: copy_hyb<4><<<grid, kBlock>>>(src, dst, nvec, nst, heads, done, stamps); break;
             case 4: copy_dyn<4><<<grid, kBlock>>>(src, dst, nvec, heads, done, stamps); break;
             case 8: copy_dyn<8><<<grid, kBlock>>>(src, dst, nvec, heads, done, stamps); break;
             default: copy_dyn<16><<<grid, kBlock>>>(src, dst, nvec, heads, done, stamps); break;
