@@ -158,3 +158,22 @@ def test_rccl_glue_one_rank(shm, op, dtype):
     assert same_bits(shm.get(dt, n, dtype), x, dtype)
     shm.free_device(dt)
     shm.free_device(ds)
+
+
+def test_peer_device_ptr(shm):
+    """shmemx_peer_device_ptr (round 6): this PE's own copy of a device-heap
+    object is its own address; anything outside the device heap, or a PE
+    outside the job, gives NULL (the peers' mappings are exercised by
+    bench.py's xGMI legs, tests/test_gpu_bench.py)."""
+    d = shm.malloc_device(4096)
+    try:
+        assert shm.peer_device_ptr(d, 0) == d
+        assert shm.peer_device_ptr(d + 100, 0) == d + 100
+        assert shm.peer_device_ptr(d, 1) is None and shm.peer_device_ptr(d, -1) is None
+        h = np.zeros(16)
+        assert shm.peer_device_ptr(h.ctypes.data, 0) is None
+        hs = shm.malloc(4096)
+        assert shm.peer_device_ptr(hs, 0) is None   # the host heap is not the device heap
+        shm.free(hs)
+    finally:
+        shm.free_device(d)
