@@ -62,6 +62,53 @@ __global__ __launch_bounds__(kBlock) void copy_stamped(const u32x4 *s, u32x4 *d,
     }
 }
 
+// Rotated static loop: pass k of the grid-stride loop gives block b the
+// sub-chunk (b + k) mod grid of stripe k instead of sub-chunk b, so every
+// block meets every residue of the stripe (warm, the blocks with even
+// blockIdx finished ~13 us before the odd ones: their fixed sub-chunks'
+// source lines stayed in the Infinity Cache more often).
+template <int UNROLL>
+__global__ __launch_bounds__(kBlock) void copy_rot(const u32x4 *s, u32x4 *d, uint64_t nvec, uint64_t *stamps) {
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    const uint64_t sub = (uint64_t)kBlock * UNROLL;              // vectors per sub-chunk
+    const uint64_t step = (uint64_t)gridDim.x * sub;             // vectors per stripe (pass)
+    unsigned j = blockIdx.x;                                     // this pass's sub-chunk
+    uint64_t stripe = 0;
+    uint64_t base = (uint64_t)j * sub + threadIdx.x;
+    u32x4 x[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+        const uint64_t i = base + (uint64_t)u * kBlock;
+        if (i < nvec) x[u] = s[i];
+    }
+    while (stripe < nvec) {
+        const uint64_t nstripe = stripe + step;
+        j = j + 1 == gridDim.x ? 0 : j + 1;
+        const uint64_t next = nstripe + (uint64_t)j * sub + threadIdx.x;
+        u32x4 y[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = next + (uint64_t)u * kBlock;
+            if (i < nvec) y[u] = s[i];
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = base + (uint64_t)u * kBlock;
+            if (i < nvec) st16(d + i, x[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) x[u] = y[u];
+        base = next;
+        stripe = nstripe;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        stamps[2 * blockIdx.x] = t_start;
+        stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
 // Dynamic variant: each WAVE takes chunks of 64 x U vectors from one of 8
 // per-XCD queues (queue q holds chunks q, q + 8, ...; an atomic head per
 // queue), moving on to the next queue when its own is empty. The atomic for
@@ -246,8 +293,10 @@ int main() {
     CHECK(hipDeviceSynchronize());
     // kind 0 static<4>, 4/8/16 dyn<U>; 100 + t: hybrid, static share t/16, tail chunks of 64 x 8
     struct V { const char *name; int kind; int bpc; };
-    const V vs[] = {{"static U4", 0, 1}, {"hybrid 15/16 UD8", 115, 1}, {"hybrid 14/16 UD8", 114, 1},
-                    {"hybrid 12/16 UD8", 112, 1}, {"hybrid 14/16 UD4", 214, 1}, {"hybrid 14/16 UD8", 114, 2}};
+    const bool xcd_only = getenv("COPY_TAIL_XCD") != nullptr;   // per-XCD end times of the static loop only
+    const V all[] = {{"static U4", 0, 1}, {"rotated U4", 1, 1}, {"rotated U4", 1, 2}, {"hybrid 15/16 UD8", 115, 1}, {"hybrid 14/16 UD8", 114, 1},
+                     {"hybrid 12/16 UD8", 112, 1}, {"hybrid 14/16 UD4", 214, 1}, {"hybrid 14/16 UD8", 114, 2}};
+    const std::vector<V> vs(all, all + (xcd_only ? 3 : sizeof all / sizeof all[0]));
     std::vector<unsigned> hs(S / 4), hd(S / 4);
     for (const V &v : vs) {
         const unsigned grid = (unsigned)cus * v.bpc;
@@ -258,6 +307,7 @@ int main() {
             const uint64_t nst = v.kind >= 100 ? nvec * (uint64_t)(v.kind % 100) / 16 / stp * stp : 0;
             switch (v.kind) {
             case 0: copy_stamped<4><<<grid, kBlock>>>(src, dst, nvec, stamps); break;
+            case 1: copy_rot<4><<<grid, kBlock>>>(src, dst, nvec, stamps); break;
             case 112: case 114: case 115:
                 copy_hyb<8><<<grid, kBlock>>>(src, dst, nvec, nst, heads, done, stamps); break;
             case 214: copy_hyb<4><<<grid, kBlock>>>(src, dst, nvec, nst, heads, done, stamps); break;
@@ -279,6 +329,7 @@ int main() {
         std::vector<uint64_t> h(2 * grid);
         for (int cold = 0; cold < 2; ++cold) {
             std::vector<double> med_end, last_end, first_end, kern;
+            std::vector<double> xcd_end(8, 0.0), xcd_start(8, 0.0);   // mean end / start per blockIdx % 8
             for (int r = 0; r < 60; ++r) {
                 const int p = cold ? r % pairs : 0;
                 CHECK(hipEventRecord(e0, 0));
@@ -294,6 +345,10 @@ int main() {
                 for (unsigned b = 0; b < grid; ++b) {
                     t0 = std::min(t0, h[2 * b]);
                     ends[b] = h[2 * b + 1];
+                }
+                for (unsigned b = 0; b < grid; ++b) {
+                    xcd_end[b % 8] += (h[2 * b + 1] - t0) * 0.01 / (grid / 8) / 50.0;
+                    xcd_start[b % 8] += (h[2 * b] - t0) * 0.01 / (grid / 8) / 50.0;
                 }
                 for (auto &e : ends) e -= t0;
                 std::sort(ends.begin(), ends.end());
@@ -312,6 +367,14 @@ int main() {
                    "\"last_block_end_us\": %.2f, \"tail_us\": %.2f, \"frac_event\": %.4f}\n",
                    v.name, v.bpc, grid, cold ? "true" : "false", ok ? "true" : "false", mean(kern), mean(first_end),
                    mean(med_end), mean(last_end), mean(last_end) - mean(med_end), 2.0 * S / (mean(kern) * 1e-6) / 8e12);
+            if (xcd_only) {
+                printf("{\"variant\": \"%s\", \"cold\": %s, \"mean_end_us_by_blockIdx_mod_8\": [", v.name,
+                       cold ? "true" : "false");
+                for (int x = 0; x < 8; ++x) printf("%s%.2f", x ? ", " : "", xcd_end[x]);
+                printf("], \"mean_start_us_by_blockIdx_mod_8\": [");
+                for (int x = 0; x < 8; ++x) printf("%s%.2f", x ? ", " : "", xcd_start[x]);
+                printf("]}\n");
+            }
             fflush(stdout);
         }
     }
