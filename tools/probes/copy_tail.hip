@@ -67,12 +67,15 @@ __global__ __launch_bounds__(kBlock) void copy_stamped(const u32x4 *s, u32x4 *d,
 // block meets every residue of the stripe (warm, the blocks with even
 // blockIdx finished ~13 us before the odd ones: their fixed sub-chunks'
 // source lines stayed in the Infinity Cache more often).
+// (generalized: pass k gives block b the sub-chunk ((b + k * rot) mod grid) xor xr)
 template <int UNROLL>
-__global__ __launch_bounds__(kBlock) void copy_rot(const u32x4 *s, u32x4 *d, uint64_t nvec, uint64_t *stamps) {
+__global__ __launch_bounds__(kBlock) void copy_rot(const u32x4 *s, u32x4 *d, uint64_t nvec, uint64_t *stamps,
+                                                   unsigned rot, unsigned xr) {
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     const uint64_t sub = (uint64_t)kBlock * UNROLL;              // vectors per sub-chunk
     const uint64_t step = (uint64_t)gridDim.x * sub;             // vectors per stripe (pass)
-    unsigned j = blockIdx.x;                                     // this pass's sub-chunk
+    unsigned jr = blockIdx.x;                                    // rotated index, before the xor
+    unsigned j = jr ^ xr;                                        // this pass's sub-chunk
     uint64_t stripe = 0;
     uint64_t base = (uint64_t)j * sub + threadIdx.x;
     u32x4 x[UNROLL];
@@ -83,7 +86,8 @@ __global__ __launch_bounds__(kBlock) void copy_rot(const u32x4 *s, u32x4 *d, uin
     }
     while (stripe < nvec) {
         const uint64_t nstripe = stripe + step;
-        j = j + 1 == gridDim.x ? 0 : j + 1;
+        jr = (jr + rot) % gridDim.x;
+        j = jr ^ xr;
         const uint64_t next = nstripe + (uint64_t)j * sub + threadIdx.x;
         u32x4 y[UNROLL];
 #pragma unroll
@@ -100,6 +104,50 @@ __global__ __launch_bounds__(kBlock) void copy_rot(const u32x4 *s, u32x4 *d, uin
         for (int u = 0; u < UNROLL; ++u) x[u] = y[u];
         base = next;
         stripe = nstripe;
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        stamps[2 * blockIdx.x] = t_start;
+        stamps[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
+// copy_rot without the division: the grid is a power of two, so the rotated
+// index wraps with a mask (rmask = grid - 1); the stripe loop as copy_stamped.
+template <int UNROLL>
+__global__ __launch_bounds__(kBlock) void copy_rotm(const u32x4 *s, u32x4 *d, uint64_t nvec, uint64_t *stamps,
+                                                    unsigned rot, unsigned rmask) {
+    const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
+    const uint64_t sub = (uint64_t)kBlock * UNROLL;
+    const uint64_t step = (uint64_t)gridDim.x * sub;
+    unsigned j = blockIdx.x;
+    uint64_t stripe = 0;
+    uint64_t base = (uint64_t)j * sub + threadIdx.x;
+    u32x4 x[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+        const uint64_t i = base + (uint64_t)u * kBlock;
+        if (i < nvec) x[u] = s[i];
+    }
+    while (base < nvec) {
+        stripe += step;
+        j = (j + rot) & rmask;
+        const uint64_t next = stripe + (uint64_t)j * sub + threadIdx.x;
+        u32x4 y[UNROLL];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = next + (uint64_t)u * kBlock;
+            if (i < nvec) y[u] = s[i];
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = base + (uint64_t)u * kBlock;
+            if (i < nvec) st16(d + i, x[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) x[u] = y[u];
+        base = next;
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -294,9 +342,14 @@ int main() {
     // kind 0 static<4>, 4/8/16 dyn<U>; 100 + t: hybrid, static share t/16, tail chunks of 64 x 8
     struct V { const char *name; int kind; int bpc; };
     const bool xcd_only = getenv("COPY_TAIL_XCD") != nullptr;   // per-XCD end times of the static loop only
-    const V all[] = {{"static U4", 0, 1}, {"rotated U4", 1, 1}, {"rotated U4", 1, 2}, {"hybrid 15/16 UD8", 115, 1}, {"hybrid 14/16 UD8", 114, 1},
+    // kind 1000 + 16 * rot + xor: copy_rot with that rotation and xor
+    const V all[] = {{"static U4", 0, 1}, {"mask rot 0", 2000, 1}, {"mask rot 8", 2008, 1}, {"mask rot 1", 2001, 1},
+                     {"mask rot 32", 2032, 1}, {"mask rot 8", 2008, 2},
+                     {"rot 0 xor 0", 1000, 1}, {"rot 0 xor 0", 1000, 2}, {"xor 1", 1001, 1}, {"xor 2", 1002, 1}, {"xor 4", 1004, 1},
+                     {"xor 8", 1008, 1}, {"rot 8", 1000 + 16 * 8, 1}, {"rot 2", 1000 + 16 * 2, 1},
+                     {"hybrid 15/16 UD8", 115, 1}, {"hybrid 14/16 UD8", 114, 1},
                      {"hybrid 12/16 UD8", 112, 1}, {"hybrid 14/16 UD4", 214, 1}, {"hybrid 14/16 UD8", 114, 2}};
-    const std::vector<V> vs(all, all + (xcd_only ? 3 : sizeof all / sizeof all[0]));
+    const std::vector<V> vs(all, all + (xcd_only ? 6 : sizeof all / sizeof all[0]));
     std::vector<unsigned> hs(S / 4), hd(S / 4);
     for (const V &v : vs) {
         const unsigned grid = (unsigned)cus * v.bpc;
@@ -307,13 +360,23 @@ int main() {
             const uint64_t nst = v.kind >= 100 ? nvec * (uint64_t)(v.kind % 100) / 16 / stp * stp : 0;
             switch (v.kind) {
             case 0: copy_stamped<4><<<grid, kBlock>>>(src, dst, nvec, stamps); break;
-            case 1: copy_rot<4><<<grid, kBlock>>>(src, dst, nvec, stamps); break;
+            case 1: copy_rot<4><<<grid, kBlock>>>(src, dst, nvec, stamps, 1u, 0u); break;
             case 112: case 114: case 115:
                 copy_hyb<8><<<grid, kBlock>>>(src, dst, nvec, nst, heads, done, stamps); break;
             case 214: copy_hyb<4><<<grid, kBlock>>>(src, dst, nvec, nst, heads, done, stamps); break;
+            default:
+                if (v.kind >= 2000) {
+                    copy_rotm<4><<<grid, kBlock>>>(src, dst, nvec, stamps, (unsigned)(v.kind - 2000), grid - 1);
+                    break;
+                }
+                if (v.kind >= 1000) {
+                    copy_rot<4><<<grid, kBlock>>>(src, dst, nvec, stamps, (unsigned)(v.kind - 1000) / 16,
+                                                  (unsigned)(v.kind - 1000) % 16);
+                    break;
+                }
             case 4: copy_dyn<4><<<grid, kBlock>>>(src, dst, nvec, heads, done, stamps); break;
             case 8: copy_dyn<8><<<grid, kBlock>>>(src, dst, nvec, heads, done, stamps); break;
-            default: copy_dyn<16><<<grid, kBlock>>>(src, dst, nvec, heads, done, stamps); break;
+            case 16: copy_dyn<16><<<grid, kBlock>>>(src, dst, nvec, heads, done, stamps); break;
             }
         };
         // correctness: pair 0 after a fresh fill of its target
