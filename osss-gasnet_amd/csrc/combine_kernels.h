@@ -418,10 +418,75 @@ __device__ __forceinline__ Pack<T> member_chain(const Pack<T> (&x)[NSRC], int q)
     return acc;
 }
 
+// Vector i of every member's fold, the sources' vectors of that position in x.
+template <int OP, typename T, int NSRC, bool ALL>
+__device__ __forceinline__ void orders_one(const OrdersParams &p, const Pack<T> (&x)[NSRC], uint64_t i) {
+    constexpr int V = 16 / sizeof(T);
+    if constexpr ((OP == MI355_OP_MIN || OP == MI355_OP_MAX) &&
+                  (std::is_floating_point<T>::value || std::is_same<T, x80>::value)) {
+        // When no operand is a NaN or a zero (long double: every operand
+        // a normal number), `a < b ? a : b` picks the same value bits in
+        // every order (equal numbers of these classes have one
+        // encoding): one fold serves every member. The members' orders
+        // only differ on NaNs, +-0 ties and (x87) equal values with
+        // different encodings (reduce-op.c:138-150), which take the
+        // per-member folds below (wave-uniform choice).
+        bool plain = true;
+#pragma unroll
+        for (int k = 0; k < NSRC; ++k)
+#pragma unroll
+            for (int e = 0; e < V; ++e) plain &= single_fold_ok(x[k].e[e]);
+        if (__all(plain)) {
+            Pack<T> m = x[0];
+#pragma unroll
+            for (int k = 1; k < NSRC; ++k)
+#pragma unroll
+                for (int e = 0; e < V; ++e) m.e[e] = apply<OP>(m.e[e], x[k].e[e]);
+#pragma unroll
+            for (int q = 0; q < NSRC; ++q)
+                if (ALL || p.dst[q] != nullptr) st16_fold((u32x4 *)p.dst[q] + i, m.v);
+            return;
+        }
+    }
+    // every member's chain with the fast operator forms (ops.h
+    // apply_fast), each output stored as its chain ends; a lane where
+    // any chain had a NaN come out redoes every chain with the
+    // reference's operator (member_chain, from registers, so an output
+    // aliasing its source is safe) and rewrites the outputs -- the
+    // same bits either way. For complex products this is also Annex G's recovery (the
+    // former float-only wave vote, now per lane and for every type).
+    bool redo = false;
+#pragma unroll
+    for (int q = 0; q < NSRC; ++q) {
+        if (!ALL && p.dst[q] == nullptr) continue;
+        Pack<T> acc = x[q];
+#pragma unroll
+        for (int k = 0; k < NSRC; ++k) {
+            if (k == q) continue;
+#pragma unroll
+            for (int e = 0; e < V; ++e) acc.e[e] = apply_fast<OP>(acc.e[e], x[k].e[e]);
+        }
+#pragma unroll
+        for (int e = 0; e < V; ++e) redo |= redo_needed<OP>(acc.e[e]);
+        st16_fold((u32x4 *)p.dst[q] + i, acc.v);
+    }
+    if constexpr (has_fast_form<OP, T>()) {
+        if (redo) {
+#pragma unroll 1
+            for (int q = 0; q < NSRC; ++q) {
+                u32x4 *dq = (u32x4 *)p.dst[0];
+#pragma unroll
+                for (int k = 1; k < NSRC; ++k) dq = q == k ? (u32x4 *)p.dst[k] : dq;
+                if (!ALL && dq == nullptr) continue;
+                st16_fold(dq + i, member_chain<OP, T, NSRC>(x, q).v);
+            }
+        }
+    }
+}
+
 // The vector loop of combine_orders_vec (SHIFT: as fold_vectors).
 template <int OP, typename T, int NSRC, int UNROLL, int POL, bool ALL, bool SHIFT>
 __device__ __forceinline__ void orders_vectors(const OrdersParams &p) {
-    constexpr int V = 16 / sizeof(T);
     const uint64_t nvec = p.nvec;
     const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
     const u32x4 *sb[NSRC];
@@ -442,68 +507,53 @@ __device__ __forceinline__ void orders_vectors(const OrdersParams &p) {
 #pragma unroll
         for (int u = 0; u < UNROLL; ++u) {
             const uint64_t i = base + (uint64_t)u * kBlock;
-            if (i >= nvec) continue;
-            if constexpr ((OP == MI355_OP_MIN || OP == MI355_OP_MAX) &&
-                          (std::is_floating_point<T>::value || std::is_same<T, x80>::value)) {
-                // When no operand is a NaN or a zero (long double: every operand
-                // a normal number), `a < b ? a : b` picks the same value bits in
-                // every order (equal numbers of these classes have one
-                // encoding): one fold serves every member. The members' orders
-                // only differ on NaNs, +-0 ties and (x87) equal values with
-                // different encodings (reduce-op.c:138-150), which take the
-                // per-member folds below (wave-uniform choice).
-                bool plain = true;
+            if (i < nvec) orders_one<OP, T, NSRC, ALL>(p, x[u], i);
+        }
+    }
+}
+
+// The same loop with the next pass's loads issued before this pass's folds
+// and stores (the copy loop's pipelining, copy_segments): a wave keeps loads
+// in flight while it folds, so few waves per CU can stream.
+template <int OP, typename T, int NSRC, int UNROLL, int POL, bool ALL, bool SHIFT>
+__device__ __forceinline__ void orders_vectors_pipe(const OrdersParams &p) {
+    const uint64_t nvec = p.nvec;
+    const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
+    const u32x4 *sb[NSRC];
 #pragma unroll
-                for (int k = 0; k < NSRC; ++k)
+    for (int k = 0; k < NSRC; ++k) sb[k] = (const u32x4 *)p.src[k];
+    uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
+    Pack<T> x[UNROLL][NSRC];
 #pragma unroll
-                    for (int e = 0; e < V; ++e) plain &= single_fold_ok(x[u][k].e[e]);
-                if (__all(plain)) {
-                    Pack<T> m = x[u][0];
+    for (int u = 0; u < UNROLL; ++u) {
+        const uint64_t i = base + (uint64_t)u * kBlock;
+        if (i < nvec) {
 #pragma unroll
-                    for (int k = 1; k < NSRC; ++k)
+            for (int k = 0; k < NSRC; ++k) x[u][k].v = ld16_src<POL, SHIFT>(sb[k], i);
+        }
+    }
+    while (base < nvec) {
+        const uint64_t next = base + step;
+        Pack<T> y[UNROLL][NSRC];
 #pragma unroll
-                        for (int e = 0; e < V; ++e) m.e[e] = apply<OP>(m.e[e], x[u][k].e[e]);
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = next + (uint64_t)u * kBlock;
+            if (i < nvec) {
 #pragma unroll
-                    for (int q = 0; q < NSRC; ++q)
-                        if (ALL || p.dst[q] != nullptr) st16_fold((u32x4 *)p.dst[q] + i, m.v);
-                    continue;
-                }
-            }
-            // every member's chain with the fast operator forms (ops.h
-            // apply_fast), each output stored as its chain ends; a lane where
-            // any chain had a NaN come out redoes every chain with the
-            // reference's operator (member_chain, from registers, so an output
-            // aliasing its source is safe) and rewrites the outputs -- the
-            // same bits either way. For complex products this is also Annex G's recovery (the
-            // former float-only wave vote, now per lane and for every type).
-            bool redo = false;
-#pragma unroll
-            for (int q = 0; q < NSRC; ++q) {
-                if (!ALL && p.dst[q] == nullptr) continue;
-                Pack<T> acc = x[u][q];
-#pragma unroll
-                for (int k = 0; k < NSRC; ++k) {
-                    if (k == q) continue;
-#pragma unroll
-                    for (int e = 0; e < V; ++e) acc.e[e] = apply_fast<OP>(acc.e[e], x[u][k].e[e]);
-                }
-#pragma unroll
-                for (int e = 0; e < V; ++e) redo |= redo_needed<OP>(acc.e[e]);
-                st16_fold((u32x4 *)p.dst[q] + i, acc.v);
-            }
-            if constexpr (has_fast_form<OP, T>()) {
-                if (redo) {
-#pragma unroll 1
-                    for (int q = 0; q < NSRC; ++q) {
-                        u32x4 *dq = (u32x4 *)p.dst[0];
-#pragma unroll
-                        for (int k = 1; k < NSRC; ++k) dq = q == k ? (u32x4 *)p.dst[k] : dq;
-                        if (!ALL && dq == nullptr) continue;
-                        st16_fold(dq + i, member_chain<OP, T, NSRC>(x[u], q).v);
-                    }
-                }
+                for (int k = 0; k < NSRC; ++k) y[u][k].v = ld16_src<POL, SHIFT>(sb[k], i);
             }
         }
+        __builtin_amdgcn_sched_barrier(0);   // the next pass's loads first
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = base + (uint64_t)u * kBlock;
+            if (i < nvec) orders_one<OP, T, NSRC, ALL>(p, x[u], i);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+            for (int k = 0; k < NSRC; ++k) x[u][k] = y[u][k];
+        base = next;
     }
 }
 
@@ -680,20 +730,30 @@ template <int OP, int NSRC, typename T> struct ShapeOp : Shape<NSRC, T> {
 // max 86.2 -> 82.7 us at two -> one, profiles/r02/orders_vs_fold_alu_shapes.jsonl).
 // 3-4 sources of min/max or complex products: eight blocks per CU (alu4:
 // float max 95.2 -> 81.2 us, complex double product 102.7 -> 80.7 at 4 x 64 MiB).
+// 8 sources (every PE's shard at N = 8), real and integer types: one vector
+// per lane and one block per CU, as the 4-source fold and the copy -- the
+// 8 loads and 8 stores per vector are 16 streams, and a small resident grid
+// sweeping them in order keeps HBM's rows open: 8 x 32 MiB -> 8 from HBM
+// 93.5 -> 90.3 us (double sum), 97.7 -> 90.9 (float max), 93.1 -> 89.8
+// (float sum), 96.9 -> 90.6 (double max); at 8 x 8 MiB within +-2 %, float
+// max 25.3 -> 24.6 (profiles/r06/orders_window/; the k-source fold's
+// shape, 4 vectors per lane at 8 blocks per CU, was tuned with one output).
 template <int OP, int NSRC, typename T> struct OrdersShape {
     static constexpr bool cplx = std::is_same<T, cplxf>::value || std::is_same<T, cplxd>::value;
     static constexpr bool sel = (OP == MI355_OP_MIN || OP == MI355_OP_MAX) && NSRC >= 5;
     using S = Shape<NSRC, T>;
     static constexpr bool alu_heavy = S::alu_heavy;
+    static constexpr bool stream8 = NSRC == 8 && !S::alu_heavy && !cplx;
     // 3-4 sources with compare-select chains or complex products: the sum's
     // shape there (one block per CU) leaves too few waves to hide their ALU
     // latency; eight blocks per CU
     static constexpr bool alu4 = !S::alu_heavy && NSRC >= 3 && NSRC <= 4 &&
                                  (OP == MI355_OP_MIN || OP == MI355_OP_MAX || (cplx && OP == MI355_OP_PROD));
-    static constexpr int unroll = cplx ? 1 : alu4 ? 2 : sel && S::unroll > 2 ? 1 : S::unroll;
-    static constexpr int blocks_per_cu = alu4 ? 8
-                                         : cplx ? (S::blocks_per_cu * S::unroll < 8 ? S::blocks_per_cu * S::unroll : 8)
-                                                : S::blocks_per_cu;
+    static constexpr int unroll = cplx || stream8 ? 1 : alu4 ? 2 : sel && S::unroll > 2 ? 1 : S::unroll;
+    static constexpr int blocks_per_cu = alu4      ? 8
+                                         : stream8 ? 1
+                                         : cplx    ? (S::blocks_per_cu * S::unroll < 8 ? S::blocks_per_cu * S::unroll : 8)
+                                                   : S::blocks_per_cu;
     static constexpr int policy = POL_NT_LOAD;
 };
 

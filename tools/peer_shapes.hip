@@ -2,8 +2,8 @@
 // for bench.py's `peer_fold_shapes` leg (a measurement probe, not part of the
 // library; tools/libpeershapes.so, built by tools/Makefile `peershapes`).
 //
-// Why: the fold's launch shape (combine_kernels.h Shape<8> / OrdersShape: 4
-// vectors per lane, 8 blocks per CU) was tuned with all 8 sources in local
+// Why: the fold's launch shape (combine_kernels.h OrdersShape: 1 vector per
+// lane, 1 block per CU at 4 and 8 sources) was tuned with all sources in local
 // HBM. In BASELINE config 3 at N = 8 each GPU folds its shard with 7 of its 8
 // sources on other GPUs, read over xGMI with several times HBM's latency, so
 // the bytes in flight per CU that hide it may differ. This library
@@ -28,15 +28,26 @@ namespace {
 using namespace mi355k;
 
 struct Variant {
-    int unroll, bpc;
+    int unroll, bpc, pipe;  // pipe: the pipelined loop (orders_vectors_pipe), a probe-only kernel
 };
-// the library's shape first (4, 8), then fewer vectors per lane with more
-// blocks, and the deeper queue with more blocks queued
-constexpr Variant kVariants[] = {{4, 8}, {2, 8}, {1, 16}, {2, 16}, {4, 16}};
+// the library's shape is one vector per lane and one block per CU at 4 and
+// (since round 6) 8 sources: the 8-source shape of rounds 1-5 (4, 8), then
+// more bytes in flight per CU in steps -- more blocks, more vectors per lane
+// -- for xGMI's latency
+// (a probe build may pass its own list: -DPEER_SHAPES_VARIANTS='{1, 1}, {2, 1}')
+#ifndef PEER_SHAPES_VARIANTS
+#define PEER_SHAPES_VARIANTS {4, 8}, {1, 2}, {1, 4}, {2, 8}, {1, 16}
+#endif
+constexpr Variant kVariants[] = {PEER_SHAPES_VARIANTS};
 constexpr int kCount = sizeof(kVariants) / sizeof(kVariants[0]);
 
 template <int OP, typename T, int NSRC, int U>
-int run(int bpc, void *const *dsts, const void *const *srcs, size_t n, hipEvent_t e0, hipEvent_t e1,
+__global__ __launch_bounds__(kBlock) void orders_pipe_kernel(OrdersParams p) {
+    orders_vectors_pipe<OP, T, NSRC, U, POL_NT_LOAD, true, false>(p);
+}
+
+template <int OP, typename T, int NSRC, int U>
+int run(int bpc, int pipe, void *const *dsts, const void *const *srcs, size_t n, hipEvent_t e0, hipEvent_t e1,
         hipStream_t st) {
     OrdersParams p{};
     for (int k = 0; k < NSRC; ++k) {
@@ -44,7 +55,7 @@ int run(int bpc, void *const *dsts, const void *const *srcs, size_t n, hipEvent_
         p.dst[k] = dsts[k];
     }
     p.nvec = n / (16 / sizeof(T));
-    auto kern = combine_orders_vec<OP, T, NSRC, U, POL_NT_LOAD, true>;
+    auto kern = pipe ? orders_pipe_kernel<OP, T, NSRC, U> : combine_orders_vec<OP, T, NSRC, U, POL_NT_LOAD, true>;
     const unsigned grid = grid_for((uint64_t)kBlock * U, p.nvec, bpc);
     hipExtLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, e0, e1, 0, p);
     const hipError_t e = hipGetLastError();
@@ -55,9 +66,9 @@ template <int OP, typename T, int NSRC>
 int dispatch(int v, void *const *dsts, const void *const *srcs, size_t n, hipEvent_t e0, hipEvent_t e1,
              hipStream_t st) {
     switch (kVariants[v].unroll) {
-    case 1: return run<OP, T, NSRC, 1>(kVariants[v].bpc, dsts, srcs, n, e0, e1, st);
-    case 2: return run<OP, T, NSRC, 2>(kVariants[v].bpc, dsts, srcs, n, e0, e1, st);
-    case 4: return run<OP, T, NSRC, 4>(kVariants[v].bpc, dsts, srcs, n, e0, e1, st);
+    case 1: return run<OP, T, NSRC, 1>(kVariants[v].bpc, kVariants[v].pipe, dsts, srcs, n, e0, e1, st);
+    case 2: return run<OP, T, NSRC, 2>(kVariants[v].bpc, kVariants[v].pipe, dsts, srcs, n, e0, e1, st);
+    case 4: return run<OP, T, NSRC, 4>(kVariants[v].bpc, kVariants[v].pipe, dsts, srcs, n, e0, e1, st);
     default: return -1;
     }
 }
@@ -65,6 +76,8 @@ int dispatch(int v, void *const *dsts, const void *const *srcs, size_t n, hipEve
 }  // namespace
 
 extern "C" int peer_shapes_count(void) { return kCount; }
+
+extern "C" int peer_shapes_pipe(int v) { return v < 0 || v >= kCount ? -1 : kVariants[v].pipe; }
 
 extern "C" int peer_shapes_describe(int v, int *unroll, int *blocks_per_cu) {
     if (v < 0 || v >= kCount) return -1;
@@ -92,3 +105,18 @@ extern "C" int peer_shapes_orders_float_max(int v, void *const *dsts, const void
         if (((uintptr_t)dsts[k] | (uintptr_t)srcs[k]) & 15) return -1;
     return dispatch<MI355_OP_MAX, float, 8>(v, dsts, srcs, n, e0, e1, st);
 }
+
+// More pairs for the every-member fold's shape probe (tools/probes/orders_shapes_cold.py):
+// 8 sources, n a whole number of 16-byte vectors.
+#define PEER_SHAPES_PAIR(NAME, OP, T)                                                                             \
+    extern "C" int NAME(int v, void *const *dsts, const void *const *srcs, size_t n, hipEvent_t e0, hipEvent_t e1, \
+                        hipStream_t st) {                                                                          \
+        if (v < 0 || v >= kCount || n % (16 / sizeof(T)) != 0) return -1;                                         \
+        for (int k = 0; k < 8; ++k)                                                                                \
+            if (((uintptr_t)dsts[k] | (uintptr_t)srcs[k]) & 15) return -1;                                         \
+        return dispatch<OP, T, 8>(v, dsts, srcs, n, e0, e1, st);                                                   \
+    }
+PEER_SHAPES_PAIR(peer_shapes_orders_double_max, MI355_OP_MAX, double)
+PEER_SHAPES_PAIR(peer_shapes_orders_float_sum, MI355_OP_SUM, float)
+PEER_SHAPES_PAIR(peer_shapes_orders_double_prod, MI355_OP_PROD, double)
+PEER_SHAPES_PAIR(peer_shapes_orders_int_sum, MI355_OP_SUM, int)

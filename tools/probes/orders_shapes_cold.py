@@ -39,7 +39,8 @@ def main():
     shm = shmem_reduce.Shmem()
     shm.init()
     L, vp = shm.lib, ctypes.c_void_p
-    P = ctypes.CDLL(os.path.join(ROOT, "tools", "libpeershapes.so"))
+    # SHAPES_LIB: another build of tools/peer_shapes.hip with its own shape list
+    P = ctypes.CDLL(os.environ.get("SHAPES_LIB", os.path.join(ROOT, "tools", "libpeershapes.so")))
     for f in (P.peer_shapes_orders_float_max,):
         f.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.c_size_t, vp, vp, vp]
     P.peer_shapes_orders_double_sum.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp),
@@ -51,8 +52,11 @@ def main():
     for e in ev:
         L.hipEventCreate(ctypes.byref(e))
     u, b = ctypes.c_int(), ctypes.c_int()
-    for op, dtype, nb in (("max", "float", 8 << 20), ("max", "float", 32 << 20), ("sum", "double", 8 << 20)):
-        es = 4 if dtype == "float" else 8
+    # SHAPES_CASES: op:dtype:MiB,... (default: the three below)
+    cases = [(c.split(":")[0], c.split(":")[1], int(c.split(":")[2]) << 20)
+             for c in os.environ.get("SHAPES_CASES", "max:float:8,max:float:32,sum:double:8").split(",")]
+    for op, dtype, nb in cases:
+        es = 4 if dtype in ("float", "int") else 8
         n = nb // es
         span = nb + STAGGER
         set_bytes = 16 * span
@@ -61,7 +65,9 @@ def main():
         assert L.hipMalloc(ctypes.byref(pool), ctypes.c_size_t(sets * set_bytes)) == 0
         base = pool.value
         x = np.random.default_rng(5).random(n * 8) - 0.5
-        xs = x.astype(np.float32) if dtype == "float" else x
+        xs = x.astype(np.float32) if dtype == "float" else (x * 2**31).astype(np.int32) if dtype == "int" else x
+        if op == "prod":
+            xs = (1.0 + x * 1e-3).astype(xs.dtype)
         for j in range(sets):
             for q in range(8):
                 shm.put(base + j * set_bytes + q * span, xs[q * n:(q + 1) * n])
@@ -75,9 +81,11 @@ def main():
             if v < 0:
                 return lambda j, e0, e1: (L.mi355_time_next_launch(e0, e1) if e0 else None,
                                           shm.combine_orders(op, dtype, bufs(j)[2], bufs(j)[3], n))[1]
-            if dtype == "float":
-                return lambda j, e0, e1: P.peer_shapes_orders_float_max(v, bufs(j)[0], bufs(j)[1], n, e0, e1, None)
-            return lambda j, e0, e1: P.peer_shapes_orders_double_sum(v, 8, bufs(j)[0], bufs(j)[1], n, e0, e1, None)
+            if (op, dtype) == ("sum", "double"):
+                return lambda j, e0, e1: P.peer_shapes_orders_double_sum(v, 8, bufs(j)[0], bufs(j)[1], n, e0, e1, None)
+            f = getattr(P, f"peer_shapes_orders_{dtype}_{op}")
+            f.argtypes = [ctypes.c_int, ctypes.POINTER(vp), ctypes.POINTER(vp), ctypes.c_size_t, vp, vp, vp]
+            return lambda j, e0, e1: f(v, bufs(j)[0], bufs(j)[1], n, e0, e1, None)
 
         def timed(f, cold):
             for j in range(sets):
@@ -109,6 +117,8 @@ def main():
             if v >= 0:
                 P.peer_shapes_describe(v, ctypes.byref(u), ctypes.byref(b))
                 shape = f"{u.value} vectors/lane, {b.value} blocks/CU"
+                if hasattr(P, "peer_shapes_pipe") and P.peer_shapes_pipe(v) == 1:
+                    shape += ", pipelined"
             else:
                 shape = "library"
             print(json.dumps({"kernel": f"combine_orders_vec<{op},{dtype},8>", "bytes_per_source": nb, "shape": shape,
