@@ -8,8 +8,10 @@ entry records the hash of the gfx950 code objects it was taken from
 (shmem_reduce.kernel_code_hash): bench.py reports an entry's traffic only
 for a library with the same machine code.
 
-usage: pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR MIN_GRID[:MAX_GRID] KEY [out.json]
-(grid in threads: launches of one kernel at different sizes told apart)
+usage: pmc_traffic.py FETCH_DIR WRITE_DIR KERNEL_SUBSTR MIN_GRID[:MAX_GRID][@MIN_B:MAX_B] KEY [out.json]
+(grid in threads: launches of one kernel at different sizes told apart; a
+kernel launched with one grid at several sizes is told apart by @MIN_B:MAX_B,
+the dispatch's own bytes in each pass -- FETCH_SIZE doubled, WRITE_SIZE)
 """
 import csv
 import glob
@@ -33,13 +35,24 @@ def per_dispatch(d, counter, kname, min_grid, max_grid=1 << 62):
     return list(vals.values())
 
 
+def in_bytes(vals, scale, brange):
+    """Dispatches whose counter, as bytes (x scale), lies in brange."""
+    return [v for v in vals if brange[0] <= v * scale <= brange[1]]
+
+
 def main():
     fdir, wdir, kname, grid, key = sys.argv[1:6]
     out = sys.argv[6] if len(sys.argv) > 6 else None
+    grid, _, bsel = grid.partition("@")
     lo, _, hi = grid.partition(":")
     rng = (int(lo), int(hi) if hi else 1 << 62)
     f = per_dispatch(fdir, "FETCH_SIZE", kname, *rng)
     w = per_dispatch(wdir, "WRITE_SIZE", kname, *rng)
+    if bsel:
+        blo, _, bhi = bsel.partition(":")
+        brange = (int(blo), int(bhi) if bhi else 1 << 62)
+        f = in_bytes(f, 2 * 1024, brange)
+        w = in_bytes(w, 1024, brange)
     if not f or not w:
         sys.exit(f"no dispatches of {kname}: fetch {len(f)} write {len(w)}")
     fetch = sorted(f)[len(f) // 2] * 1024

@@ -35,6 +35,8 @@ timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TA_BUSY_avr --output-
 J=gpurun_out/profiles/pmc_traffic.json
 cp profiles/pmc_traffic.json "$J" 2>/dev/null || true
 # key, kernel-name substring (~ = space), minimum grid (threads) of the launches to count
+# (since round 6 the 8-source double sum runs one block per CU at every size: its two legs
+# are told apart by their bytes per pass, 256 MiB read + 256 MiB written vs 64 + 64)
 while read -r key sub grid; do
     python3 tools/pmc_traffic.py "$OUT/fetch" "$OUT/write" "${sub//\~/ }" "$grid" "$key" "$J" > /dev/null
 done <<'EOF'
@@ -42,8 +44,8 @@ n1_256mib copy_segments<4,~1> 1000
 offset_target_copy_shift copy_segments_shift<4,~1> 1000
 kernel_fold_k2_double_sum combine_vec<0,~double,~2, 1000
 kernel_fold_k8_double_sum combine_vec<0,~double,~8, 1000
-kernel_rs_shard_n8_double_sum combine_orders_vec<0,~double,~8, 300000
-kernel_rs_shard_n8_double_sum_8mib combine_orders_vec<0,~double,~8, 1000:300000
+kernel_rs_shard_n8_double_sum combine_orders_vec<0,~double,~8, 1000@134217729
+kernel_rs_shard_n8_double_sum_8mib combine_orders_vec<0,~double,~8, 1000@1:134217728
 kernel_fold_k8_float_max combine_vec<6,~float,~8, 1000
 kernel_fold_k8_longlong_and combine_vec<2,~long,~8, 300000
 kernel_rs_shard_n8_longlong_and combine_vec<2,~long,~8, 1000:300000
