@@ -730,20 +730,23 @@ template <int OP, int NSRC, typename T> struct ShapeOp : Shape<NSRC, T> {
 // max 86.2 -> 82.7 us at two -> one, profiles/r02/orders_vs_fold_alu_shapes.jsonl).
 // 3-4 sources of min/max or complex products: eight blocks per CU (alu4:
 // float max 95.2 -> 81.2 us, complex double product 102.7 -> 80.7 at 4 x 64 MiB).
-// 8 sources (every PE's shard at N = 8), real and integer types: one vector
-// per lane and one block per CU, as the 4-source fold and the copy -- the
-// 8 loads and 8 stores per vector are 16 streams, and a small resident grid
-// sweeping them in order keeps HBM's rows open: 8 x 32 MiB -> 8 from HBM
-// 93.5 -> 90.3 us (double sum), 97.7 -> 90.9 (float max), 93.1 -> 89.8
-// (float sum), 96.9 -> 90.6 (double max); at 8 x 8 MiB within +-2 %, float
-// max 25.3 -> 24.6 (profiles/r06/orders_window/; the k-source fold's
-// shape, 4 vectors per lane at 8 blocks per CU, was tuned with one output).
+// 8 sources (every PE's shard at N = 8) of sums, products and bitwise
+// operators on real and integer types: one vector per lane and one block per
+// CU, as the 4-source fold and the copy -- the 8 loads and 8 stores per
+// vector are 16 streams, and a small resident grid sweeping them in order
+// keeps HBM's rows open: 8 x 32 MiB -> 8 from HBM 93.5 -> 90.3 us (double
+// sum), 93.1 -> 89.8 (float sum), 93.1 -> 89.6 (double product); at 8 x 8
+// MiB within +-2 % (profiles/r06/orders_window/; the k-source fold's shape,
+// 4 vectors per lane at 8 blocks per CU, was tuned with one output). Not
+// min/max: their per-member chains run whenever a vector holds a NaN or a
+// zero, and one wave per SIMD does not hide those (bench.py's float max leg,
+// whose floats are doubles' bytes: 8 x 8 MiB 21.5 -> 26.5 us warm).
 template <int OP, int NSRC, typename T> struct OrdersShape {
     static constexpr bool cplx = std::is_same<T, cplxf>::value || std::is_same<T, cplxd>::value;
     static constexpr bool sel = (OP == MI355_OP_MIN || OP == MI355_OP_MAX) && NSRC >= 5;
     using S = Shape<NSRC, T>;
     static constexpr bool alu_heavy = S::alu_heavy;
-    static constexpr bool stream8 = NSRC == 8 && !S::alu_heavy && !cplx;
+    static constexpr bool stream8 = NSRC == 8 && !S::alu_heavy && !cplx && !sel;
     // 3-4 sources with compare-select chains or complex products: the sum's
     // shape there (one block per CU) leaves too few waves to hide their ALU
     // latency; eight blocks per CU
