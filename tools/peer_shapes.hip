@@ -120,3 +120,34 @@ PEER_SHAPES_PAIR(peer_shapes_orders_double_max, MI355_OP_MAX, double)
 PEER_SHAPES_PAIR(peer_shapes_orders_float_sum, MI355_OP_SUM, float)
 PEER_SHAPES_PAIR(peer_shapes_orders_double_prod, MI355_OP_PROD, double)
 PEER_SHAPES_PAIR(peer_shapes_orders_int_sum, MI355_OP_SUM, int)
+
+// The plain k-source fold (one output; combine_vec) at the same shapes, for the order-free
+// operators' shard at N = 8 (BASELINE config 4's longlong and: 8 x 8 MiB -> 1); probe only.
+namespace {
+template <int U>
+int fold_run(int bpc, void *dst, const void *const *srcs, size_t n, hipEvent_t e0, hipEvent_t e1, hipStream_t st) {
+    CombineParams p{};
+    p.dst = dst;
+    for (int k = 0; k < 8; ++k) p.src[k] = srcs[k];
+    p.nvec = n / 2;
+    auto kern = combine_vec<MI355_OP_AND, long, 8, U, POL_NT_LOAD>;
+    const unsigned grid = grid_for((uint64_t)kBlock * U, p.nvec, bpc);
+    hipExtLaunchKernelGGL(kern, dim3(grid), dim3(kBlock), 0, st, e0, e1, 0, p);
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : (int)e;
+}
+}  // namespace
+
+extern "C" int peer_shapes_fold_long_and(int v, void *dst, const void *const *srcs, size_t n, hipEvent_t e0,
+                                         hipEvent_t e1, hipStream_t st) {
+    if (v < 0 || v >= kCount || n % 2 != 0 || kVariants[v].pipe) return -1;
+    if ((uintptr_t)dst & 15) return -1;
+    for (int k = 0; k < 8; ++k)
+        if ((uintptr_t)srcs[k] & 15) return -1;
+    switch (kVariants[v].unroll) {
+    case 1: return fold_run<1>(kVariants[v].bpc, dst, srcs, n, e0, e1, st);
+    case 2: return fold_run<2>(kVariants[v].bpc, dst, srcs, n, e0, e1, st);
+    case 4: return fold_run<4>(kVariants[v].bpc, dst, srcs, n, e0, e1, st);
+    default: return -1;
+    }
+}
