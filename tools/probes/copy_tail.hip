@@ -27,10 +27,12 @@ __device__ __forceinline__ void st16(u32x4 *p, u32x4 v) {
 }
 
 template <int UNROLL>
-__global__ __launch_bounds__(kBlock) void copy_stamped(const u32x4 *s, u32x4 *d, uint64_t nvec, uint64_t *stamps) {
+__global__ __launch_bounds__(kBlock) void copy_stamped(const u32x4 *s, u32x4 *d, uint64_t nvec, uint64_t *stamps,
+                                                       unsigned remap = 0) {
     const uint64_t t_start = __builtin_amdgcn_s_memrealtime();
     const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
-    uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
+    // remap (probe): block b copies block (b ^ remap)'s sub-chunks, the loop unchanged
+    uint64_t base = (uint64_t)(blockIdx.x ^ remap) * kBlock * UNROLL + threadIdx.x;
     u32x4 x[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
@@ -343,13 +345,14 @@ int main() {
     struct V { const char *name; int kind; int bpc; };
     const bool xcd_only = getenv("COPY_TAIL_XCD") != nullptr;   // per-XCD end times of the static loop only
     // kind 1000 + 16 * rot + xor: copy_rot with that rotation and xor
-    const V all[] = {{"static U4", 0, 1}, {"mask rot 0", 2000, 1}, {"mask rot 8", 2008, 1}, {"mask rot 1", 2001, 1},
+    const V all[] = {{"static U4", 0, 1}, {"static xor 1", 3001, 1}, {"static xor 2", 3002, 1}, {"static xor 4", 3004, 1},
+                     {"static xor 8", 3008, 1}, {"mask rot 0", 2000, 1}, {"mask rot 8", 2008, 1}, {"mask rot 1", 2001, 1},
                      {"mask rot 32", 2032, 1}, {"mask rot 8", 2008, 2},
                      {"rot 0 xor 0", 1000, 1}, {"rot 0 xor 0", 1000, 2}, {"xor 1", 1001, 1}, {"xor 2", 1002, 1}, {"xor 4", 1004, 1},
                      {"xor 8", 1008, 1}, {"rot 8", 1000 + 16 * 8, 1}, {"rot 2", 1000 + 16 * 2, 1},
                      {"hybrid 15/16 UD8", 115, 1}, {"hybrid 14/16 UD8", 114, 1},
                      {"hybrid 12/16 UD8", 112, 1}, {"hybrid 14/16 UD4", 214, 1}, {"hybrid 14/16 UD8", 114, 2}};
-    const std::vector<V> vs(all, all + (xcd_only ? 6 : sizeof all / sizeof all[0]));
+    const std::vector<V> vs(all, all + (xcd_only ? 5 : sizeof all / sizeof all[0]));
     std::vector<unsigned> hs(S / 4), hd(S / 4);
     for (const V &v : vs) {
         const unsigned grid = (unsigned)cus * v.bpc;
@@ -365,6 +368,10 @@ int main() {
                 copy_hyb<8><<<grid, kBlock>>>(src, dst, nvec, nst, heads, done, stamps); break;
             case 214: copy_hyb<4><<<grid, kBlock>>>(src, dst, nvec, nst, heads, done, stamps); break;
             default:
+                if (v.kind >= 3000) {
+                    copy_stamped<4><<<grid, kBlock>>>(src, dst, nvec, stamps, (unsigned)(v.kind - 3000));
+                    break;
+                }
                 if (v.kind >= 2000) {
                     copy_rotm<4><<<grid, kBlock>>>(src, dst, nvec, stamps, (unsigned)(v.kind - 2000), grid - 1);
                     break;
