@@ -793,7 +793,13 @@ KERNEL_LEGS = [
     # t = fixed + bytes / rate per launch (FIXED_COST_FITS) -- why the small shards run below the big
     ("rs_shard_n8_float_max_2mib", "combine_orders_vec<max,float,8>", "max", "float", 8, 2 << 20, True),
     ("rs_shard_n8_double_sum_8mib", "combine_orders_vec<sum,double,8>", "sum", "double", 8, 8 << 20, True),
+    # config 4's every-member float max on NaN-laden floats (the doubles' bytes read as floats: a NaN in
+    # about one 16-byte vector in eight), which send min/max down their per-member chains
+    ("rs_shard_n8_float_max_nan_rich", "combine_orders_vec<max,float,8>", "max", "float", 8, 8 << 20, True),
 ]
+# float legs on the doubles' bytes read as floats; the others take the doubles' values rounded to
+# float (SURVEY 8d's config-4 recipe: finite, full mantissa)
+DOUBLE_BYTES_LEGS = {"rs_shard_n8_float_max_nan_rich"}
 # (kernel, [legs of that kernel at two or more shard sizes]) for the fixed-cost fit
 FIXED_COST_FITS = [("combine_orders_vec<max,float,8>", ["rs_shard_n8_float_max_2mib", "rs_shard_n8_float_max"]),
                    ("combine_orders_vec<sum,double,8>", ["rs_shard_n8_double_sum_8mib", "rs_shard_n8_double_sum"])]
@@ -855,9 +861,10 @@ def kernel_legs(shm, reps, check):
                    config 3 / 4 at N = 8 with the default result order -- 8
                    sources of one shard, 8 outputs (every member's reference
                    order), algorithmic bytes 16 x shard bytes.
-    Sources: (uniform - 0.5) doubles, full mantissa (the float/longlong legs
-    read the same bytes as their type; the long double legs the same values
-    widened to x87). Checked bit-exact (value bytes) against the oracle on a
+    Sources: (uniform - 0.5) doubles, full mantissa (the float legs the same
+    values rounded to float, except DOUBLE_BYTES_LEGS, which read the doubles'
+    bytes as floats; the longlong legs read the same bytes as their type; the
+    long double legs the same values widened to x87). Checked bit-exact (value bytes) against the oracle on a
     sample of every output. The long double legs also carry their VALU
     floor and the bound it implies (VALU_FLOOR)."""
     import ctypes
@@ -892,12 +899,13 @@ def kernel_legs(shm, reps, check):
     for e in ev:
         L.hipEventCreate(ctypes.byref(e))
     res = {}
-    rewritten = 0   # sources a long double / complex leg overwrote (the others read hosts' bytes)
+    rewritten = 0   # sources a float / long double / complex leg overwrote (the others read hosts' bytes)
     for name, kname, op, dtype, k, nbytes, orders in KERNEL_LEGS:
         es = np.dtype(shmem_reduce.NP[dtype]).itemsize
         n = nbytes // es
         nout = k if orders else 1
-        if dtype not in ("longdouble", "complexf"):
+        rewrites = dtype in ("longdouble", "complexf") or (dtype == "float" and name not in DOUBLE_BYTES_LEGS)
+        if not rewrites:
             for p in range(rewritten):
                 shm.put(srcs[p], hosts[p])
             rewritten = 0
@@ -905,6 +913,10 @@ def kernel_legs(shm, reps, check):
             rewritten = max(rewritten, k)
         if dtype == "longdouble":   # realistic x87 operands, not doubles' bytes read as x87
             lds = [hosts[p][:n].astype(np.longdouble) for p in range(k)]
+            for p in range(k):
+                shm.put(srcs[p], lds[p])
+        if rewrites and dtype == "float":   # finite floats, full mantissa
+            lds = [hosts[p][:n].astype(np.float32) for p in range(k)]
             for p in range(k):
                 shm.put(srcs[p], lds[p])
         if dtype == "complexf":     # finite complex operands of magnitude ~1 (products stay finite)
@@ -993,7 +1005,7 @@ def kernel_legs(shm, reps, check):
         ck = "skipped"
         if check:
             idx = np.unique(np.random.default_rng(5).integers(0, n, 1 << 14))
-            if dtype in ("longdouble", "complexf"):
+            if rewrites:
                 samp = [np.ascontiguousarray(x[idx]) for x in lds]
             else:
                 samp = [np.ascontiguousarray(h.view(np.uint8)[:nbytes].view(shmem_reduce.NP[dtype])[idx])

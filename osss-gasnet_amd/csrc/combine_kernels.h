@@ -737,16 +737,20 @@ template <int OP, int NSRC, typename T> struct ShapeOp : Shape<NSRC, T> {
 // keeps HBM's rows open: 8 x 32 MiB -> 8 from HBM 93.5 -> 90.3 us (double
 // sum), 93.1 -> 89.8 (float sum), 93.1 -> 89.6 (double product); at 8 x 8
 // MiB within +-2 % (profiles/r06/orders_window/; the k-source fold's shape,
-// 4 vectors per lane at 8 blocks per CU, was tuned with one output). Not
-// min/max: their per-member chains run whenever a vector holds a NaN or a
-// zero, and one wave per SIMD does not hide those (bench.py's float max leg,
-// whose floats are doubles' bytes: 8 x 8 MiB 21.5 -> 26.5 us warm).
+// 4 vectors per lane at 8 blocks per CU, was tuned with one output). Min/max
+// at 8 sources: two blocks per CU -- their per-member chains run whenever a
+// vector holds a NaN or a zero, and one wave per SIMD does not hide those
+// (doubles' bytes read as floats, 8 x 8 MiB: 20.7 -> 25.2 us warm at one
+// block), two do: 8 x 8 MiB float max 20.7 -> 19.7 us warm with NaNs, 19.5
+// -> 18.4 finite, cold within 1-3 %; 8 x 32 MiB cold 102.2 -> 95.9 with NaNs
+// (profiles/r06/orders_window/minmax_*.jsonl).
 template <int OP, int NSRC, typename T> struct OrdersShape {
     static constexpr bool cplx = std::is_same<T, cplxf>::value || std::is_same<T, cplxd>::value;
     static constexpr bool sel = (OP == MI355_OP_MIN || OP == MI355_OP_MAX) && NSRC >= 5;
     using S = Shape<NSRC, T>;
     static constexpr bool alu_heavy = S::alu_heavy;
     static constexpr bool stream8 = NSRC == 8 && !S::alu_heavy && !cplx && !sel;
+    static constexpr bool sel8 = NSRC == 8 && !S::alu_heavy && sel;
     // 3-4 sources with compare-select chains or complex products: the sum's
     // shape there (one block per CU) leaves too few waves to hide their ALU
     // latency; eight blocks per CU
@@ -755,6 +759,7 @@ template <int OP, int NSRC, typename T> struct OrdersShape {
     static constexpr int unroll = cplx || stream8 ? 1 : alu4 ? 2 : sel && S::unroll > 2 ? 1 : S::unroll;
     static constexpr int blocks_per_cu = alu4      ? 8
                                          : stream8 ? 1
+                                         : sel8    ? 2
                                          : cplx    ? (S::blocks_per_cu * S::unroll < 8 ? S::blocks_per_cu * S::unroll : 8)
                                                    : S::blocks_per_cu;
     static constexpr int policy = POL_NT_LOAD;

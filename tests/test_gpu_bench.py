@@ -130,7 +130,7 @@ def test_bench_one_gpu_line():
     for name in ("fold_k2_double_sum", "fold_k8_double_sum", "rs_shard_n8_double_sum", "fold_k8_float_max",
                  "fold_k8_longlong_and", "rs_shard_n8_float_max", "rs_shard_n8_longdouble_sum",
                  "rs_shard_n8_longdouble_prod", "rs_shard_n8_complexf_prod", "rs_shard_n8_longlong_and",
-                 "rs_shard_n8_float_max_2mib", "rs_shard_n8_double_sum_8mib"):
+                 "rs_shard_n8_float_max_2mib", "rs_shard_n8_double_sum_8mib", "rs_shard_n8_float_max_nan_rich"):
         assert k[name]["check"].startswith("bit-exact"), (name, k[name])
         assert 0 < k[name]["frac"] <= 1.0 and k[name]["kernel_avg_us"] > 0, (name, k[name])
         assert 0 < k[name]["cold"]["frac"] <= 1.0 and k[name]["cold"]["footprint_MiB"] >= 2048, (name, k[name])

@@ -68,6 +68,8 @@ def main():
         xs = x.astype(np.float32) if dtype == "float" else (x * 2**31).astype(np.int32) if dtype == "int" else x
         if op == "prod":
             xs = (1.0 + x * 1e-3).astype(xs.dtype)
+        if dtype == "float" and os.environ.get("SHAPES_DATA") == "doublebytes":
+            xs = x.view(np.float32)[:n * 8]   # bench.py's kernel legs: doubles' bytes read as floats (NaNs, zeros)
         for j in range(sets):
             for q in range(8):
                 shm.put(base + j * set_bytes + q * span, xs[q * n:(q + 1) * n])

@@ -35,8 +35,9 @@ timeout -k 10 300 rocprofv3 --pmc TCC_HIT_sum TCC_MISS_sum TA_BUSY_avr --output-
 J=gpurun_out/profiles/pmc_traffic.json
 cp profiles/pmc_traffic.json "$J" 2>/dev/null || true
 # key, kernel-name substring (~ = space), minimum grid (threads) of the launches to count
-# (since round 6 the 8-source double sum runs one block per CU at every size: its two legs
-# are told apart by their bytes per pass, 256 MiB read + 256 MiB written vs 64 + 64)
+# (since round 6 the 8-source every-member folds run a grid of one or two blocks per CU at
+# every size: their legs are told apart by their bytes per pass -- double sum 256 MiB read +
+# 256 MiB written vs 64 + 64, float max 64 + 64 vs 16 + 16)
 while read -r key sub grid; do
     python3 tools/pmc_traffic.py "$OUT/fetch" "$OUT/write" "${sub//\~/ }" "$grid" "$key" "$J" > /dev/null
 done <<'EOF'
@@ -49,8 +50,9 @@ kernel_rs_shard_n8_double_sum_8mib combine_orders_vec<0,~double,~8, 1000@1:13421
 kernel_fold_k8_float_max combine_vec<6,~float,~8, 1000
 kernel_fold_k8_longlong_and combine_vec<2,~long,~8, 300000
 kernel_rs_shard_n8_longlong_and combine_vec<2,~long,~8, 1000:300000
-kernel_rs_shard_n8_float_max combine_orders_vec<6,~float,~8, 300000
-kernel_rs_shard_n8_float_max_2mib combine_orders_vec<6,~float,~8, 1000:300000
+kernel_rs_shard_n8_float_max combine_orders_vec<6,~float,~8, 1000@33554433
+kernel_rs_shard_n8_float_max_nan_rich combine_orders_vec<6,~float,~8, 1000@33554433
+kernel_rs_shard_n8_float_max_2mib combine_orders_vec<6,~float,~8, 1000@1:33554432
 kernel_rs_shard_n8_longdouble_sum combine_orders_vec<0,~x80,~8, 1000
 kernel_rs_shard_n8_longdouble_prod combine_orders_vec<1,~x80,~8, 1000
 kernel_rs_shard_n8_complexf_prod combine_orders_vec<1,~mi355::cplxf,~8, 1000
