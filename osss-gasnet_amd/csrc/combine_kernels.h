@@ -512,51 +512,6 @@ __device__ __forceinline__ void orders_vectors(const OrdersParams &p) {
     }
 }
 
-// The same loop with the next pass's loads issued before this pass's folds
-// and stores (the copy loop's pipelining, copy_segments): a wave keeps loads
-// in flight while it folds, so few waves per CU can stream.
-template <int OP, typename T, int NSRC, int UNROLL, int POL, bool ALL, bool SHIFT>
-__device__ __forceinline__ void orders_vectors_pipe(const OrdersParams &p) {
-    const uint64_t nvec = p.nvec;
-    const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
-    const u32x4 *sb[NSRC];
-#pragma unroll
-    for (int k = 0; k < NSRC; ++k) sb[k] = (const u32x4 *)p.src[k];
-    uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
-    Pack<T> x[UNROLL][NSRC];
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-        const uint64_t i = base + (uint64_t)u * kBlock;
-        if (i < nvec) {
-#pragma unroll
-            for (int k = 0; k < NSRC; ++k) x[u][k].v = ld16_src<POL, SHIFT>(sb[k], i);
-        }
-    }
-    while (base < nvec) {
-        const uint64_t next = base + step;
-        Pack<T> y[UNROLL][NSRC];
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            const uint64_t i = next + (uint64_t)u * kBlock;
-            if (i < nvec) {
-#pragma unroll
-                for (int k = 0; k < NSRC; ++k) y[u][k].v = ld16_src<POL, SHIFT>(sb[k], i);
-            }
-        }
-        __builtin_amdgcn_sched_barrier(0);   // the next pass's loads first
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) {
-            const uint64_t i = base + (uint64_t)u * kBlock;
-            if (i < nvec) orders_one<OP, T, NSRC, ALL>(p, x[u], i);
-        }
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u)
-#pragma unroll
-            for (int k = 0; k < NSRC; ++k) x[u][k] = y[u][k];
-        base = next;
-    }
-}
-
 template <int OP, typename T, int NSRC, int UNROLL, int POL, bool ALL, bool SHIFT = false>
 __global__ __launch_bounds__(kBlock) void combine_orders_vec(OrdersParams p) {
     constexpr int V = 16 / sizeof(T);

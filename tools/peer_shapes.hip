@@ -41,6 +41,52 @@ struct Variant {
 constexpr Variant kVariants[] = {PEER_SHAPES_VARIANTS};
 constexpr int kCount = sizeof(kVariants) / sizeof(kVariants[0]);
 
+// combine_kernels.h orders_vectors with the next pass's loads issued before
+// this pass's folds and stores (the copy loop's pipelining, copy_segments): a
+// wave keeps loads in flight while it folds (round 6 probe: no faster than
+// the library's loop at one block per CU, profiles/r06/orders_window/pipelined.jsonl).
+template <int OP, typename T, int NSRC, int UNROLL, int POL, bool ALL, bool SHIFT>
+__device__ __forceinline__ void orders_vectors_pipe(const OrdersParams &p) {
+    const uint64_t nvec = p.nvec;
+    const uint64_t step = (uint64_t)gridDim.x * kBlock * UNROLL;
+    const u32x4 *sb[NSRC];
+#pragma unroll
+    for (int k = 0; k < NSRC; ++k) sb[k] = (const u32x4 *)p.src[k];
+    uint64_t base = (uint64_t)blockIdx.x * kBlock * UNROLL + threadIdx.x;
+    Pack<T> x[UNROLL][NSRC];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+        const uint64_t i = base + (uint64_t)u * kBlock;
+        if (i < nvec) {
+#pragma unroll
+            for (int k = 0; k < NSRC; ++k) x[u][k].v = ld16_src<POL, SHIFT>(sb[k], i);
+        }
+    }
+    while (base < nvec) {
+        const uint64_t next = base + step;
+        Pack<T> y[UNROLL][NSRC];
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = next + (uint64_t)u * kBlock;
+            if (i < nvec) {
+#pragma unroll
+                for (int k = 0; k < NSRC; ++k) y[u][k].v = ld16_src<POL, SHIFT>(sb[k], i);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);   // the next pass's loads first
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) {
+            const uint64_t i = base + (uint64_t)u * kBlock;
+            if (i < nvec) orders_one<OP, T, NSRC, ALL>(p, x[u], i);
+        }
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u)
+#pragma unroll
+            for (int k = 0; k < NSRC; ++k) x[u][k] = y[u][k];
+        base = next;
+    }
+}
+
 template <int OP, typename T, int NSRC, int U>
 __global__ __launch_bounds__(kBlock) void orders_pipe_kernel(OrdersParams p) {
     orders_vectors_pipe<OP, T, NSRC, U, POL_NT_LOAD, true, false>(p);
